@@ -1,0 +1,189 @@
+/*
+ * aigar.h -- C-ABI of the MI355X agar.io environment stepper (libaigar_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path.  The
+ * reference has no FFI: its boundary is the Python object API of
+ * src/model/{field,model,player,cell,bot}.py.  Each entry point below names the
+ * reference call it replaces; the Python facade in aigar_amd/ binds them with
+ * ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every call returns int: 0 = OK, < 0 = error; aigar_last_error() gives the
+ *    message (thread-local).  No C++ exception crosses the ABI.
+ *  - One handle = one HIP device + one HIP stream.  Calls on a handle are
+ *    serialised by the caller.  Handles on different devices may run
+ *    concurrently (one process per GPU).
+ *  - A handle owns n_arenas independent arenas ("fields") of bots_per_arena
+ *    players each; arrays that span all arenas are arena-major:
+ *    index = arena * bots_per_arena + player.
+ *  - on_device = 0: caller passes host pointers (copied during the call);
+ *    on_device = 1: device pointers on the handle's stream (e.g. torch tensors
+ *    via data_ptr(); adopt torch's stream with aigar_set_stream()).
+ *  - All state is fp64, like the reference (Python floats / numpy float64).
+ */
+#ifndef AIGAR_H
+#define AIGAR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIGAR_ABI_VERSION 1
+
+/* random number stream of the world (spawns, explosion angles) */
+#define AIGAR_RNG_PHILOX 0   /* Philox4x64-10 keyed by (seed, site, index): device + oracle */
+#define AIGAR_RNG_MT19937 1  /* numpy legacy MT19937 stream, reference-exact: oracle only */
+
+/* observation channels, in the reference's stacking order (bot.py:459-495) */
+#define AIGAR_OBS_PELLET     0x001u  /* PELLET_GRID: pellet mass sum      */
+#define AIGAR_OBS_SELF       0x002u  /* SELF_GRID: biggest own cell mass  */
+#define AIGAR_OBS_WALL       0x004u  /* WALL_GRID: wall fraction (3 dp)   */
+#define AIGAR_OBS_ENEMY      0x008u  /* ENEMY_GRID: biggest enemy mass    */
+#define AIGAR_OBS_ALL        0x010u  /* ALL_PLAYER_GRID                   */
+#define AIGAR_OBS_VIRUS      0x020u  /* VIRUS_GRID                        */
+#define AIGAR_OBS_SELF_SLF   0x040u  /* SELF_GRID_SLF  (second-last frame)*/
+#define AIGAR_OBS_SELF_LF    0x080u  /* SELF_GRID_LF   (last frame)       */
+#define AIGAR_OBS_ENEMY_SLF  0x100u  /* ENEMY_GRID_SLF                    */
+#define AIGAR_OBS_ENEMY_LF   0x200u  /* ENEMY_GRID_LF                     */
+/* extra inputs, in getAdditionalFeatures order (bot.py:302-323) */
+#define AIGAR_EX_LAST_FOV    0x01u
+#define AIGAR_EX_FOV         0x02u
+#define AIGAR_EX_MASS        0x04u
+#define AIGAR_EX_LAST_ACT    0x08u
+#define AIGAR_EX_2LAST_ACT   0x10u
+
+/* event codes (tick-ordered the way the reference performs them) */
+#define AIGAR_EV_MERGE           1  /* (bigger seq, smaller seq)     field.py:372  */
+#define AIGAR_EV_VIRUS_EAT_BLOB  2  /* (virus seq, blob seq)         field.py:316  */
+#define AIGAR_EV_VIRUS_SPLIT     3  /* (virus seq, new virus seq)    field.py:318  */
+#define AIGAR_EV_CELL_EAT_VIRUS  4  /* (cell seq, virus seq)         field.py:333  */
+#define AIGAR_EV_EXPLODE         5  /* (cell seq, n new cells)       field.py:350  */
+#define AIGAR_EV_CELL_EAT_PELLET 6  /* (cell seq, pellet seq)        field.py:327  */
+#define AIGAR_EV_CELL_EAT_BLOB   7  /* (cell seq, blob seq)          field.py:330  */
+#define AIGAR_EV_CELL_EAT_CELL   8  /* (eater seq, eaten seq)        field.py:346  */
+#define AIGAR_EV_PLAYER_DEATH    9  /* (player index, last cell seq) field.py:386  */
+#define AIGAR_EV_RESPAWN        10  /* (player index, new cell seq)  field.py:277  */
+
+#define AIGAR_FLAG_EVENTS 0x1       /* record the event log of each step */
+
+typedef struct aigar_handle aigar_handle;
+
+typedef struct aigar_config {
+  int32_t n_arenas;        /* independent fields per handle (batched-env mode)        */
+  int32_t bots_per_arena;  /* players per field                                       */
+  int32_t field_size;      /* 0 -> int(75 * sqrt(bots)) (field.py:58)                 */
+  int32_t virus_enabled;   /* Field(virusEnabled) (field.py:30, VIRUS_SPAWN)          */
+  double max_pellets;      /* < 0 -> size*size*0.015 (field.py:65, parameters.py:16)  */
+  double max_viruses;      /* < 0 -> size*size*5e-5 (field.py:66, parameters.py:17)   */
+  int32_t grid_squares;    /* GRID_SQUARES_PER_FOV (networkParameters.py:97); 0 -> 11 */
+  uint32_t obs_channels;   /* AIGAR_OBS_* mask (networkParameters.py:76-96)           */
+  uint32_t obs_extras;     /* AIGAR_EX_* mask (networkParameters.py:91-95)            */
+  int32_t rng_mode;        /* AIGAR_RNG_*                                             */
+  int32_t device;          /* HIP device ordinal                                      */
+  int32_t pellet_cap;      /* 0 -> max_pellets + blob_cap + 64                        */
+  int32_t blob_cap;        /* 0 -> 4 * bots + 256                                     */
+  int32_t virus_cap;       /* 0 -> 2 * max_viruses + 64                               */
+  int32_t event_cap;       /* events kept per arena per step (0 -> 65536)             */
+  int32_t flags;           /* AIGAR_FLAG_*                                            */
+} aigar_config;
+
+/*
+ * Snapshot of one arena, the unit of parity.  Record layouts (row-major):
+ *   players_f [n_players][2]  command point x, y          (player.py:99-102)
+ *   players_i [n_players][5]  alive, respawnTime, doSplit, doEject, #cells
+ *   cells_f   [n_cells][9]    x y mass radius vx vy svx svy mergeTime (cell.py:21-45)
+ *   cells_i   [n_cells][4]    owner, splitVelocityCounter, seq, in_player_hash
+ *             cells are grouped by owner in player order, each group in the
+ *             player's cell-list order
+ *   pellets_f [n_pellets][4]  x y mass radius, sorted by seq
+ *   pellets_seq [n_pellets]
+ *   blobs_f   [n_blobs][8]    x y mass radius vx vy svx svy (list order)
+ *   blobs_i   [n_blobs][3]    svc, seq, ejecter cell seq
+ *   viruses_f [n_viruses][8]  as blobs
+ *   viruses_i [n_viruses][3]  svc, seq, in_virus_hash
+ *   dead      [n_dead]        deadPlayers list (player indices, in order)
+ * seq = creation sequence number of the Cell object (canonical order).
+ * aigar_get_state: with NULL arrays only the counts are filled; otherwise the
+ * n_* fields give the capacities of the caller's arrays on input.
+ */
+typedef struct aigar_state {
+  int32_t n_players, field_size, virus_enabled, rng_mode;
+  int64_t seq_next, tick;
+  double max_pellets, max_viruses;
+  uint64_t philox_key[2];
+  uint64_t ctr_pellet, ctr_virus;
+  uint32_t mt_key[624];
+  int32_t mt_pos;
+  int32_t n_cells, n_pellets, n_blobs, n_viruses, n_dead;
+  double *players_f;
+  int64_t *players_i;
+  double *cells_f;
+  int64_t *cells_i;
+  double *pellets_f;
+  int64_t *pellets_seq;
+  double *blobs_f;
+  int64_t *blobs_i;
+  double *viruses_f;
+  int64_t *viruses_i;
+  int64_t *dead;
+} aigar_state;
+
+const char *aigar_last_error(void);
+int aigar_abi_version(void);
+
+/* Field(virusEnabled) + Model bookkeeping: allocate all device buffers.
+ * replaces model.py:51-73 / field.py:30-46 */
+int aigar_create(const aigar_config *cfg, aigar_handle **out);
+int aigar_destroy(aigar_handle *h);
+
+/* Field.initialize()/Field.reset(): spawn every player, pellets, viruses.
+ * replaces field.py:57-83 (model.py:90-98) */
+int aigar_reset(aigar_handle *h, uint64_t seed);
+
+/* Player.setCommands(x, y, split, eject) for every player: cmd[A*B][4].
+ * replaces player.py:99-102 (called from bot.py:550-577) */
+int aigar_set_commands(aigar_handle *h, const double *cmd, int on_device);
+
+/* Synthetic bot population on the device (benchmark / smoke driver): every
+ * alive player draws an action in [0,1]^2 mapped through the reference's
+ * set_command_point (bot.py:550-577) and splits/ejects with p_split/p_eject. */
+int aigar_policy_random(aigar_handle *h, double p_split, double p_eject, uint64_t seed);
+
+/* n_ticks x Field.update() with the current commands (field.py:85-92). */
+int aigar_step(aigar_handle *h, int n_ticks);
+
+/* Bot.getStateRepresentation() for every player (bot.py:272-497):
+ * out[A*B][aigar_obs_len()] (dtype 0 = float64, 1 = float32); dead players get NaN.
+ * Updates each bot's last-frame history grids like the reference does. */
+int aigar_obs_len(aigar_handle *h);
+int aigar_observe(aigar_handle *h, void *out, int dtype, int on_device);
+/* bot.currentAction / bot.lastAction used by the action extras: [A*B][4] each (may be NULL). */
+int aigar_set_actions(aigar_handle *h, const double *cur, const double *prev, int on_device);
+
+/* per-player summary [A*B][5]: alive, total mass (player.py:129), fov x, fov y, fov size
+ * (player.py:156-167). */
+int aigar_player_stats(aigar_handle *h, double *out, int on_device);
+
+/* Snapshot / restore one arena (parity harness, checkpoint/resume). */
+int aigar_get_state(aigar_handle *h, int arena, aigar_state *st);
+int aigar_load_state(aigar_handle *h, int arena, const aigar_state *st);
+
+/* Event log of the last aigar_step (AIGAR_FLAG_EVENTS): rows of (tick, code, a, b)
+ * in reference order.  *n gets the count; returns < 0 if cap is too small. */
+int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int cap, int *n);
+
+/* Stream control. */
+int aigar_set_stream(aigar_handle *h, void *hip_stream);
+int aigar_sync(aigar_handle *h);
+
+/* Timing support for bench.py: HIP-event time of the named kernel's launches
+ * on the handle's stream during the last step (ms total, launch count). */
+int aigar_profile(aigar_handle *h, int enable);
+int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AIGAR_H */

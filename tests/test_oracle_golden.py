@@ -1,0 +1,76 @@
+"""Pin the CPU oracle (oracle/oracle.c) against the reference itself.
+
+The fixtures under tests/golden were produced by running the reference
+src/model (tools/golden/gen_golden.py, canonical-order shim) in this container.
+The oracle in MT19937 mode must reproduce them BIT-EXACTLY: every tick's event
+log (eat / merge / split / explosion / death / respawn, in order), the full
+world snapshot at each checkpoint, the numpy MT19937 stream position (i.e. the
+exact number and order of random draws) and every bot's grid observation.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import Oracle, golden_state, make_config
+
+SCENARIOS = ["c1_greedy", "greedy16", "greedy16_virus_split", "stress_virus", "crowd32", "merge8",
+             "virus_feed", "random64"]
+
+
+def _same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.shape != b.shape:
+        return False
+    if a.dtype.kind == "f":
+        return bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+    return bool(np.array_equal(a, b))
+
+
+def oracle_for(z):
+    cfg = make_config(bots=int(z["n_players"]), field_size=int(z["size"]), virus=bool(z["virus_enabled"]),
+                      max_pellets=float(z["max_pellets"]), max_viruses=float(z["max_viruses"]),
+                      channels=int(z["obs_channels"]), extras=int(z["obs_extras"]), rng_mode=_abi.RNG_MT19937)
+    return Oracle(cfg)
+
+
+@pytest.mark.parametrize("name", SCENARIOS)
+def test_oracle_reproduces_reference(name, golden_dir):
+    z = np.load(os.path.join(golden_dir, name + ".npz"))
+    o = oracle_for(z)
+    o.load_state(golden_state(z, "init"))
+    has_obs = "obs/init" in z.files
+    if has_obs:
+        assert _same(o.observe(), z["obs/init"]), "initial observation"
+    T = int(z["ticks"])
+    cks = set(int(t) for t in z["ck_ticks"])
+    ev, off = z["events"], z["events_off"]
+    for t in range(T):
+        o.set_commands(z["cmds"][t])
+        o.set_mt(z["mt_keys"][t], z["mt_pos"][t])  # bots drew from the same stream before field.update()
+        o.step(1)
+        assert _same(o.events()[:, 1:], ev[off[t]:off[t + 1]]), "event log differs at tick %d" % t
+        di = z["digest_i"][t]
+        obs = o.observe() if has_obs else None
+        if (t + 1) in cks:
+            st = o.get_state()
+            pre = "ck%d/" % (t + 1)
+            for k in _abi.LAYOUT:
+                assert _same(st[k], z[pre + k]), "%s differs at tick %d" % (k, t + 1)
+            assert np.array_equal(st["mt_key"], z[pre + "mt_key"]) and st["mt_pos"] == z[pre + "mt_pos"]
+            assert st["seq_next"] == z[pre + "seq_next"]
+            if has_obs:
+                assert _same(obs, z["obs/ck%d" % (t + 1)]), "observation differs at tick %d" % (t + 1)
+        else:
+            st = o.get_state()
+            assert [st["n_cells"], st["n_pellets"], st["n_blobs"], st["n_viruses"], st["n_dead"]] == list(di)
+    o.close()
+
+
+def test_golden_covers_every_event_kind(golden_dir):
+    seen = set()
+    for name in SCENARIOS:
+        z = np.load(os.path.join(golden_dir, name + ".npz"))
+        seen |= set(np.unique(z["events"][:, 0]).tolist()) if len(z["events"]) else set()
+    assert seen == set(range(1, 11))

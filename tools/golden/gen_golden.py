@@ -1,0 +1,519 @@
+#!/usr/bin/env python3
+"""Golden-vector generator for the agar.io tick + grid observation.
+
+CONTAINER-ONLY TEST INFRASTRUCTURE.  This script imports the read-only
+reference (`/root/reference/src/model`) and runs it; it never runs on the GPU
+box and nothing in the product imports it.  It writes `tests/golden/*.npz`
+fixtures that hold numbers only (states, commands, RNG states, event logs,
+observations) -- no reference source.
+
+Shims (all live here; reference files are untouched), see SURVEY.md §8c:
+  * a stub `pygame` module (`model/rgbGenerator.py:1-3` imports it; unused
+    unless CNN_P_REPR);
+  * canonical order: every `Cell.__init__` is stamped with a creation
+    sequence number and `spatialHashTable.getObjectsFromBuckets`
+    (`spatialHashTable.py:38-43`) returns a seq-sorted list instead of a set
+    (CPython set order follows object addresses -> non-deterministic);
+  * observers wrapping `Field.eatCell/eatPlayerCell/mergeCells/...` that append
+    to an event log (they call the original method unchanged).
+
+Determinism: `Field.__init__` reseeds numpy from time/pid (`field.py:32`), so
+we reseed `numpy.random` immediately after `Model(...)`.
+
+Usage:  python tools/golden/gen_golden.py [--out tests/golden] [--only NAME]
+"""
+import argparse
+import math
+import os
+import random
+import sys
+import tracemalloc
+import types
+
+import numpy as np
+
+REF_SRC = "/root/reference/src"
+
+# event codes (shared with oracle/ and the HIP library, see include/aigar.h)
+EV_MERGE, EV_VIRUS_EAT_BLOB, EV_VIRUS_SPLIT, EV_CELL_EAT_VIRUS, EV_EXPLODE = 1, 2, 3, 4, 5
+EV_CELL_EAT_PELLET, EV_CELL_EAT_BLOB, EV_CELL_EAT_CELL, EV_PLAYER_DEATH, EV_RESPAWN = 6, 7, 8, 9, 10
+
+
+def import_reference():
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    pg = types.ModuleType("pygame")
+    pg.gfxdraw = types.ModuleType("pygame.gfxdraw")
+    sys.modules.setdefault("pygame", pg)
+    sys.modules.setdefault("pygame.gfxdraw", pg.gfxdraw)
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    import model.cell as mcell
+    import model.field as mfield
+    import model.spatialHashTable as msht
+    import model.model as mmodel
+    import model.bot as mbot
+    import model.player as mplayer
+    import model.networkParameters as mnp
+    return types.SimpleNamespace(cell=mcell, field=mfield, sht=msht, model=mmodel,
+                                 bot=mbot, player=mplayer, np=mnp)
+
+
+class Recorder:
+    def __init__(self):
+        self.seq = 0
+        self.events = []
+        self.field = None
+
+
+def install_shims(ref, rec):
+    Cell = ref.cell.Cell
+    orig_init = Cell.__init__
+
+    def init(self, *a, **k):
+        self._seq = rec.seq
+        rec.seq += 1
+        orig_init(self, *a, **k)
+    Cell.__init__ = init
+
+    def get_objects_from_buckets(self, cellIds):
+        s = set()
+        for cid in cellIds:
+            for c in self.buckets[cid]:
+                s.add(c)
+        return sorted(s, key=lambda c: c._seq)
+    ref.sht.spatialHashTable.getObjectsFromBuckets = get_objects_from_buckets
+
+    F = ref.field.Field
+    o_eatCell, o_eatPC, o_merge = F.eatCell, F.eatPlayerCell, F.mergeCells
+    o_del, o_vEB, o_expl, o_init_pl = F.deletePlayerCell, F.virusEatBlob, F.playerCellAteVirus, F.initializePlayer
+    o_spawnPlayers = F.spawnPlayers
+
+    def eatCell(self, eating, eh, cell, ch, lst, isVirus=None):
+        if lst is self.pellets:
+            code = EV_CELL_EAT_PELLET
+        elif lst is self.viruses:
+            code = EV_CELL_EAT_VIRUS
+        elif eating.getPlayer() is None:
+            code = EV_VIRUS_EAT_BLOB
+        else:
+            code = EV_CELL_EAT_BLOB
+        rec.events.append((code, eating._seq, cell._seq))
+        return o_eatCell(self, eating, eh, cell, ch, lst, isVirus)
+
+    def eatPlayerCell(self, larger, smaller):
+        rec.events.append((EV_CELL_EAT_CELL, larger._seq, smaller._seq))
+        return o_eatPC(self, larger, smaller)
+
+    def mergeCells(self, a, b):
+        big, small = (a, b) if a.getMass() > b.getMass() else (b, a)
+        rec.events.append((EV_MERGE, big._seq, small._seq))
+        return o_merge(self, a, b)
+
+    def deletePlayerCell(self, cell):
+        r = o_del(self, cell)
+        pl = cell.getPlayer()
+        if not pl.getCells():
+            rec.events.append((EV_PLAYER_DEATH, self.players.index(pl), cell._seq))
+        return r
+
+    def virusEatBlob(self, virus, blob):
+        n0 = len(self.viruses)
+        r = o_vEB(self, virus, blob)
+        if len(self.viruses) > n0:
+            rec.events.append((EV_VIRUS_SPLIT, virus._seq, self.viruses[-1]._seq))
+        return r
+
+    def playerCellAteVirus(self, cell):
+        n_new = 16 - len(cell.getPlayer().getCells())
+        rec.events.append((EV_EXPLODE, cell._seq, n_new))
+        return o_expl(self, cell)
+
+    def spawnPlayers(self):
+        self._in_respawn = True
+        try:
+            return o_spawnPlayers(self)
+        finally:
+            self._in_respawn = False
+
+    def initializePlayer(self, player):
+        r = o_init_pl(self, player)
+        if getattr(self, "_in_respawn", False):
+            rec.events.append((EV_RESPAWN, self.players.index(player), player.getCells()[0]._seq))
+        return r
+
+    F.eatCell, F.eatPlayerCell, F.mergeCells = eatCell, eatPlayerCell, mergeCells
+    F.deletePlayerCell, F.virusEatBlob, F.playerCellAteVirus = deletePlayerCell, virusEatBlob, playerCellAteVirus
+    F.spawnPlayers, F.initializePlayer = spawnPlayers, initializePlayer
+
+
+# ---------------------------------------------------------------- params ----
+def make_params(ref, n_bots, virus, split, eject, overrides=None):
+    """Copy of networkParameters with the derived obs sizes recomputed the way
+    `networkParameters.py:74-102` does at import time."""
+    p = types.ModuleType("golden_params")
+    for k, v in vars(ref.np).items():
+        if not k.startswith("__"):
+            setattr(p, k, v)
+    p.GATHER_EXP = False
+    p.VIRUS_SPAWN = virus
+    p.ENABLE_SPLIT = split
+    p.ENABLE_EJECT = eject
+    multi = n_bots > 1
+    p.MULTIPLE_BOTS_PRESENT = multi
+    p.NORMALIZE_GRID_BY_MAX_MASS = False
+    p.PELLET_GRID = True
+    p.SELF_GRID = split or virus
+    p.SELF_GRID_LF = split
+    p.SELF_GRID_SLF = False
+    p.WALL_GRID = multi
+    p.VIRUS_GRID = virus
+    p.ENEMY_GRID = multi
+    p.ENEMY_GRID_LF = split
+    p.ENEMY_GRID_SLF = False
+    p.SIZE_GRID = False
+    p.ALL_PLAYER_GRID = False
+    p.USE_FOVSIZE = True
+    p.USE_LAST_FOVSIZE = split
+    p.USE_TOTALMASS = True
+    p.USE_LAST_ACTION = split
+    p.USE_SECOND_LAST_ACTION = False
+    p.GRID_SQUARES_PER_FOV = 11
+    for k, v in (overrides or {}).items():
+        setattr(p, k, v)
+    if p.ALL_PLAYER_GRID:
+        p.SELF_GRID = False
+        p.ENEMY_GRID = False
+    p.NUM_OF_GRIDS = (p.PELLET_GRID + p.SELF_GRID + p.WALL_GRID + p.VIRUS_GRID + p.ENEMY_GRID
+                      + p.SIZE_GRID + p.SELF_GRID_LF + p.SELF_GRID_SLF + p.ENEMY_GRID_LF
+                      + p.ENEMY_GRID_SLF + p.ALL_PLAYER_GRID)
+    p.EXTRA_INPUT = (p.USE_FOVSIZE + p.USE_TOTALMASS + p.USE_LAST_ACTION * 4
+                     + p.USE_SECOND_LAST_ACTION * 4 + p.USE_LAST_FOVSIZE)
+    p.STATE_REPR_LEN = p.GRID_SQUARES_PER_FOV ** 2 * p.NUM_OF_GRIDS + p.EXTRA_INPUT
+    return p
+
+
+# obs channel bits (canonical order, bot.py:459-495) and extra bits (bot.py:302-323)
+OBS_PELLET, OBS_SELF, OBS_WALL, OBS_ENEMY, OBS_ALL, OBS_VIRUS = 1, 2, 4, 8, 16, 32
+OBS_SELF_SLF, OBS_SELF_LF, OBS_ENEMY_SLF, OBS_ENEMY_LF = 64, 128, 256, 512
+EX_LAST_FOV, EX_FOV, EX_MASS, EX_LAST_ACT, EX_2LAST_ACT = 1, 2, 4, 8, 16
+
+
+def obs_masks(p):
+    ch = 0
+    for flag, bit in ((p.PELLET_GRID, OBS_PELLET), (p.SELF_GRID, OBS_SELF), (p.WALL_GRID, OBS_WALL),
+                      (p.ENEMY_GRID, OBS_ENEMY), (p.ALL_PLAYER_GRID, OBS_ALL), (p.VIRUS_GRID, OBS_VIRUS),
+                      (p.SELF_GRID_SLF, OBS_SELF_SLF), (p.SELF_GRID_LF, OBS_SELF_LF),
+                      (p.ENEMY_GRID_SLF, OBS_ENEMY_SLF), (p.ENEMY_GRID_LF, OBS_ENEMY_LF)):
+        if flag:
+            ch |= bit
+    ex = 0
+    for flag, bit in ((p.USE_LAST_FOVSIZE, EX_LAST_FOV), (p.USE_FOVSIZE, EX_FOV), (p.USE_TOTALMASS, EX_MASS),
+                      (p.USE_LAST_ACTION, EX_LAST_ACT), (p.USE_SECOND_LAST_ACTION, EX_2LAST_ACT)):
+        if flag:
+            ex |= bit
+    return ch, ex
+
+
+# -------------------------------------------------------------- snapshot ----
+def f(v):
+    return float(v)
+
+
+def snapshot(field):
+    players = field.players
+    hashed_cells = {id(o) for b in field.playerHashTable.buckets.values() for o in b}
+    hashed_vir = {id(o) for b in field.virusHashTable.buckets.values() for o in b}
+    pl_f = np.array([[f(p.commandPoint[0]), f(p.commandPoint[1])] for p in players], np.float64).reshape(-1, 2)
+    pl_i = np.array([[int(p.isAlive), int(p.respawnTime), int(bool(p.doSplit)), int(bool(p.doEject)),
+                      len(p.cells)] for p in players], np.int64).reshape(-1, 5)
+    cf, ci = [], []
+    for pi, p in enumerate(players):
+        for c in p.cells:
+            cf.append([f(c.x), f(c.y), f(c.mass), f(c.radius), f(c.velocity[0]), f(c.velocity[1]),
+                       f(c.splitVelocity[0]), f(c.splitVelocity[1]), f(c.mergeTime)])
+            ci.append([pi, int(c.splitVelocityCounter), c._seq, int(id(c) in hashed_cells)])
+    pel = sorted(field.pellets, key=lambda c: c._seq)
+    pf = [[f(c.x), f(c.y), f(c.mass), f(c.radius)] for c in pel]
+    ps = [c._seq for c in pel]
+    bf, bi = [], []
+    for c in field.blobs:
+        bf.append([f(c.x), f(c.y), f(c.mass), f(c.radius), f(c.velocity[0]), f(c.velocity[1]),
+                   f(c.splitVelocity[0]), f(c.splitVelocity[1])])
+        bi.append([int(c.splitVelocityCounter), c._seq, c.ejecterCell._seq if c.ejecterCell is not None else -1])
+    vf, vi = [], []
+    for c in field.viruses:
+        vf.append([f(c.x), f(c.y), f(c.mass), f(c.radius), f(c.velocity[0]), f(c.velocity[1]),
+                   f(c.splitVelocity[0]), f(c.splitVelocity[1])])
+        vi.append([int(c.splitVelocityCounter), c._seq, int(id(c) in hashed_vir)])
+    dead = [players.index(p) for p in field.deadPlayers]
+    return {
+        "players_f": pl_f, "players_i": pl_i,
+        "cells_f": np.array(cf, np.float64).reshape(-1, 9), "cells_i": np.array(ci, np.int64).reshape(-1, 4),
+        "pellets_f": np.array(pf, np.float64).reshape(-1, 4), "pellets_seq": np.array(ps, np.int64),
+        "blobs_f": np.array(bf, np.float64).reshape(-1, 8), "blobs_i": np.array(bi, np.int64).reshape(-1, 3),
+        "viruses_f": np.array(vf, np.float64).reshape(-1, 8), "viruses_i": np.array(vi, np.int64).reshape(-1, 3),
+        "dead": np.array(dead, np.int64),
+    }
+
+
+def mt_state():
+    st = np.random.get_state(legacy=True)
+    assert st[0] == "MT19937"
+    return np.asarray(st[1], np.uint32).copy(), int(st[2])
+
+
+def digest(field):
+    """Cheap per-tick fingerprint (exact float sums in a fixed order)."""
+    s = snapshot(field)
+    out = [len(s["cells_f"]), len(s["pellets_f"]), len(s["blobs_f"]), len(s["viruses_f"]), len(s["dead"])]
+    vals = [float(np.sum(s[k][:, :3])) if len(s[k]) else 0.0 for k in ("cells_f", "pellets_f", "blobs_f", "viruses_f")]
+    return out, vals
+
+
+# ------------------------------------------------------------- scenarios ----
+SCENARIOS = {
+    # C1: BASELINE.json configs[0] -- 1 greedy bot, 1000x1000, 100 pellets
+    "c1_greedy": dict(n=1, driver="greedy", size_per_player=1000, max_pellets=100, virus=False,
+                      split=False, eject=False, ticks=1000, ck_every=100, obs=True, seed=0),
+    # 16 greedy bots, default size 75*sqrt(16)=300, density 0.015 (1350 pellets)
+    "greedy16": dict(n=16, driver="greedy", virus=False, split=False, eject=False, ticks=200,
+                     ck_every=40, obs=True, seed=1),
+    # greedy with viruses + greedy split (the C3 flavour, small)
+    "greedy16_virus_split": dict(n=16, driver="greedy", virus=True, virus_density=4e-4, split=True,
+                                 eject=False, greedy_split=True, ticks=200, ck_every=40, obs=True, seed=2),
+    # scripted stress: viruses, split, eject, big cells -> explosions, blobs, eating, deaths, respawns
+    "stress_virus": dict(n=16, driver="scripted", virus=True, virus_density=5e-4, split=True, eject=True,
+                         p_split=0.06, p_eject=0.08, ticks=260, ck_every=20, obs=True, seed=3,
+                         boost=[(0, 600.0), (1, 400.0), (2, 260.0), (3, 180.0), (4, 150.0), (5, 90.0)],
+                         obs_over=dict(SELF_GRID_SLF=True, ENEMY_GRID_SLF=True, USE_SECOND_LAST_ACTION=True)),
+    # crowded field: many collisions, deaths and respawns with hash-occupancy probing
+    "crowd32": dict(n=32, driver="scripted", size_per_player=30, density=0.015, virus=False, split=True,
+                    eject=True, p_split=0.03, p_eject=0.03, ticks=220, ck_every=20, obs=True, seed=4,
+                    center_bias=0.7, boost=[(i, 20.0 + 9.0 * i) for i in range(32)]),
+    # merges early: players start with several cells whose merge timers are ~0
+    "merge8": dict(n=8, driver="scripted", virus=False, split=True, eject=False, p_split=0.02, p_eject=0.0,
+                   ticks=120, ck_every=20, obs=True, seed=5, multi_cells=True),
+    # virus feeding: a big player ejects toward viruses until they split (virus-blob path)
+    "virus_feed": dict(n=4, driver="feed", virus=True, virus_density=4e-4, split=False, eject=True,
+                       ticks=160, ck_every=20, obs=True, seed=6),
+    # 64 reference Random bots (split + eject enabled via their own policy)
+    "random64": dict(n=64, driver="random", size_per_player=75, density=0.0083, virus=False, split=True,
+                     eject=True, ticks=120, ck_every=30, obs=False, seed=7),
+}
+
+
+def scripted_commands(field, rng, sc):
+    size = field.size
+    cmds = []
+    for p in field.players:
+        if rng.random() < sc.get("center_bias", 0.3):
+            x, y = size / 2 + rng.normal() * size / 8, size / 2 + rng.normal() * size / 8
+        else:
+            x, y = rng.random() * size, rng.random() * size
+        s = rng.random() < sc.get("p_split", 0.0)
+        e = rng.random() < sc.get("p_eject", 0.0)
+        cmds.append((x, y, s, e))
+    return cmds
+
+
+def feed_commands(field, rng, tick):
+    """Player 0 (huge) sits near virus 0 and ejects toward it every tick."""
+    cmds = []
+    for i, p in enumerate(field.players):
+        if i == 0 and field.viruses:
+            v = field.viruses[0]
+            cmds.append((float(v.x), float(v.y), False, True))
+        else:
+            cmds.append((rng.random() * field.size, rng.random() * field.size, False, False))
+    return cmds
+
+
+def run_scenario(ref, rec, name, sc):
+    n = sc["n"]
+    mf = ref.field
+    # world size / densities via module globals of model.field
+    mf.SIZE_INCREASE_PER_PLAYER = sc.get("size_per_player", 75)
+    size = int(mf.SIZE_INCREASE_PER_PLAYER * math.sqrt(n))
+    if "max_pellets" in sc:
+        mf.MAX_COLLECTIBLE_DENSITY = sc["max_pellets"] / (size * size)
+    else:
+        mf.MAX_COLLECTIBLE_DENSITY = sc.get("density", 0.015)
+    mf.MAX_VIRUS_DENSITY = sc.get("virus_density", 0.00005)
+
+    params = make_params(ref, n, sc["virus"], sc["split"], sc["eject"], sc.get("obs_over"))
+    params.ENABLE_GREEDY_SPLIT = sc.get("greedy_split", False)
+    model = ref.model.Model(False, False, params)
+    tracemalloc.stop()
+    np.random.seed(sc["seed"])
+    random.seed(sc["seed"])
+    rec.seq = 0  # creation sequence restarts per scenario (only relative order matters)
+    driver = sc["driver"]
+    if driver in ("greedy", "random"):
+        for _ in range(n):
+            model.createBot("Greedy" if driver == "greedy" else "Random", None, params)
+    else:
+        for i in range(n):
+            model.createPlayer("P%d" % i)
+    model.initialize()
+    field = model.field
+    rng = np.random.default_rng(1000 + sc["seed"])  # scenario driver RNG (not the field's MT stream)
+
+    # stress mutations before tick 1 (hash rebuild at tick 1 picks them up)
+    for pi, m in sc.get("boost", []):
+        field.players[pi].cells[0].setMass(m)
+    if sc.get("multi_cells"):
+        for pi, p in enumerate(field.players):
+            c0 = p.cells[0]
+            c0.setMass(120.0 + 10 * pi)
+            for k in range(3):
+                ang = 2 * math.pi * k / 3
+                c = ref.cell.Cell(min(field.size, max(0, c0.x + 6 * math.cos(ang))),
+                                  min(field.size, max(0, c0.y + 6 * math.sin(ang))), 40.0 + 5 * k, p)
+                c.mergeTime = float(k)
+                p.addCell(c)
+    if driver == "feed":
+        v = field.viruses[0]
+        big = field.players[0].cells[0]
+        big.setMass(3000.0)
+        big.setPos([min(field.size, float(v.x) + 45.0), float(v.y)])
+
+    obs_bots = []
+    if sc.get("obs"):
+        for p in field.players:
+            obs_bots.append(ref.bot.Bot(p, field, "NN", None, params))
+    ch_mask, ex_mask = obs_masks(params)
+
+    out = {
+        "n_players": np.int64(n), "size": np.int64(field.size),
+        "max_pellets": np.float64(field.maxCollectibleCount), "max_viruses": np.float64(field.maxVirusCount),
+        "virus_enabled": np.int64(int(field.virusEnabled)),
+        "obs_channels": np.int64(ch_mask), "obs_extras": np.int64(ex_mask),
+        "obs_len": np.int64(params.STATE_REPR_LEN), "obs_grids": np.int64(params.NUM_OF_GRIDS),
+        "ticks": np.int64(sc["ticks"]),
+    }
+    for k, v in snapshot(field).items():
+        out["init/" + k] = v
+    out["init/seq_next"] = np.int64(rec.seq)
+    keys, pos = mt_state()
+    out["init/mt_key"], out["init/mt_pos"] = keys, np.int64(pos)
+
+    T = sc["ticks"]
+    cmds_all = np.zeros((T, n, 4), np.float64)
+    mt_keys = np.zeros((T, 624), np.uint32)
+    mt_pos = np.zeros(T, np.int64)
+    ev_rows, ev_off = [], [0]
+    dig_i, dig_f = [], []
+    ck_ticks = []
+
+    def record_obs(tag):
+        L = params.STATE_REPR_LEN
+        arr = np.full((n, L), np.nan)
+        for i, b in enumerate(obs_bots):
+            s = b.getStateRepresentation()
+            if s is not None:
+                arr[i] = np.asarray(s, np.float64).reshape(-1)
+        return arr
+
+    if obs_bots:
+        out["obs/init"] = record_obs("init")
+    for t in range(T):
+        if driver in ("greedy", "random"):
+            model.takeBotActions()
+        else:
+            cmds = scripted_commands(field, rng, sc) if driver == "scripted" else feed_commands(field, rng, t)
+            for p, (x, y, s, e) in zip(field.players, cmds):
+                p.setCommands(x, y, s, e)
+        for i, p in enumerate(field.players):
+            cmds_all[t, i] = (f(p.commandPoint[0]), f(p.commandPoint[1]), float(bool(p.doSplit)), float(bool(p.doEject)))
+        mt_keys[t], mt_pos[t] = mt_state()
+        rec.events = []
+        field.update()
+        ev_rows.extend(rec.events)
+        ev_off.append(len(ev_rows))
+        di, dfv = digest(field)
+        dig_i.append(di)
+        dig_f.append(dfv)
+        obs_now = record_obs("t") if obs_bots else None
+        if (t + 1) % sc["ck_every"] == 0 or t == T - 1:
+            ck_ticks.append(t + 1)
+            for k, v in snapshot(field).items():
+                out["ck%d/%s" % (t + 1, k)] = v
+            out["ck%d/seq_next" % (t + 1)] = np.int64(rec.seq)
+            kk, pp = mt_state()
+            out["ck%d/mt_key" % (t + 1)], out["ck%d/mt_pos" % (t + 1)] = kk, np.int64(pp)
+            if obs_now is not None:
+                out["obs/ck%d" % (t + 1)] = obs_now
+    out["cmds"] = cmds_all
+    out["mt_keys"], out["mt_pos"] = mt_keys, mt_pos
+    out["events"] = np.array(ev_rows, np.int64).reshape(-1, 3)
+    out["events_off"] = np.array(ev_off, np.int64)
+    out["digest_i"] = np.array(dig_i, np.int64)
+    out["digest_f"] = np.array(dig_f, np.float64)
+    out["ck_ticks"] = np.array(ck_ticks, np.int64)
+    ev = out["events"]
+    counts = {c: int(np.sum(ev[:, 0] == c)) for c in range(1, 11)} if len(ev) else {}
+    return out, counts
+
+
+def rng_kats():
+    """Known-answer vectors for the numpy legacy MT19937 draws the tick uses
+    (randint with int and float bounds, random())."""
+    rs = np.random.RandomState(12345)
+    st = rs.get_state(legacy=True)
+    spec = [(0, 1000), (0, 50), (50, 200), (0, 360), (-7.18, 7.18), (101.784, 118.216), (-18.2, -1.7),
+            (0, 57600), (0, 3), (9950, 10000), (0, 1 << 31)]
+    seq_i, seq_lo, seq_hi = [], [], []
+    for _ in range(400):
+        for lo, hi in spec:
+            seq_lo.append(lo)
+            seq_hi.append(hi)
+            seq_i.append(int(rs.randint(lo, hi)))
+    randoms = np.array([rs.random() for _ in range(200)], np.float64)
+    end = rs.get_state(legacy=True)
+    return {"mt_key": np.asarray(st[1], np.uint32), "mt_pos": np.int64(st[2]),
+            "lo": np.array(seq_lo, np.float64), "hi": np.array(seq_hi, np.float64),
+            "val": np.array(seq_i, np.int64), "random": randoms,
+            "end_key": np.asarray(end[1], np.uint32), "end_pos": np.int64(end[2])}
+
+
+def numeric_kats():
+    """numpy pairwise sum, Python round(x, 3), deg2rad, pow as used by the path."""
+    rng = np.random.default_rng(99)
+    sums_in, sums_off, sums_out = [], [0], []
+    for n in range(1, 40):
+        for _ in range(20):
+            a = list(rng.random(n) * rng.choice([1.0, 100.0, 5000.0]))
+            sums_in.extend(a)
+            sums_off.append(len(sums_in))
+            sums_out.append(float(np.sum(a)))
+    rv = np.concatenate([rng.random(4000) * 2 - 0.5, np.arange(-5, 2005) / 2000.0,
+                         np.array([-2e-16, 2e-16, 0.0005, 0.0015, 0.0025, 1 - 1e-16])])
+    rounded = np.array([round(float(v), 3) for v in rv], np.float64)
+    return {"sum_in": np.array(sums_in), "sum_off": np.array(sums_off, np.int64), "sum_out": np.array(sums_out),
+            "round_in": rv, "round_out": rounded,
+            "deg2rad": np.array([np.deg2rad(d) for d in range(360)], np.float64)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "..", "tests", "golden"))
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    ref = import_reference()
+    rec = Recorder()
+    install_shims(ref, rec)
+    if args.only in (None, "kats"):
+        np.savez_compressed(os.path.join(args.out, "kat_rng.npz"), **rng_kats())
+        np.savez_compressed(os.path.join(args.out, "kat_numeric.npz"), **numeric_kats())
+    for name, sc in SCENARIOS.items():
+        if args.only not in (None, name):
+            continue
+        out, counts = run_scenario(ref, rec, name, sc)
+        np.savez_compressed(os.path.join(args.out, name + ".npz"), **out)
+        print(name, "events:", counts, "final counts:", out["digest_i"][-1].tolist(), flush=True)
+
+
+if __name__ == "__main__":
+    main()
