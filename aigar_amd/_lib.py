@@ -1,0 +1,181 @@
+"""ctypes binding of libaigar_hip.so (include/aigar.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded
+this module raises, so a GPU run can never silently take another path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(HERE, "libaigar_hip.so")
+
+_lib = None
+
+
+def load(build_if_missing=False):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(SO_PATH):
+        if build_if_missing:
+            from . import _build
+            _build.build()
+        else:
+            raise RuntimeError("libaigar_hip.so not found at %s: build it with `python -m aigar_amd._build` "
+                               "(hipcc --offload-arch=gfx950)" % SO_PATH)
+    L = C.CDLL(SO_PATH)
+    vp, i32, u64, dp = C.c_void_p, C.c_int, C.c_uint64, C.POINTER(C.c_double)
+    L.aigar_last_error.restype = C.c_char_p
+    L.aigar_abi_version.restype = i32
+    sig = {
+        "aigar_create": [C.POINTER(_abi.Config), C.POINTER(vp)],
+        "aigar_destroy": [vp],
+        "aigar_reset": [vp, u64],
+        "aigar_set_commands": [vp, vp, i32],
+        "aigar_policy_random": [vp, C.c_double, C.c_double, u64],
+        "aigar_step": [vp, i32],
+        "aigar_obs_len": [vp],
+        "aigar_observe": [vp, vp, i32, i32],
+        "aigar_set_actions": [vp, vp, vp, i32],
+        "aigar_player_stats": [vp, vp, i32],
+        "aigar_get_state": [vp, i32, C.POINTER(_abi.State)],
+        "aigar_load_state": [vp, i32, C.POINTER(_abi.State)],
+        "aigar_get_events": [vp, i32, C.POINTER(C.c_int64), i32, C.POINTER(i32)],
+        "aigar_set_stream": [vp, vp],
+        "aigar_sync": [vp],
+        "aigar_profile": [vp, i32],
+        "aigar_kernel_time": [vp, C.c_char_p, dp, C.POINTER(i32)],
+        "aigar_selftest_pow": [dp, dp, dp, i32],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = i32
+    if L.aigar_abi_version() != _abi.ABI_VERSION:
+        raise RuntimeError("libaigar_hip.so ABI %d != python binding %d" % (L.aigar_abi_version(), _abi.ABI_VERSION))
+    _lib = L
+    return L
+
+
+def _ptr(x):
+    """Host numpy array or device tensor -> (void pointer, on_device)."""
+    if x is None:
+        return None, 0
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data_as(C.c_void_p), 0
+    if hasattr(x, "data_ptr"):  # torch tensor (device memory when x.is_cuda)
+        return C.c_void_p(x.data_ptr()), int(bool(getattr(x, "is_cuda", False)))
+    raise TypeError("expected numpy array or torch tensor, got %r" % type(x))
+
+
+class Stepper:
+    """One handle of the device stepper: n_arenas fields x bots_per_arena players."""
+
+    def __init__(self, cfg):
+        self.L = load()
+        self.cfg = cfg
+        h = C.c_void_p()
+        self._chk(self.L.aigar_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+        self.A, self.B = cfg.n_arenas, cfg.bots_per_arena
+        self.NP = self.A * self.B
+        self.obs_len = self.L.aigar_obs_len(self.h)
+
+    def _chk(self, r):
+        if r < 0:
+            raise RuntimeError("aigar: " + self.L.aigar_last_error().decode())
+        return r
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.aigar_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, seed=0):
+        self._chk(self.L.aigar_reset(self.h, int(seed)))
+
+    def set_commands(self, cmd):
+        if isinstance(cmd, np.ndarray):
+            cmd = np.ascontiguousarray(cmd, np.float64).reshape(self.NP, 4)
+        p, dev = _ptr(cmd)
+        self._chk(self.L.aigar_set_commands(self.h, p, dev))
+
+    def policy_random(self, p_split=0.0, p_eject=0.0, seed=0):
+        self._chk(self.L.aigar_policy_random(self.h, float(p_split), float(p_eject), int(seed)))
+
+    def step(self, n=1):
+        self._chk(self.L.aigar_step(self.h, int(n)))
+
+    def observe(self, out=None, dtype=np.float64):
+        if out is None:
+            out = np.zeros((self.NP, self.obs_len), dtype)
+        dt = 0 if (getattr(out, "dtype", None) in (np.float64,) or str(getattr(out, "dtype", "")) == "torch.float64") else 1
+        p, dev = _ptr(out)
+        self._chk(self.L.aigar_observe(self.h, p, dt, dev))
+        return out
+
+    def set_actions(self, cur=None, prev=None):
+        c = None if cur is None else np.ascontiguousarray(cur, np.float64)
+        q = None if prev is None else np.ascontiguousarray(prev, np.float64)
+        self._chk(self.L.aigar_set_actions(self.h, _ptr(c)[0], _ptr(q)[0], 0))
+
+    def player_stats(self):
+        out = np.zeros((self.NP, 5), np.float64)
+        self._chk(self.L.aigar_player_stats(self.h, out.ctypes.data_as(C.c_void_p), 0))
+        return out
+
+    def get_state(self, arena=0):
+        cnt = _abi.State()
+        self._chk(self.L.aigar_get_state(self.h, arena, C.byref(cnt)))
+        st, arrays = _abi.alloc_state(cnt)
+        self._chk(self.L.aigar_get_state(self.h, arena, C.byref(st)))
+        return _abi.struct_to_dict(st, arrays)
+
+    def load_state(self, d, arena=0):
+        st, keep = _abi.state_to_struct(d)
+        self._chk(self.L.aigar_load_state(self.h, arena, C.byref(st)))
+
+    def events(self, arena=0):
+        n = C.c_int(0)
+        self._chk(self.L.aigar_get_events(self.h, arena, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 4), np.int64)
+        if n.value:
+            self._chk(self.L.aigar_get_events(self.h, arena, out.ctypes.data_as(C.POINTER(C.c_int64)), n.value,
+                                              C.byref(n)))
+        return out
+
+    def set_stream(self, stream_ptr):
+        self._chk(self.L.aigar_set_stream(self.h, C.c_void_p(int(stream_ptr))))
+
+    def sync(self):
+        self._chk(self.L.aigar_sync(self.h))
+
+    def profile(self, enable=True):
+        self._chk(self.L.aigar_profile(self.h, int(bool(enable))))
+
+    def kernel_time(self, name):
+        ms, n = C.c_double(0), C.c_int(0)
+        self._chk(self.L.aigar_kernel_time(self.h, name.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+def selftest_pow(x, y):
+    """Device pow_cr(x, y) for host arrays (diagnostics)."""
+    L = load()
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.zeros_like(x)
+    dp = C.POINTER(C.c_double)
+    if L.aigar_selftest_pow(x.ctypes.data_as(dp), y.ctypes.data_as(dp), out.ctypes.data_as(dp), len(x)) < 0:
+        raise RuntimeError("aigar: " + L.aigar_last_error().decode())
+    return out

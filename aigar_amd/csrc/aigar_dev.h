@@ -1,0 +1,135 @@
+// aigar_dev.h -- HBM layout of the stepper (all arenas of one handle).
+//
+// Structure-of-arrays, fp64 state (the reference computes in Python floats).
+// Index conventions (A arenas, B players per arena, NP = A*B):
+//   player  gp = a*B + p
+//   cell    pool index ci = slot*NP + gp, slot in [0,16): the 16 pool slots
+//           owned by a player; the player's cell *list* (order matters:
+//           player.py:22,48-61) is p_list[k*NP + gp] = slot of the k-th cell.
+//           Slot-major layout makes per-player loops coalesce across lanes.
+//   pellet  a*Pcap + i  (two buffers: P0 at tick boundaries, P1 during the
+//           eat phases; each rebuild counting-sorts records by centre bucket,
+//           so bucket b's pellets are contiguous: [pstart[b], pstart[b+1]) )
+//   blob    a*Ecap + i,   virus a*Vcap + i   (list order == creation order)
+//   grids   a*(H+1) + bucket   (H = cols*cols, 20-unit buckets)
+#pragma once
+#include <stdint.h>
+
+#include "../../include/aigar.h"
+
+namespace aigar {
+
+struct ArenaCtl {
+  int64_t seq_next;  // next Cell creation sequence number
+  int64_t tick;      // completed Field.update() calls since reset
+  uint64_t key0, key1, ctr_pellet, ctr_virus;
+  int64_t seq_base_upd;  // seq_next before updatePlayers' creations (this tick)
+  int64_t seq_base_spawn;
+  uint64_t ctr_pellet_base, ctr_virus_base;
+  int n_pel;          // pellets in the current primary buffer
+  int n_pnew;         // staged pellets (blob conversions, spawns)
+  int n_pel_eaten;    // eaten in this tick's eat phase
+  int n_blob;         // blob slots in use
+  int n_blob_base;    // blob count before this tick's ejections
+  int n_vir;          // virus slots in use
+  int n_vir_start;    // viruses that existed when virusBlobOverlap started
+  int n_dead;         // deadPlayers list length
+  int n_ev;           // events recorded this step
+  int n_pend;         // worklist length (serial phases)
+  int n_pend2;
+  int n_spawn_p, n_spawn_v, n_spawn_pl;
+  int vir_base_spawn;
+  uint32_t err;   // sticky error bits (capacity overflow ...)
+  uint32_t warn;  // sticky quirk bits (reference would raise)
+  double rmax_cell, rmax_virus;
+  uint64_t ev_order;  // serial-phase event counter
+};
+
+enum : uint32_t {
+  ERR_PELLET_CAP = 1, ERR_BLOB_CAP = 2, ERR_VIRUS_CAP = 4, ERR_EVENT_CAP = 8, ERR_WORK_CAP = 16,
+  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128
+};
+enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2 };
+
+// event phases (sort key high word), in reference order within a tick
+enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4, PH_PP = 5, PH_SPAWN = 6 };
+
+struct Dev {
+  int A, B, NP, size, cols, H;
+  int Pcap, Ecap, Vcap, Wcap, EVcap;
+  int virus_enabled;
+  double max_pellets, max_viruses;
+  int G, L;
+  uint32_t obs_ch, obs_ex;
+  int flags;
+  ArenaCtl *ctl;
+  // players [NP]
+  int *p_alive, *p_respawn, *p_ncells, *p_split, *p_eject, *p_pend;
+  double *p_cmdx, *p_cmdy;
+  uint8_t *p_list;  // [16][NP]
+  int *p_newc, *p_newb, *p_seqoff, *p_bloboff;
+  // cells [16*NP]
+  double *c_x, *c_y, *c_m, *c_r, *c_vx, *c_vy, *c_svx, *c_svy, *c_mt;
+  int *c_svc;
+  uint32_t *c_flags;
+  int64_t *c_seq;
+  uint8_t *c_active;
+  // per-player blob staging [16][NP]
+  double *sb_x, *sb_y, *sb_svx, *sb_svy;
+  uint8_t *sb_slot;
+  // pellets: two record buffers + staging
+  double *pel_x[2], *pel_y[2], *pel_m[2];
+  int64_t *pel_seq[2];
+  double *pn_x, *pn_y, *pn_m;
+  int64_t *pn_seq;
+  uint8_t *pel_dead;  // [A*Pcap] for the eat-phase buffer
+  int *pel_rank;      // scratch [A*(Pcap)]
+  int *pcnt, *pstart; // [A*(H+1)] counts / bucket starts (pellets)
+  uint64_t *pel_owner;  // reservation keys [A*Pcap]
+  // blobs [A*Ecap]
+  double *b_x, *b_y, *b_m, *b_r, *b_vx, *b_vy, *b_svx, *b_svy;
+  int *b_svc;
+  int64_t *b_seq, *b_ej;
+  uint32_t *b_flags;
+  uint64_t *b_owner;
+  int *bcnt, *bstart, *bitems, *b_rank;
+  // viruses [A*Vcap]
+  double *v_x, *v_y, *v_m, *v_r, *v_vx, *v_vy, *v_svx, *v_svy;
+  int *v_svc;
+  int64_t *v_seq;
+  uint32_t *v_flags;
+  uint8_t *v_active;
+  int *vcnt, *vstart, *vitems, *v_rank;
+  // cell grid
+  int *ccnt, *cstart, *citems, *c_rank;
+  // occupancy bitmap of the player hash [A][ceil(H/64)]
+  unsigned long long *occ;
+  int occ_words;
+  // dead list [NP], worklists [A*Wcap]
+  int *dead;
+  int *work, *work2;
+  // food-phase per-cell candidate lists [16*NP][FCAP]
+  int *f_list;
+  uint8_t *f_cnt;
+  uint8_t *f_done;
+  // spawn staging
+  int *respawn_list;  // [NP]
+  // events [A*EVcap][5]: key_hi, key_lo, code, a, b
+  int64_t *ev;
+  // observation state
+  double *o_lastfov;                             // [NP]
+  double *o_self_lf, *o_self_slf, *o_en_lf, *o_en_slf;  // [NP][G*G]
+  double *o_act_cur, *o_act_prev;                // [NP][4]
+  // observation overflow pool (bots that see more objects than their LDS lists hold)
+  int OBcap;
+  int *ob_used;
+  int64_t *ob_seq;
+  double *ob_m, *ob_r;
+  uint32_t *ob_mask;
+  uint8_t *ob_own;
+  int *ob_perm;
+};
+
+constexpr int FCAP = 32;  // stored candidate foods per cell (overflow -> serial)
+
+}  // namespace aigar

@@ -1,0 +1,751 @@
+// api.hip -- host implementation of include/aigar.h (libaigar_hip.so).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/aigar.h"
+#include "aigar_dev.h"
+#include "aigar_sem.h"
+
+namespace aigar {
+void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v);
+void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype);
+void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
+void launch_player_stats(const Dev &d, hipStream_t s, double *out);
+void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd);
+}  // namespace aigar
+
+using namespace aigar;
+
+static thread_local std::string g_err;
+static int fail(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) return fail("%s failed: %s", #x, hipGetErrorString(e_));       \
+  } while (0)
+
+struct aigar_handle {
+  aigar_config cfg;
+  Dev d;
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  int rounds = 4;
+  int64_t *scr_k = nullptr;
+  int *scr_v = nullptr;
+  double *d_cmd = nullptr, *d_stats = nullptr;
+  void *d_obs = nullptr;
+  std::vector<void *> allocs;
+  bool profile = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double obs_ms = 0, tick_ms = 0;
+  int obs_launches = 0, tick_launches = 0;
+  hipGraphExec_t graph = nullptr;
+  bool use_graph = false;
+  uint64_t policy_calls = 0;
+};
+
+extern "C" const char *aigar_last_error(void) { return g_err.c_str(); }
+extern "C" int aigar_abi_version(void) { return AIGAR_ABI_VERSION; }
+
+template <class T>
+static T *dalloc(aigar_handle *h, size_t n) {
+  void *p = nullptr;
+  if (n == 0) n = 1;
+  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
+  (void)hipMemset(p, 0, n * sizeof(T));
+  h->allocs.push_back(p);
+  return (T *)p;
+}
+
+static int obs_len_of(const aigar_config &c) {
+  int G = c.grid_squares ? c.grid_squares : 11, n = 0, e = 0;
+  for (int b = 0; b < 10; b++) n += (c.obs_channels >> b) & 1;
+  e += (c.obs_extras & AIGAR_EX_LAST_FOV) ? 1 : 0;
+  e += (c.obs_extras & AIGAR_EX_FOV) ? 1 : 0;
+  e += (c.obs_extras & AIGAR_EX_MASS) ? 1 : 0;
+  e += (c.obs_extras & AIGAR_EX_LAST_ACT) ? 4 : 0;
+  e += (c.obs_extras & AIGAR_EX_2LAST_ACT) ? 4 : 0;
+  return G * G * n + e;
+}
+
+static void free_all(aigar_handle *h) {
+  if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  for (void *p : h->allocs) (void)hipFree(p);
+  h->allocs.clear();
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
+}
+
+extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
+  if (!cfg || !out) return fail("aigar_create: null argument");
+  if (cfg->n_arenas < 1 || cfg->bots_per_arena < 1) return fail("aigar_create: need n_arenas >= 1 and bots >= 1");
+  if (cfg->rng_mode != AIGAR_RNG_PHILOX)
+    return fail("aigar_create: the device stepper runs AIGAR_RNG_PHILOX only (MT19937 lives in the CPU oracle)");
+  int G = cfg->grid_squares ? cfg->grid_squares : 11;
+  if (G < 1 || G > 16) return fail("aigar_create: grid_squares must be in [1, 16]");
+  if (cfg->obs_channels & AIGAR_OBS_ALL &&
+      cfg->obs_channels & (AIGAR_OBS_SELF_LF | AIGAR_OBS_SELF_SLF | AIGAR_OBS_ENEMY_LF | AIGAR_OBS_ENEMY_SLF))
+    return fail("aigar_create: ALL_PLAYER_GRID with last-frame grids is undefined in the reference");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail("aigar_create: device %d not present (%d devices)", cfg->device, ndev);
+  HIPCHK(hipSetDevice(cfg->device));
+  aigar_handle *h = new aigar_handle();
+  h->cfg = *cfg;
+  Dev &d = h->d;
+  d.A = cfg->n_arenas;
+  d.B = cfg->bots_per_arena;
+  d.NP = d.A * d.B;
+  d.size = cfg->field_size > 0 ? cfg->field_size : (int)(75 * std::sqrt((double)d.B));
+  d.cols = (int)std::ceil(d.size / 20.0);
+  d.H = d.cols * d.cols;
+  d.virus_enabled = cfg->virus_enabled ? 1 : 0;
+  d.max_pellets = cfg->max_pellets >= 0 ? cfg->max_pellets : (double)d.size * d.size * 0.015;
+  d.max_viruses = cfg->max_viruses >= 0 ? cfg->max_viruses : (double)d.size * d.size * 0.00005;
+  if (!d.virus_enabled) d.max_viruses = 0;
+  d.Ecap = cfg->blob_cap > 0 ? cfg->blob_cap : 4 * d.B + 256;
+  d.Pcap = cfg->pellet_cap > 0 ? cfg->pellet_cap : (int)std::ceil(d.max_pellets) + d.Ecap + 64;
+  d.Vcap = cfg->virus_cap > 0 ? cfg->virus_cap : 2 * (int)std::ceil(d.max_viruses) + 64;
+  d.Wcap = std::max(kMaxCells * d.B, std::max(d.Ecap, 4096));
+  d.EVcap = cfg->event_cap > 0 ? cfg->event_cap : 65536;
+  d.G = G;
+  d.L = obs_len_of(*cfg);
+  d.obs_ch = cfg->obs_channels;
+  d.obs_ex = cfg->obs_extras;
+  d.flags = cfg->flags;
+  d.occ_words = (d.H + 63) / 64;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return fail("hipStreamCreate failed");
+  }
+  const size_t A = d.A, NP = d.NP, C = (size_t)kMaxCells * NP, H1 = (size_t)d.H + 1, GG = (size_t)G * G;
+  bool ok = true;
+#define AL(field, T, n)                     \
+  do {                                      \
+    d.field = dalloc<T>(h, (n));            \
+    ok = ok && d.field != nullptr;          \
+  } while (0)
+  AL(ctl, ArenaCtl, A);
+  AL(p_alive, int, NP); AL(p_respawn, int, NP); AL(p_ncells, int, NP); AL(p_split, int, NP); AL(p_eject, int, NP);
+  AL(p_pend, int, NP); AL(p_cmdx, double, NP); AL(p_cmdy, double, NP); AL(p_list, uint8_t, C);
+  AL(p_newc, int, NP); AL(p_newb, int, NP); AL(p_seqoff, int, NP); AL(p_bloboff, int, NP);
+  AL(c_x, double, C); AL(c_y, double, C); AL(c_m, double, C); AL(c_r, double, C); AL(c_vx, double, C);
+  AL(c_vy, double, C); AL(c_svx, double, C); AL(c_svy, double, C); AL(c_mt, double, C); AL(c_svc, int, C);
+  AL(c_flags, uint32_t, C); AL(c_seq, int64_t, C); AL(c_active, uint8_t, C);
+  AL(sb_x, double, C); AL(sb_y, double, C); AL(sb_svx, double, C); AL(sb_svy, double, C); AL(sb_slot, uint8_t, C);
+  const size_t P = A * d.Pcap;
+  for (int b = 0; b < 2; b++) {
+    AL(pel_x[b], double, P); AL(pel_y[b], double, P); AL(pel_m[b], double, P); AL(pel_seq[b], int64_t, P);
+  }
+  AL(pn_x, double, P); AL(pn_y, double, P); AL(pn_m, double, P); AL(pn_seq, int64_t, P);
+  AL(pel_dead, uint8_t, P); AL(pel_rank, int, 2 * P); AL(pcnt, int, A * H1); AL(pstart, int, A * H1);
+  AL(pel_owner, uint64_t, P);
+  const size_t E = A * d.Ecap, V = A * d.Vcap;
+  AL(b_x, double, E); AL(b_y, double, E); AL(b_m, double, E); AL(b_r, double, E); AL(b_vx, double, E);
+  AL(b_vy, double, E); AL(b_svx, double, E); AL(b_svy, double, E); AL(b_svc, int, E); AL(b_seq, int64_t, E);
+  AL(b_ej, int64_t, E); AL(b_flags, uint32_t, E); AL(b_owner, uint64_t, E);
+  AL(bcnt, int, A * H1); AL(bstart, int, A * H1); AL(bitems, int, E); AL(b_rank, int, E);
+  AL(v_x, double, V); AL(v_y, double, V); AL(v_m, double, V); AL(v_r, double, V); AL(v_vx, double, V);
+  AL(v_vy, double, V); AL(v_svx, double, V); AL(v_svy, double, V); AL(v_svc, int, V); AL(v_seq, int64_t, V);
+  AL(v_flags, uint32_t, V); AL(v_active, uint8_t, V);
+  AL(vcnt, int, A * H1); AL(vstart, int, A * H1); AL(vitems, int, V); AL(v_rank, int, V);
+  AL(ccnt, int, A * H1); AL(cstart, int, A * H1); AL(citems, int, C); AL(c_rank, int, C);
+  AL(occ, unsigned long long, A * d.occ_words);
+  AL(dead, int, NP); AL(work, int, A * d.Wcap); AL(work2, int, A * d.Wcap);
+  AL(f_list, int, C * FCAP); AL(f_cnt, uint8_t, C); AL(f_done, uint8_t, C);
+  AL(respawn_list, int, NP);
+  AL(ev, int64_t, A * d.EVcap * 5);
+  AL(o_lastfov, double, NP); AL(o_self_lf, double, NP * GG); AL(o_self_slf, double, NP * GG);
+  AL(o_en_lf, double, NP * GG); AL(o_en_slf, double, NP * GG); AL(o_act_cur, double, NP * 4);
+  AL(o_act_prev, double, NP * 4);
+  d.OBcap = (int)std::min<size_t>(std::max<size_t>(1u << 20, 64 * NP), (size_t)1 << 24);
+  AL(ob_used, int, 1); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
+  AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
+#undef AL
+  h->scr_k = dalloc<int64_t>(h, A * d.Wcap);
+  h->scr_v = dalloc<int>(h, A * d.Wcap);
+  h->d_cmd = dalloc<double>(h, NP * 4);
+  h->d_stats = dalloc<double>(h, NP * 5);
+  h->d_obs = dalloc<double>(h, NP * (size_t)d.L);
+  ok = ok && h->scr_k && h->scr_v && h->d_cmd && h->d_stats && h->d_obs;
+  (void)hipEventCreate(&h->ev0);
+  (void)hipEventCreate(&h->ev1);
+  if (!ok) {
+    free_all(h);
+    delete h;
+    return fail("aigar_create: device allocation failed");
+  }
+  if (hipDeviceSynchronize() != hipSuccess) {
+    free_all(h);
+    delete h;
+    return fail("aigar_create: device synchronize failed");
+  }
+  *out = h;
+  return 0;
+}
+
+extern "C" int aigar_destroy(aigar_handle *h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_all(h);
+  delete h;
+  return 0;
+}
+
+static int check_device_errors(aigar_handle *h) {
+  std::vector<ArenaCtl> ctl(h->d.A);
+  HIPCHK(hipMemcpyAsync(ctl.data(), h->d.ctl, sizeof(ArenaCtl) * h->d.A, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int a = 0; a < h->d.A; a++)
+    if (ctl[a].err)
+      return fail("device error bits 0x%x in arena %d (1 pellet cap, 2 blob cap, 4 virus cap, 8 event cap, "
+                  "16 worklist cap, 32 observation cap, 64 candidate cap)",
+                  ctl[a].err, a);
+  return 0;
+}
+
+__global__ void k_fill_d(double *p, size_t n, double v) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  Dev &d = h->d;
+  const size_t NP = d.NP, GG = (size_t)d.G * d.G, A = d.A, H1 = (size_t)d.H + 1;
+  hipLaunchKernelGGL(k_fill_d, dim3((NP + 255) / 256), dim3(256), 0, h->stream, d.p_cmdx, NP, -1.0);
+  hipLaunchKernelGGL(k_fill_d, dim3((NP + 255) / 256), dim3(256), 0, h->stream, d.p_cmdy, NP, -1.0);
+  HIPCHK(hipMemsetAsync(d.cstart, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.vstart, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.bstart, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.o_lastfov, 0, sizeof(double) * NP, h->stream));
+  for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
+    HIPCHK(hipMemsetAsync(p, 0, sizeof(double) * NP * GG, h->stream));
+  launch_reset(d, h->stream, seed);
+  HIPCHK(hipGetLastError());
+  return check_device_errors(h);
+}
+
+extern "C" int aigar_set_commands(aigar_handle *h, const double *cmd, int on_device) {
+  if (!h || !cmd) return fail("null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const double *src = cmd;
+  if (!on_device) {
+    HIPCHK(hipMemcpyAsync(h->d_cmd, cmd, sizeof(double) * 4 * h->d.NP, hipMemcpyHostToDevice, h->stream));
+    src = h->d_cmd;
+  }
+  launch_set_commands(h->d, h->stream, src);
+  HIPCHK(hipGetLastError());
+  if (!on_device) HIPCHK(hipStreamSynchronize(h->stream));  // caller may reuse its buffer
+  return 0;
+}
+
+extern "C" int aigar_policy_random(aigar_handle *h, double p_split, double p_eject, uint64_t seed) {
+  if (!h) return fail("null handle");
+  launch_policy(h->d, h->stream, p_split, p_eject, seed + (h->policy_calls++ << 20));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+__global__ void k_step_begin(Dev d) {
+  int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < d.A) d.ctl[a].n_ev = 0;
+}
+
+extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
+  if (!h) return fail("null handle");
+  if (n_ticks < 0) return fail("n_ticks < 0");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  for (int t = 0; t < n_ticks; t++) {
+    if (h->profile) HIPCHK(hipEventRecord(h->ev0, h->stream));
+    launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
+    if (h->profile) {
+      HIPCHK(hipEventRecord(h->ev1, h->stream));
+      HIPCHK(hipEventSynchronize(h->ev1));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+      h->tick_ms += ms;
+      h->tick_launches++;
+    }
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int aigar_obs_len(aigar_handle *h) { return h ? h->d.L : -1; }
+
+extern "C" int aigar_observe(aigar_handle *h, void *out, int dtype, int on_device) {
+  if (!h || !out) return fail("null argument");
+  if (dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  void *dst = on_device ? out : h->d_obs;
+  if (h->profile) HIPCHK(hipEventRecord(h->ev0, h->stream));
+  launch_observe(h->d, h->stream, dst, dtype);
+  if (h->profile) {
+    HIPCHK(hipEventRecord(h->ev1, h->stream));
+    HIPCHK(hipEventSynchronize(h->ev1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    h->obs_ms += ms;
+    h->obs_launches++;
+  }
+  HIPCHK(hipGetLastError());
+  if (!on_device) {
+    size_t bytes = (size_t)h->d.NP * h->d.L * (dtype == 0 ? 8 : 4);
+    HIPCHK(hipMemcpyAsync(out, h->d_obs, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return check_device_errors(h);
+  }
+  return 0;
+}
+
+__global__ void k_set_actions(Dev d, const double *cur, const double *prev) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= (size_t)d.NP * 4) return;
+  if (cur) d.o_act_cur[i] = cur[i];
+  if (prev) d.o_act_prev[i] = prev[i];
+}
+
+extern "C" int aigar_set_actions(aigar_handle *h, const double *cur, const double *prev, int on_device) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  size_t n = (size_t)h->d.NP * 4;
+  if (on_device) {
+    hipLaunchKernelGGL(k_set_actions, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d, cur, prev);
+  } else {
+    if (cur) HIPCHK(hipMemcpyAsync(h->d.o_act_cur, cur, n * 8, hipMemcpyHostToDevice, h->stream));
+    if (prev) HIPCHK(hipMemcpyAsync(h->d.o_act_prev, prev, n * 8, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return 0;
+}
+
+extern "C" int aigar_player_stats(aigar_handle *h, double *out, int on_device) {
+  if (!h || !out) return fail("null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  launch_player_stats(h->d, h->stream, on_device ? out : h->d_stats);
+  if (!on_device) {
+    HIPCHK(hipMemcpyAsync(out, h->d_stats, sizeof(double) * 5 * h->d.NP, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return 0;
+}
+
+extern "C" int aigar_set_stream(aigar_handle *h, void *s) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (h->own_stream) (void)hipStreamDestroy(h->stream);
+  h->stream = (hipStream_t)s;
+  h->own_stream = false;
+  return 0;
+}
+
+extern "C" int aigar_sync(aigar_handle *h) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  return check_device_errors(h);
+}
+
+extern "C" int aigar_profile(aigar_handle *h, int enable) {
+  if (!h) return fail("null handle");
+  h->profile = enable != 0;
+  h->obs_ms = h->tick_ms = 0;
+  h->obs_launches = h->tick_launches = 0;
+  return 0;
+}
+extern "C" int aigar_kernel_time(aigar_handle *h, const char *name, double *ms, int *launches) {
+  if (!h || !name || !ms || !launches) return fail("null argument");
+  if (!strcmp(name, "observe")) {
+    *ms = h->obs_ms;
+    *launches = h->obs_launches;
+  } else if (!strcmp(name, "tick")) {
+    *ms = h->tick_ms;
+    *launches = h->tick_launches;
+  } else {
+    return fail("unknown timer '%s' (observe | tick)", name);
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- snapshots
+template <class T>
+static int d2h(aigar_handle *h, std::vector<T> &v, const T *src, size_t n) {
+  v.resize(n);
+  if (n) HIPCHK(hipMemcpyAsync(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+  return 0;
+}
+template <class T>
+static int h2d(aigar_handle *h, T *dst, const std::vector<T> &v) {
+  if (!v.empty()) HIPCHK(hipMemcpyAsync(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, h->stream));
+  return 0;
+}
+
+extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
+  if (!h || !st) return fail("null argument");
+  Dev &d = h->d;
+  if (arena < 0 || arena >= d.A) return fail("arena %d out of range", arena);
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (check_device_errors(h)) return -1;
+  ArenaCtl c;
+  HIPCHK(hipMemcpy(&c, d.ctl + arena, sizeof c, hipMemcpyDeviceToHost));
+  const int B = d.B, NP = d.NP;
+  const size_t p0 = (size_t)arena * B;
+  std::vector<int> alive, resp, ncells, split, eject, dead;
+  std::vector<double> cmdx, cmdy;
+  if (d2h(h, alive, d.p_alive + p0, B) || d2h(h, resp, d.p_respawn + p0, B) || d2h(h, ncells, d.p_ncells + p0, B) ||
+      d2h(h, split, d.p_split + p0, B) || d2h(h, eject, d.p_eject + p0, B) || d2h(h, cmdx, d.p_cmdx + p0, B) ||
+      d2h(h, cmdy, d.p_cmdy + p0, B) || d2h(h, dead, d.dead + p0, c.n_dead))
+    return -1;
+  // cells: 16 slot rows of this arena's players
+  std::vector<uint8_t> lst((size_t)kMaxCells * B);
+  std::vector<double> cf[9];
+  std::vector<int> csvc((size_t)kMaxCells * B);
+  std::vector<uint32_t> cfl((size_t)kMaxCells * B);
+  std::vector<int64_t> cseq((size_t)kMaxCells * B);
+  double *cfs[9] = {d.c_x, d.c_y, d.c_m, d.c_r, d.c_vx, d.c_vy, d.c_svx, d.c_svy, d.c_mt};
+  for (int f = 0; f < 9; f++) cf[f].resize((size_t)kMaxCells * B);
+  for (int s = 0; s < kMaxCells; s++) {
+    size_t o = (size_t)s * NP + p0, ho = (size_t)s * B;
+    HIPCHK(hipMemcpyAsync(lst.data() + ho, d.p_list + o, B, hipMemcpyDeviceToHost, h->stream));
+    for (int f = 0; f < 9; f++)
+      HIPCHK(hipMemcpyAsync(cf[f].data() + ho, cfs[f] + o, 8 * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(csvc.data() + ho, d.c_svc + o, 4 * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(cfl.data() + ho, d.c_flags + o, 4 * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(cseq.data() + ho, d.c_seq + o, 8 * B, hipMemcpyDeviceToHost, h->stream));
+  }
+  const size_t po = (size_t)arena * d.Pcap, bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;
+  std::vector<double> px, py, pm, bf[8], vf[8];
+  std::vector<int64_t> ps, bseq, bej, vseq;
+  std::vector<int> bsvc, vsvc;
+  std::vector<uint32_t> bfl, vfl;
+  if (d2h(h, px, d.pel_x[0] + po, c.n_pel) || d2h(h, py, d.pel_y[0] + po, c.n_pel) ||
+      d2h(h, pm, d.pel_m[0] + po, c.n_pel) || d2h(h, ps, d.pel_seq[0] + po, c.n_pel))
+    return -1;
+  double *bfs[8] = {d.b_x, d.b_y, d.b_m, d.b_r, d.b_vx, d.b_vy, d.b_svx, d.b_svy};
+  double *vfs[8] = {d.v_x, d.v_y, d.v_m, d.v_r, d.v_vx, d.v_vy, d.v_svx, d.v_svy};
+  for (int f = 0; f < 8; f++)
+    if (d2h(h, bf[f], bfs[f] + bo, c.n_blob) || d2h(h, vf[f], vfs[f] + vo, c.n_vir)) return -1;
+  if (d2h(h, bsvc, d.b_svc + bo, c.n_blob) || d2h(h, bseq, d.b_seq + bo, c.n_blob) ||
+      d2h(h, bej, d.b_ej + bo, c.n_blob) || d2h(h, bfl, d.b_flags + bo, c.n_blob) ||
+      d2h(h, vsvc, d.v_svc + vo, c.n_vir) || d2h(h, vseq, d.v_seq + vo, c.n_vir) ||
+      d2h(h, vfl, d.v_flags + vo, c.n_vir))
+    return -1;
+  HIPCHK(hipStreamSynchronize(h->stream));
+
+  int nc = 0;
+  for (int p = 0; p < B; p++) nc += ncells[p];
+  std::vector<int> bl, vl;
+  for (int i = 0; i < c.n_blob; i++)
+    if (bfl[i] & F_ALIVE) bl.push_back(i);
+  for (int i = 0; i < c.n_vir; i++)
+    if (vfl[i] & F_ALIVE) vl.push_back(i);
+  std::sort(bl.begin(), bl.end(), [&](int x, int y) { return bseq[x] < bseq[y]; });
+  std::sort(vl.begin(), vl.end(), [&](int x, int y) { return vseq[x] < vseq[y]; });
+  int caps[5] = {st->n_cells, st->n_pellets, st->n_blobs, st->n_viruses, st->n_dead};
+  st->n_players = B;
+  st->field_size = d.size;
+  st->virus_enabled = d.virus_enabled;
+  st->rng_mode = AIGAR_RNG_PHILOX;
+  st->seq_next = c.seq_next;
+  st->tick = c.tick;
+  st->max_pellets = d.max_pellets;
+  st->max_viruses = d.max_viruses;
+  st->philox_key[0] = c.key0;
+  st->philox_key[1] = c.key1;
+  st->ctr_pellet = c.ctr_pellet;
+  st->ctr_virus = c.ctr_virus;
+  memset(st->mt_key, 0, sizeof st->mt_key);
+  st->mt_pos = 0;
+  st->n_cells = nc;
+  st->n_pellets = c.n_pel;
+  st->n_blobs = (int)bl.size();
+  st->n_viruses = (int)vl.size();
+  st->n_dead = c.n_dead;
+  if (!st->cells_f) return 0;
+  if (caps[0] < nc || caps[1] < c.n_pel || caps[2] < (int)bl.size() || caps[3] < (int)vl.size() || caps[4] < c.n_dead)
+    return fail("get_state: caller arrays too small");
+  for (int p = 0; p < B; p++) {
+    st->players_f[2 * p] = cmdx[p];
+    st->players_f[2 * p + 1] = cmdy[p];
+    int64_t *q = st->players_i + 5 * p;
+    q[0] = alive[p]; q[1] = resp[p]; q[2] = split[p]; q[3] = eject[p]; q[4] = ncells[p];
+  }
+  int k = 0;
+  for (int p = 0; p < B; p++)
+    for (int j = 0; j < ncells[p]; j++, k++) {
+      size_t hi = (size_t)lst[(size_t)j * B + p] * B + p;
+      for (int f = 0; f < 9; f++) st->cells_f[9 * k + f] = cf[f][hi];
+      int64_t *q = st->cells_i + 4 * k;
+      q[0] = p; q[1] = csvc[hi]; q[2] = cseq[hi]; q[3] = (cfl[hi] & F_INHASH) ? 1 : 0;
+    }
+  std::vector<int> pord(c.n_pel);
+  for (int i = 0; i < c.n_pel; i++) pord[i] = i;
+  std::sort(pord.begin(), pord.end(), [&](int x, int y) { return ps[x] < ps[y]; });
+  for (int i = 0; i < c.n_pel; i++) {
+    int j = pord[i];
+    double *f = st->pellets_f + 4 * i;
+    f[0] = px[j]; f[1] = py[j]; f[2] = pm[j]; f[3] = pm[j] > 0 ? std::sqrt(pm[j] / 3.141592653589793) : 0.0;
+    st->pellets_seq[i] = ps[j];
+  }
+  for (size_t i = 0; i < bl.size(); i++) {
+    int j = bl[i];
+    for (int f = 0; f < 8; f++) st->blobs_f[8 * i + f] = bf[f][j];
+    st->blobs_i[3 * i] = bsvc[j]; st->blobs_i[3 * i + 1] = bseq[j]; st->blobs_i[3 * i + 2] = bej[j];
+  }
+  for (size_t i = 0; i < vl.size(); i++) {
+    int j = vl[i];
+    for (int f = 0; f < 8; f++) st->viruses_f[8 * i + f] = vf[f][j];
+    st->viruses_i[3 * i] = vsvc[j]; st->viruses_i[3 * i + 1] = vseq[j];
+    st->viruses_i[3 * i + 2] = (vfl[j] & F_INHASH) ? 1 : 0;
+  }
+  for (int i = 0; i < c.n_dead; i++) st->dead[i] = dead[i];
+  return 0;
+}
+
+// counting sort of items by centre bucket (host side, used by load_state)
+static void host_grid(int cols, const std::vector<double> &x, const std::vector<double> &y, std::vector<int> &start,
+                      std::vector<int> &order) {
+  int H = cols * cols;
+  start.assign(H + 1, 0);
+  std::vector<int> b(x.size());
+  for (size_t i = 0; i < x.size(); i++) {
+    auto cb = [&](double v) {
+      int q = (int)(v / 20);
+      if (v < 0) q = 0;
+      return q < cols ? q : cols - 1;
+    };
+    b[i] = cb(y[i]) * cols + cb(x[i]);
+    start[b[i] + 1]++;
+  }
+  for (int i = 0; i < H; i++) start[i + 1] += start[i];
+  std::vector<int> cur(start.begin(), start.end() - 1);
+  order.assign(x.size(), 0);
+  for (size_t i = 0; i < x.size(); i++) order[cur[b[i]]++] = (int)i;
+}
+
+extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *st) {
+  if (!h || !st) return fail("null argument");
+  Dev &d = h->d;
+  if (arena < 0 || arena >= d.A) return fail("arena %d out of range", arena);
+  if (st->n_players != d.B) return fail("load_state: n_players %d != bots_per_arena %d", st->n_players, d.B);
+  if (st->field_size != d.size) return fail("load_state: field_size %d != %d", st->field_size, d.size);
+  if (!!st->virus_enabled != !!d.virus_enabled) return fail("load_state: virus_enabled mismatch");
+  if (st->n_pellets > d.Pcap || st->n_blobs > d.Ecap || st->n_viruses > d.Vcap)
+    return fail("load_state: snapshot exceeds capacities (pellets %d/%d blobs %d/%d viruses %d/%d)", st->n_pellets,
+                d.Pcap, st->n_blobs, d.Ecap, st->n_viruses, d.Vcap);
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int B = d.B, NP = d.NP;
+  const size_t p0 = (size_t)arena * B, GG = (size_t)d.G * d.G;
+  std::vector<int> alive(B), resp(B), ncells(B, 0), split(B), eject(B), dead(st->n_dead);
+  std::vector<double> cmdx(B), cmdy(B);
+  for (int p = 0; p < B; p++) {
+    cmdx[p] = st->players_f[2 * p];
+    cmdy[p] = st->players_f[2 * p + 1];
+    const int64_t *q = st->players_i + 5 * p;
+    alive[p] = (int)q[0]; resp[p] = (int)q[1]; split[p] = (int)q[2]; eject[p] = (int)q[3];
+  }
+  const size_t CB = (size_t)kMaxCells * B;
+  std::vector<uint8_t> lst(CB, 0);
+  std::vector<double> cf[9];
+  for (int f = 0; f < 9; f++) cf[f].assign(CB, 0.0);
+  std::vector<int> csvc(CB, 0);
+  std::vector<uint32_t> cfl(CB, 0);
+  std::vector<int64_t> cseq(CB, 0);
+  std::vector<double> gx, gy;
+  std::vector<int> gid;
+  double rmax_c = 0;
+  for (int k = 0; k < st->n_cells; k++) {
+    const int64_t *q = st->cells_i + 4 * k;
+    int p = (int)q[0];
+    if (p < 0 || p >= B) return fail("load_state: cell owner %d out of range", p);
+    int j = ncells[p]++;
+    if (j >= kMaxCells) return fail("load_state: player %d has more than 16 cells", p);
+    lst[(size_t)j * B + p] = (uint8_t)j;  // slot j == list position j
+    size_t hi = (size_t)j * B + p;
+    for (int f = 0; f < 9; f++) cf[f][hi] = st->cells_f[9 * k + f];
+    csvc[hi] = (int)q[1];
+    cseq[hi] = q[2];
+    cfl[hi] = F_ALIVE | (q[3] ? F_INHASH : 0);
+    gx.push_back(cf[0][hi]);
+    gy.push_back(cf[1][hi]);
+    gid.push_back((int)((size_t)j * NP + p0 + p));
+    rmax_c = std::max(rmax_c, cf[3][hi]);
+  }
+  for (int i = 0; i < st->n_dead; i++) dead[i] = (int)st->dead[i];
+  if (h2d(h, d.p_alive + p0, alive) || h2d(h, d.p_respawn + p0, resp) || h2d(h, d.p_ncells + p0, ncells) ||
+      h2d(h, d.p_split + p0, split) || h2d(h, d.p_eject + p0, eject) || h2d(h, d.p_cmdx + p0, cmdx) ||
+      h2d(h, d.p_cmdy + p0, cmdy) || h2d(h, d.dead + p0, dead))
+    return -1;
+  double *cfs[9] = {d.c_x, d.c_y, d.c_m, d.c_r, d.c_vx, d.c_vy, d.c_svx, d.c_svy, d.c_mt};
+  for (int s = 0; s < kMaxCells; s++) {
+    size_t o = (size_t)s * NP + p0, ho = (size_t)s * B;
+    HIPCHK(hipMemcpyAsync(d.p_list + o, lst.data() + ho, B, hipMemcpyHostToDevice, h->stream));
+    for (int f = 0; f < 9; f++)
+      HIPCHK(hipMemcpyAsync(cfs[f] + o, cf[f].data() + ho, 8 * B, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(d.c_svc + o, csvc.data() + ho, 4 * B, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(d.c_flags + o, cfl.data() + ho, 4 * B, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(d.c_seq + o, cseq.data() + ho, 8 * B, hipMemcpyHostToDevice, h->stream));
+  }
+  // cell grid (for observations before the next tick)
+  std::vector<int> start, order;
+  host_grid(d.cols, gx, gy, start, order);
+  std::vector<int> items(order.size());
+  for (size_t i = 0; i < order.size(); i++) items[i] = gid[order[i]];
+  const size_t H1 = (size_t)d.H + 1;
+  HIPCHK(hipMemcpyAsync(d.cstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
+  if (!items.empty())
+    HIPCHK(hipMemcpyAsync(d.citems + (size_t)arena * CB, items.data(), 4 * items.size(), hipMemcpyHostToDevice,
+                          h->stream));
+  // pellets -> P0 sorted by bucket
+  std::vector<double> px(st->n_pellets), py(st->n_pellets), pm(st->n_pellets);
+  std::vector<int64_t> ps(st->n_pellets);
+  for (int i = 0; i < st->n_pellets; i++) {
+    px[i] = st->pellets_f[4 * i];
+    py[i] = st->pellets_f[4 * i + 1];
+    pm[i] = st->pellets_f[4 * i + 2];
+    ps[i] = st->pellets_seq[i];
+  }
+  host_grid(d.cols, px, py, start, order);
+  {
+    std::vector<double> sx(order.size()), sy(order.size()), sm(order.size());
+    std::vector<int64_t> ss(order.size());
+    for (size_t i = 0; i < order.size(); i++) {
+      sx[i] = px[order[i]]; sy[i] = py[order[i]]; sm[i] = pm[order[i]]; ss[i] = ps[order[i]];
+    }
+    const size_t po = (size_t)arena * d.Pcap;
+    if (h2d(h, d.pel_x[0] + po, sx) || h2d(h, d.pel_y[0] + po, sy) || h2d(h, d.pel_m[0] + po, sm) ||
+        h2d(h, d.pel_seq[0] + po, ss))
+      return -1;
+    HIPCHK(hipMemcpyAsync(d.pstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
+  }
+  // blobs and viruses in list order; blob grid for completeness, virus grid for observations
+  const size_t bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;
+  double *bfs[8] = {d.b_x, d.b_y, d.b_m, d.b_r, d.b_vx, d.b_vy, d.b_svx, d.b_svy};
+  double *vfs[8] = {d.v_x, d.v_y, d.v_m, d.v_r, d.v_vx, d.v_vy, d.v_svx, d.v_svy};
+  for (int f = 0; f < 8; f++) {
+    std::vector<double> bv(st->n_blobs), vv(st->n_viruses);
+    for (int i = 0; i < st->n_blobs; i++) bv[i] = st->blobs_f[8 * i + f];
+    for (int i = 0; i < st->n_viruses; i++) vv[i] = st->viruses_f[8 * i + f];
+    if (h2d(h, bfs[f] + bo, bv) || h2d(h, vfs[f] + vo, vv)) return -1;
+  }
+  std::vector<int> bsvc(st->n_blobs), vsvc(st->n_viruses);
+  std::vector<int64_t> bseq(st->n_blobs), bej(st->n_blobs), vseq(st->n_viruses);
+  std::vector<uint32_t> bfl(d.Ecap, 0), vfl(d.Vcap, 0);
+  std::vector<double> vgx, vgy;
+  double rmax_v = 0;
+  for (int i = 0; i < st->n_blobs; i++) {
+    bsvc[i] = (int)st->blobs_i[3 * i]; bseq[i] = st->blobs_i[3 * i + 1]; bej[i] = st->blobs_i[3 * i + 2];
+    bfl[i] = F_ALIVE;
+  }
+  std::vector<int> vg_ids;
+  for (int i = 0; i < st->n_viruses; i++) {
+    vsvc[i] = (int)st->viruses_i[3 * i]; vseq[i] = st->viruses_i[3 * i + 1];
+    vfl[i] = F_ALIVE | (st->viruses_i[3 * i + 2] ? F_INHASH : 0);
+    vgx.push_back(st->viruses_f[8 * i]);
+    vgy.push_back(st->viruses_f[8 * i + 1]);
+    rmax_v = std::max(rmax_v, st->viruses_f[8 * i + 3]);
+  }
+  if (h2d(h, d.b_svc + bo, bsvc) || h2d(h, d.b_seq + bo, bseq) || h2d(h, d.b_ej + bo, bej) ||
+      h2d(h, d.b_flags + bo, bfl) || h2d(h, d.v_svc + vo, vsvc) || h2d(h, d.v_seq + vo, vseq) ||
+      h2d(h, d.v_flags + vo, vfl))
+    return -1;
+  host_grid(d.cols, vgx, vgy, start, order);
+  HIPCHK(hipMemcpyAsync(d.vstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
+  if (!order.empty()) HIPCHK(hipMemcpyAsync(d.vitems + vo, order.data(), 4 * order.size(), hipMemcpyHostToDevice, h->stream));
+  // control block
+  ArenaCtl c;
+  memset(&c, 0, sizeof c);
+  c.seq_next = st->seq_next;
+  c.tick = st->tick;
+  c.key0 = st->philox_key[0];
+  c.key1 = st->philox_key[1];
+  c.ctr_pellet = st->ctr_pellet;
+  c.ctr_virus = st->ctr_virus;
+  c.n_pel = st->n_pellets;
+  c.n_blob = st->n_blobs;
+  c.n_vir = st->n_viruses;
+  c.n_dead = st->n_dead;
+  c.rmax_cell = std::max(rmax_c, std::sqrt(10.0 / 3.141592653589793));
+  c.rmax_virus = std::max(rmax_v, std::sqrt(100.0 / 3.141592653589793));
+  HIPCHK(hipMemcpyAsync(d.ctl + arena, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
+  // bot-side observation history restarts (NN bot reset, bot.py:151-158)
+  HIPCHK(hipMemsetAsync(d.o_lastfov + p0, 0, 8 * B, h->stream));
+  for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
+    HIPCHK(hipMemsetAsync(p + p0 * GG, 0, 8 * B * GG, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int cap, int *n) {
+  if (!h || !n) return fail("null argument");
+  Dev &d = h->d;
+  if (arena < 0 || arena >= d.A) return fail("arena %d out of range", arena);
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (check_device_errors(h)) return -1;
+  ArenaCtl c;
+  HIPCHK(hipMemcpy(&c, d.ctl + arena, sizeof c, hipMemcpyDeviceToHost));
+  int ne = std::min(c.n_ev, d.EVcap);
+  *n = ne;
+  if (!out) return 0;
+  if (cap < ne) return fail("get_events: cap %d < %d events", cap, ne);
+  std::vector<int64_t> ev((size_t)ne * 5);
+  if (ne) HIPCHK(hipMemcpy(ev.data(), d.ev + (size_t)arena * d.EVcap * 5, ev.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<int> ord(ne);
+  for (int i = 0; i < ne; i++) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](int x, int y) {
+    if (ev[5 * x] != ev[5 * y]) return ev[5 * x] < ev[5 * y];
+    return (uint64_t)ev[5 * x + 1] < (uint64_t)ev[5 * y + 1];
+  });
+  for (int i = 0; i < ne; i++) {
+    const int64_t *e = &ev[5 * (size_t)ord[i]];
+    out[4 * i] = e[0] >> 8;
+    out[4 * i + 1] = e[2];
+    out[4 * i + 2] = e[3];
+    out[4 * i + 3] = e[4];
+  }
+  return 0;
+}
+
+__global__ void k_selftest_pow(const double *x, const double *y, double *out, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = aigar_math::pow_cr(x[i], y[i]);
+}
+
+extern "C" int aigar_selftest_pow(const double *x, const double *y, double *out, int n) {
+  if (!x || !y || !out || n < 0) return fail("null argument");
+  double *dx = nullptr, *dy = nullptr, *dz = nullptr;
+  size_t b = sizeof(double) * (size_t)(n > 0 ? n : 1);
+  HIPCHK(hipMalloc(&dx, b));
+  HIPCHK(hipMalloc(&dy, b));
+  HIPCHK(hipMalloc(&dz, b));
+  HIPCHK(hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy, y, sizeof(double) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_selftest_pow, dim3((n + 255) / 256), dim3(256), 0, 0, dx, dy, dz, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dz, sizeof(double) * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dz);
+  return 0;
+}

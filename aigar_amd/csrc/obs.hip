@@ -1,0 +1,438 @@
+// obs.hip -- Bot.getStateRepresentation() (bot.py:272-497) for every bot, one
+// 64-lane wavefront per bot, plus the synthetic-population policy and the
+// per-player summary (player.py:129-167).
+//
+// Per bot: the FOV query runs on the field's centre-bucket grids with the
+// reference's exact bucket-footprint membership (spatialHashTable.py:70-83)
+// and isInFov (cell.py:169-177).  The per-bot float hash of the reference
+// (spatialHashTable.py:85-108, including the cols==12 quirk and the size-1
+// limit) is reproduced as a pair of 16-bit masks per object: the x- and
+// y-indices its accumulation loops visit; grid square t = r + c*G reads the
+// bucket id t, i.e. (t % cols, t / cols).  Visible objects are compacted into
+// LDS with ballot + prefix-sum; pellets are ranked by creation sequence so
+// every pellet-mass sum runs in the reference's order.
+#include <hip/hip_runtime.h>
+
+#include "aigar_dev.h"
+#include "aigar_sem.h"
+
+namespace aigar {
+
+#define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
+
+constexpr int OBS_PCAP = 512;  // visible pellets per bot kept in LDS
+constexpr int OBS_CCAP = 128;  // visible player cells
+constexpr int OBS_VCAP = 64;   // visible viruses
+
+struct Fov {
+  double fx, fy, fs, mass;
+  int n;
+};
+
+// getFovSize / getFovPos / getTotalMass for one player (sequential)
+__device__ Fov player_fov(const Dev &d, int gp) {
+  const int NP = d.NP;
+  Fov f;
+  int n = d.p_ncells[gp];
+  f.n = n;
+  double ms[kMaxCells], xs[kMaxCells], ys[kMaxCells];
+  double rb = -1;
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    double m = d.c_m[ci], r = d.c_r[ci];
+    ms[k] = m;
+    xs[k] = d.c_x[ci] * m;
+    ys[k] = d.c_y[ci] * m;
+    if (k == 0 || r > rb) rb = r;
+  }
+  f.mass = n ? np_sum(ms, n) : 0.0;
+  f.fs = aigar_math::pow_cr(rb, 0.475) * aigar_math::pow_cr((double)n, 0.32) * 35;
+  f.fx = np_sum(xs, n) / f.mass;
+  f.fy = np_sum(ys, n) / f.mass;
+  return f;
+}
+
+// x / y index masks of the reference's float-hash insertion loops
+__device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, double lim) {
+  double cl = py_max(0.0, p - r);
+  double bl = cl - py_mod(cl, gs);
+  double lx = py_min(lim, p + r);
+  uint32_t m = 0;
+  for (double x = bl; x <= lx; x += gs) m |= 1u << min(31, (int)(x / gs));
+  return m;
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// One list of visible objects (structure of arrays).  Lives in LDS; when a
+// bot sees more objects than the LDS list holds, the same scan is repeated
+// into a slice of the global overflow pool (exact, only slower).
+struct ObjList {
+  int64_t *seq;
+  double *m, *r;
+  uint32_t *mask;
+  uint8_t *own;
+  int *perm;
+};
+struct Cand {
+  bool keep;
+  int64_t seq;
+  double m, r;
+  uint32_t mask;
+  uint8_t own;
+};
+
+// wave-wide append (ballot + prefix count); *count keeps the true total
+__device__ __forceinline__ void list_append(const Cand &c, ObjList &L, int cap, int *count) {
+  unsigned long long bal = __ballot(c.keep);
+  int before = __popcll(bal & ((1ull << lane_id()) - 1));
+  int base = *count;
+  int slot = base + before;
+  __syncthreads();  // the block is one wavefront: a cheap s_barrier
+  if (lane_id() == 0) *count = base + __popcll(bal);
+  __syncthreads();
+  if (c.keep && slot < cap) {
+    if (L.seq) L.seq[slot] = c.seq;
+    if (L.m) L.m[slot] = c.m;
+    if (L.r) L.r[slot] = c.r;
+    L.mask[slot] = c.mask;
+    if (L.own) L.own[slot] = c.own;
+  }
+}
+
+// rows [by0, by1] x buckets [bx0, bx1] of a centre-bucket grid, one candidate per lane
+template <class F>
+__device__ __forceinline__ void scan_rows(const int *st, const int *items, int cols, Rect Q, int E, F f) {
+  if (Q.x1 < Q.x0 || Q.y1 < Q.y0) return;
+  int bx0 = max(0, Q.x0 - E), bx1 = min(cols - 1, Q.x1 + E);
+  int by0 = max(0, Q.y0 - E), by1 = min(cols - 1, Q.y1 + E);
+  for (int by = by0; by <= by1; by++) {
+    int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
+    for (int t0 = lo; t0 < hi; t0 += 64) {
+      int t = t0 + lane_id();
+      f(t < hi ? (items ? items[t] : t) : -1);
+    }
+  }
+}
+
+template <typename OutT>
+__global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
+  __shared__ int64_t p_seq[OBS_PCAP];
+  __shared__ double p_m[OBS_PCAP];
+  __shared__ uint32_t p_mask[OBS_PCAP];
+  __shared__ int p_perm[OBS_PCAP];
+  __shared__ double c_mass[OBS_CCAP];
+  __shared__ uint32_t c_mask[OBS_CCAP];
+  __shared__ uint8_t c_own[OBS_CCAP];
+  __shared__ double v_rad[OBS_VCAP], v_mass[OBS_VCAP];
+  __shared__ int64_t v_seqs[OBS_VCAP];
+  __shared__ uint32_t v_mask[OBS_VCAP];
+  __shared__ int cnt, gbase;
+  __shared__ Fov sf;
+
+  const int gp = blockIdx.x, lane = threadIdx.x;
+  const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
+  OutT *row = out + (size_t)gp * L;
+  if (!d.p_alive[gp]) {  // getStateRepresentation returns None for dead players
+    for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
+    return;
+  }
+  if (lane == 0) sf = player_fov(d, gp);
+  __syncthreads();
+  const double fx = sf.fx, fy = sf.fy, fs = sf.fs;
+  const double left = fx - fs / 2, top = fy - fs / 2, gs = fs / G;
+  const int cols = (int)ceil(fs / gs);
+  const double lim = fs - 1;
+  const Rect Q = footprint(fx, fy, fs / 2, d.size);
+  const ArenaCtl &ctl = d.ctl[a];
+
+  // collect(run, L, cap): run the scan into the LDS list; on overflow claim a
+  // slice of the global pool and rerun the scan into it.  Returns the count.
+  auto collect = [&](auto run, ObjList &Lst, int cap, ObjList G) -> int {
+    if (lane == 0) cnt = 0;
+    __syncthreads();
+    run(Lst, cap);
+    __syncthreads();
+    int n = cnt;
+    if (n <= cap) return n;
+    if (lane == 0) {
+      int b = atomicAdd(d.ob_used, n);
+      gbase = (b + n <= d.OBcap) ? b : -1;
+      if (gbase < 0) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
+      cnt = 0;
+    }
+    __syncthreads();
+    if (gbase < 0) return 0;
+    ObjList Gl = G;
+    int b = gbase;
+    if (Gl.seq) Gl.seq += b;
+    if (Gl.m) Gl.m += b;
+    if (Gl.r) Gl.r += b;
+    Gl.mask += b;
+    if (Gl.own) Gl.own += b;
+    if (Gl.perm) Gl.perm += b;
+    run(Gl, n);
+    __syncthreads();
+    Lst = Gl;
+    return n;
+  };
+  const ObjList Gpool{d.ob_seq, d.ob_m, d.ob_r, d.ob_mask, d.ob_own, d.ob_perm};
+
+  // ---- pellets: getPelletsInFov (field.py:442-444) -> float hash
+  ObjList PL{p_seq, p_m, nullptr, p_mask, nullptr, p_perm};
+  int np = 0;
+  if (d.obs_ch & AIGAR_OBS_PELLET) {
+    const int *st = d.pstart + (size_t)a * (d.H + 1);
+    auto run = [&](ObjList &Lst, int cap) {
+      scan_rows(st, nullptr, d.cols, Q, 1, [&](int t) {
+        Cand c{false, 0, 0, 0, 0, 0};
+        if (t >= 0) {
+          size_t g = (size_t)a * d.Pcap + t;
+          double px = d.pel_x[0][g], py = d.pel_y[0][g], pm = d.pel_m[0][g];
+          double pr = radius_of(pm);
+          if (rect_hit(footprint(px, py, pr, d.size), Q) && in_fov(px, py, pr, fx, fy, fs)) {
+            uint32_t ix = axis_mask(px - left, pr, gs, lim), iy = axis_mask(py - top, pr, gs, lim);
+            if (ix && iy) c = Cand{true, d.pel_seq[0][g], pm, pr, ix | (iy << 16), 0};
+          }
+        }
+        list_append(c, Lst, cap, &cnt);
+      });
+    };
+    np = collect(run, PL, OBS_PCAP, ObjList{Gpool.seq, Gpool.m, nullptr, Gpool.mask, nullptr, Gpool.perm});
+  }
+  // ---- cells: own (getPortionOfCellsInFov(player.getCells())) then enemies in the
+  // player hash (getEnemyPlayerCellsInFov, field.py:434-436)
+  ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
+  int nc;
+  {
+    const int *st = d.cstart + (size_t)a * (d.H + 1);
+    const int *it = d.citems + (size_t)a * kMaxCells * d.B;
+    int E = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
+    auto run = [&](ObjList &Lst, int cap) {
+      Cand c{false, 0, 0, 0, 0, 1};
+      if (lane < sf.n) {
+        size_t ci = (size_t)d.p_list[lane * NP + gp] * NP + gp;
+        double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci];
+        if (in_fov(x, y, r, fx, fy, fs)) {
+          uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
+          if (ix && iy) c = Cand{true, 0, d.c_m[ci], r, ix | (iy << 16), 1};
+        }
+      }
+      list_append(c, Lst, cap, &cnt);
+      scan_rows(st, it, d.cols, Q, E, [&](int e) {
+        Cand q{false, 0, 0, 0, 0, 0};
+        if (e >= 0 && (d.c_flags[e] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && (e % NP) != gp) {
+          double x = d.c_x[e], y = d.c_y[e], r = d.c_r[e];
+          if (rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs)) {
+            uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
+            if (ix && iy) q = Cand{true, 0, d.c_m[e], r, ix | (iy << 16), 0};
+          }
+        }
+        list_append(q, Lst, cap, &cnt);
+      });
+    };
+    nc = collect(run, CL, OBS_CCAP, ObjList{nullptr, Gpool.m, nullptr, Gpool.mask, Gpool.own, nullptr});
+  }
+  // ---- viruses: getVirusesInFov (virus hash members only)
+  ObjList VL{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
+  int nv = 0;
+  if (d.virus_enabled) {
+    const int *st = d.vstart + (size_t)a * (d.H + 1);
+    const int *it = d.vitems + (size_t)a * d.Vcap;
+    int E = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
+    auto run = [&](ObjList &Lst, int cap) {
+      scan_rows(st, it, d.cols, Q, E, [&](int j) {
+        Cand c{false, 0, 0, 0, 0, 0};
+        if (j >= 0) {
+          size_t g = (size_t)a * d.Vcap + j;
+          if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH)) {
+            double x = d.v_x[g], y = d.v_y[g], vr = d.v_r[g];
+            if (rect_hit(footprint(x, y, vr, d.size), Q) && in_fov(x, y, vr, fx, fy, fs)) {
+              uint32_t ix = axis_mask(x - left, vr, gs, lim), iy = axis_mask(y - top, vr, gs, lim);
+              if (ix && iy) c = Cand{true, d.v_seq[g], d.v_m[g], vr, ix | (iy << 16), 0};
+            }
+          }
+        }
+        list_append(c, Lst, cap, &cnt);
+      });
+    };
+    nv = collect(run, VL, OBS_VCAP, ObjList{Gpool.seq, Gpool.m, Gpool.r, Gpool.mask, nullptr, nullptr});
+  }
+  // rank pellets by creation sequence (the sum order of the reference)
+  for (int i = lane; i < np; i += 64) {
+    int64_t sq = PL.seq[i];
+    int rk = 0;
+    for (int j = 0; j < np; j++) rk += (PL.seq[j] < sq);
+    PL.perm[rk] = i;
+  }
+  __syncthreads();
+
+  // ---- per grid square (bot.py:387-456); lane owns squares t = lane + 64*j
+  const uint32_t ch = d.obs_ch;
+  const double fieldSize = (double)d.size;
+  int off = 0;
+  int o_pel = -1, o_self = -1, o_wall = -1, o_enemy = -1, o_all = -1, o_vir = -1;
+  int o_sslf = -1, o_slf = -1, o_eslf = -1, o_elf = -1;
+  if (ch & AIGAR_OBS_PELLET) { o_pel = off; off += GG; }
+  if (ch & AIGAR_OBS_SELF) { o_self = off; off += GG; }
+  if (ch & AIGAR_OBS_WALL) { o_wall = off; off += GG; }
+  if (ch & AIGAR_OBS_ENEMY) { o_enemy = off; off += GG; }
+  if (ch & AIGAR_OBS_ALL) { o_all = off; off += GG; }
+  if (ch & AIGAR_OBS_VIRUS) { o_vir = off; off += GG; }
+  if (ch & AIGAR_OBS_SELF_SLF) { o_sslf = off; off += GG; }
+  if (ch & AIGAR_OBS_SELF_LF) { o_slf = off; off += GG; }
+  if (ch & AIGAR_OBS_ENEMY_SLF) { o_eslf = off; off += GG; }
+  if (ch & AIGAR_OBS_ENEMY_LF) { o_elf = off; off += GG; }
+  double *slf = d.o_self_lf + (size_t)gp * GG, *sslf = d.o_self_slf + (size_t)gp * GG;
+  double *elf = d.o_en_lf + (size_t)gp * GG, *eslf = d.o_en_slf + (size_t)gp * GG;
+  for (int t = lane; t < GG; t += 64) {
+    int c = t / G, r = t - c * G;
+    double mx = left + gs / 2, my = top + gs / 2;
+    for (int i = 0; i < r; i++) mx += gs;
+    for (int i = 0; i < c; i++) my += gs;
+    int ix = t % cols, iy = t / cols;
+    uint32_t need = (1u << ix) | (1u << (16 + iy));
+    double vp = 0, ve = 0, vs = 0, vv = 0;
+    bool within = !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
+    if (within && ix < 16) {
+      double s = 0;
+      bool anyp = false;
+      for (int k = 0; k < np; k++) {
+        int e = PL.perm[k];
+        if ((PL.mask[e] & need) == need) {
+          s += PL.m[e];
+          anyp = true;
+        }
+      }
+      if (anyp) vp = s;
+      bool fe = false, fo = false;
+      for (int k = 0; k < nc; k++) {
+        if ((CL.mask[k] & need) != need) continue;
+        double m = CL.m[k];
+        if (CL.own[k]) {
+          if (!fo || m > vs) vs = m;
+          fo = true;
+        } else {
+          if (!fe || m > ve) ve = m;
+          fe = true;
+        }
+      }
+      bool fv = false;
+      double br = 0;
+      int64_t bs = 0;
+      for (int k = 0; k < nv; k++) {
+        if ((VL.mask[k] & need) != need) continue;
+        double rr = VL.r[k];
+        if (!fv || rr > br || (rr == br && VL.seq[k] < bs)) {
+          br = rr;
+          bs = VL.seq[k];
+          vv = VL.m[k];
+        }
+        fv = true;
+      }
+    }
+    double lb = py_min(py_max(mx - gs / 2, 0.0), fieldSize), tb = py_min(py_max(my - gs / 2, 0.0), fieldSize);
+    double rb = py_max(py_min(mx + gs / 2, fieldSize), 0.0), bb = py_max(py_min(my + gs / 2, fieldSize), 0.0);
+    double freeA = (rb - lb) * (bb - tb);
+    double vw = py_round3(1 - (freeA / (gs * gs)));
+    if (o_pel >= 0) row[o_pel + t] = (OutT)vp;
+    if (o_self >= 0) row[o_self + t] = (OutT)vs;
+    if (o_wall >= 0) row[o_wall + t] = (OutT)vw;
+    if (o_enemy >= 0) row[o_enemy + t] = (OutT)ve;
+    if (o_all >= 0) row[o_all + t] = (OutT)py_max(ve, vs);
+    if (o_vir >= 0) row[o_vir + t] = (OutT)vv;
+    if (o_sslf >= 0) {
+      row[o_sslf + t] = (OutT)sslf[t];
+      sslf[t] = slf[t];
+    }
+    if (o_slf >= 0) {
+      row[o_slf + t] = (OutT)slf[t];
+      slf[t] = vs;
+    }
+    if (o_eslf >= 0) {
+      row[o_eslf + t] = (OutT)eslf[t];
+      eslf[t] = elf[t];
+    }
+    if (o_elf >= 0) {
+      row[o_elf + t] = (OutT)elf[t];
+      elf[t] = ve;
+    }
+  }
+  if (lane == 0) {  // getAdditionalFeatures (bot.py:302-323)
+    const uint32_t ex = d.obs_ex;
+    int o = off;
+    if (ex & AIGAR_EX_LAST_FOV) row[o++] = (OutT)d.o_lastfov[gp];
+    if (ex & AIGAR_EX_FOV) {
+      d.o_lastfov[gp] = fs;
+      row[o++] = (OutT)fs;
+    }
+    if (ex & AIGAR_EX_MASS) row[o++] = (OutT)sf.mass;
+    if (ex & AIGAR_EX_LAST_ACT)
+      for (int k = 0; k < 4; k++) row[o++] = (OutT)d.o_act_cur[(size_t)gp * 4 + k];
+    if (ex & AIGAR_EX_2LAST_ACT)
+      for (int k = 0; k < 4; k++) row[o++] = (OutT)d.o_act_prev[(size_t)gp * 4 + k];
+  }
+}
+
+// synthetic bot population: random action in [0,1]^2 through set_command_point
+// (bot.py:550-577), split/eject with the given probabilities
+__global__ void k_policy_random(Dev d, double p_split, double p_eject, uint64_t salt) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  int a = gp / d.B;
+  Fov f = player_fov(d, gp);
+  uint64_t u[4];
+  philox((uint64_t)gp, ST_POLICY, (uint64_t)d.ctl[a].tick, salt, d.ctl[a].key0, d.ctl[a].key1, u);
+  double a0 = u01(u[0]), a1 = u01(u[1]);
+  int64_t x = (int64_t)f.fx, y = (int64_t)f.fy;
+  int64_t left = x - (int64_t)(f.fs / 2), top = y - (int64_t)(f.fs / 2);
+  int64_t size = (int64_t)f.fs;
+  d.p_cmdx[gp] = (double)left + a0 * (double)size;
+  d.p_cmdy[gp] = (double)top + a1 * (double)size;
+  d.p_split[gp] = u01(u[2]) < p_split;
+  d.p_eject[gp] = u01(u[3]) < p_eject;
+}
+
+__global__ void k_player_stats(Dev d, double *out) {
+  int gp = GTID;
+  if (gp >= d.NP) return;
+  double *o = out + (size_t)gp * 5;
+  if (!d.p_alive[gp]) {
+    o[0] = 0;
+    o[1] = 0;
+    o[2] = o[3] = o[4] = __builtin_nan("");
+    return;
+  }
+  Fov f = player_fov(d, gp);
+  o[0] = 1;
+  o[1] = f.mass;
+  o[2] = f.fx;
+  o[3] = f.fy;
+  o[4] = f.fs;
+}
+
+__global__ void k_set_commands(Dev d, const double *cmd) {
+  int gp = GTID;
+  if (gp >= d.NP) return;
+  d.p_cmdx[gp] = cmd[4 * (size_t)gp];
+  d.p_cmdy[gp] = cmd[4 * (size_t)gp + 1];
+  d.p_split[gp] = cmd[4 * (size_t)gp + 2] != 0;
+  d.p_eject[gp] = cmd[4 * (size_t)gp + 3] != 0;
+}
+
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype) {
+  (void)hipMemsetAsync(d.ob_used, 0, sizeof(int), s);
+  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out);
+  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out);
+}
+void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt) {
+  hipLaunchKernelGGL(k_policy_random, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, ps, pe, salt);
+}
+void launch_player_stats(const Dev &d, hipStream_t s, double *out) {
+  hipLaunchKernelGGL(k_player_stats, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, out);
+}
+void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd) {
+  hipLaunchKernelGGL(k_set_commands, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, cmd);
+}
+
+}  // namespace aigar

@@ -1,0 +1,1568 @@
+// tick.hip -- Field.update() (field.py:85-92) as a sequence of gfx950 kernels.
+//
+// Phase map (kernel <- reference):
+//   k_update_viruses          updateViruses            field.py:94-97
+//   k_update_blobs            updateBlobs              field.py:99-110
+//   k_update_players          updatePlayers + Player.update + performEjections
+//                             + handlePlayerCollisions field.py:112-181, player.py:30-72
+//   k_scan_players/finalize   creation-sequence numbers (canonical order) + blob append
+//   grid builds               updateHashTables         field.py:121-132 (centre-bucket
+//                             counting sort; membership is tested exactly per query)
+//   k_merge                   mergePlayerCells         field.py:183-198
+//   k_vb_*                    virusBlobOverlap         field.py:246-253, 316-325
+//   k_pv_*                    playerVirusOverlap       field.py:225-231, 333-370
+//   k_food_*  (pellets/blobs) playerPelletOverlap / playerBlobOverlap field.py:207-222
+//                             parallel "deterministic reservations": each cell reserves
+//                             the foods it could ever eat; a cell commits once it owns
+//                             them all (=> every earlier conflicting cell has committed);
+//                             leftovers run serially in priority order.
+//   k_pp_*                    playerPlayerOverlap      field.py:233-244
+//                             parallel activity test, then one thread per arena walks
+//                             the active players in order (live-list semantics incl.
+//                             skip-after-removal), re-activating neighbours on growth.
+//   k_spawn_*                 spawnStuff               field.py:256-313
+#include <hip/hip_runtime.h>
+
+#include "aigar_dev.h"
+#include "aigar_sem.h"
+
+namespace aigar {
+
+#define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
+
+__device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { atomicOr(&d.ctl[a].err, bit); }
+
+__device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int code, int64_t x, int64_t y) {
+  if (!(d.flags & 1)) return;
+  int i = atomicAdd(&d.ctl[a].n_ev, 1);
+  if (i >= d.EVcap) {
+    set_err(d, a, ERR_EVENT_CAP);
+    return;
+  }
+  int64_t *e = d.ev + ((size_t)a * d.EVcap + i) * 5;
+  e[0] = (d.ctl[a].tick << 8) | phase;
+  e[1] = (int64_t)order;
+  e[2] = code;
+  e[3] = x;
+  e[4] = y;
+}
+
+__device__ __forceinline__ void atomic_max_pos(double *addr, double v) {  // v >= 0
+  atomicMax((unsigned long long *)addr, (unsigned long long)__double_as_longlong(v));
+}
+
+// centre-bucket grid iteration: every entity whose centre bucket lies in the
+// query rectangle grown by E buckets (E covers the largest footprint).
+template <class F>
+__device__ __forceinline__ void grid_visit(const int *start, const int *items, int cols, Rect q, int E, F f) {
+  if (q.x1 < q.x0 || q.y1 < q.y0) return;
+  int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
+  int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
+  for (int by = by0; by <= by1; by++) {
+    int lo = start[by * cols + bx0], hi = start[by * cols + bx1 + 1];
+    for (int t = lo; t < hi; t++) f(items ? items[t] : t);
+  }
+}
+__device__ __forceinline__ int expand_for(double rmax) { return (int)ceil((rmax + 1.0) / kBucket) + 1; }
+
+// ------------------------------------------------------------ T1 viruses
+__global__ void k_update_viruses(Dev d) {
+  int gi = GTID;
+  if (gi >= d.A * d.Vcap) return;
+  int a = gi / d.Vcap, i = gi - a * d.Vcap;
+  if (i >= d.ctl[a].n_vir || !(d.v_flags[gi] & F_ALIVE)) return;
+  int svc = d.v_svc[gi];
+  double svx = d.v_svx[gi], svy = d.v_svy[gi], x = d.v_x[gi], y = d.v_y[gi];
+  update_momentum(svc, svx, svy);
+  update_pos(x, y, d.v_vx[gi], d.v_vy[gi], svx, svy, svc, (double)d.size, (double)d.size);
+  d.v_svc[gi] = svc;
+  d.v_svx[gi] = svx;
+  d.v_svy[gi] = svy;
+  d.v_x[gi] = x;
+  d.v_y[gi] = y;
+  d.v_flags[gi] |= F_INHASH;  // updateHashTables (later this tick) inserts every virus
+}
+
+// ------------------------------------------------------------ T2 blobs
+__global__ void k_update_blobs(Dev d) {
+  int gi = GTID;
+  if (gi >= d.A * d.Ecap) return;
+  int a = gi / d.Ecap, i = gi - a * d.Ecap;
+  if (i >= d.ctl[a].n_blob || !(d.b_flags[gi] & F_ALIVE)) return;
+  if (d.b_svc[gi] == 0) {  // stopped blob becomes a pellet (addPellet)
+    int j = atomicAdd(&d.ctl[a].n_pnew, 1);
+    if (j >= d.Pcap) {
+      set_err(d, a, ERR_PELLET_CAP);
+      return;
+    }
+    size_t pj = (size_t)a * d.Pcap + j;
+    d.pn_x[pj] = d.b_x[gi];
+    d.pn_y[pj] = d.b_y[gi];
+    d.pn_m[pj] = d.b_m[gi];
+    d.pn_seq[pj] = d.b_seq[gi];
+    d.b_flags[gi] = 0;
+    return;
+  }
+  int svc = d.b_svc[gi];
+  double svx = d.b_svx[gi], svy = d.b_svy[gi], x = d.b_x[gi], y = d.b_y[gi];
+  update_momentum(svc, svx, svy);
+  update_pos(x, y, d.b_vx[gi], d.b_vy[gi], svx, svy, svc, (double)d.size, (double)d.size);
+  d.b_svc[gi] = svc;
+  d.b_svx[gi] = svx;
+  d.b_svy[gi] = svy;
+  d.b_x[gi] = x;
+  d.b_y[gi] = y;
+}
+
+// ------------------------------------------------------------ T4 players
+__global__ void __launch_bounds__(256) k_update_players(Dev d) {
+  int gp = GTID;
+  if (gp >= d.NP) return;
+  const int NP = d.NP;
+  d.p_newc[gp] = 0;
+  d.p_newb[gp] = 0;
+  if (!d.p_alive[gp]) {  // updateRespawnTime (player.py:74-75)
+    d.p_respawn[gp] -= 1;
+    return;
+  }
+  const double W = (double)d.size;
+  const double cpx = d.p_cmdx[gp], cpy = d.p_cmdy[gp];
+  int n = d.p_ncells[gp];
+  uint8_t lst[kMaxCells];
+  for (int k = 0; k < n; k++) lst[k] = d.p_list[k * NP + gp];
+  // Player.decayMass -> Cell.decayMass (cell.py:123-126)
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)lst[k] * NP + gp;
+    double m = d.c_m[ci];
+    if (m >= 4) {
+      m = m * kDecay;
+      d.c_m[ci] = m;
+      d.c_r[ci] = radius_of(m);
+    }
+  }
+  // updateCellProperties: momentum, merge timer, direction (player.py:39-44)
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)lst[k] * NP + gp;
+    int svc = d.c_svc[ci];
+    double svx = d.c_svx[ci], svy = d.c_svy[ci];
+    update_momentum(svc, svx, svy);
+    d.c_svc[ci] = svc;
+    d.c_svx[ci] = svx;
+    d.c_svy[ci] = svy;
+    double mt = d.c_mt[ci];
+    if (mt > 0) d.c_mt[ci] = mt - 1;
+    double vx, vy;
+    set_move_direction(d.c_x[ci], d.c_y[ci], d.c_m[ci], d.c_r[ci], cpx, cpy, vx, vy);
+    d.c_vx[ci] = vx;
+    d.c_vy[ci] = vy;
+  }
+  int n_new = 0;
+  if (d.p_split[gp]) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
+    for (int i = 1; i < n; i++) {
+      uint8_t key = lst[i];
+      double km = d.c_m[(size_t)key * NP + gp];
+      int j = i - 1;
+      while (j >= 0 && km > d.c_m[(size_t)lst[j] * NP + gp]) {
+        lst[j + 1] = lst[j];
+        j--;
+      }
+      lst[j + 1] = key;
+    }
+    uint32_t used = 0;
+    for (int k = 0; k < n; k++) used |= 1u << lst[k];
+    int n0 = n;
+    uint8_t snap[kMaxCells];
+    for (int k = 0; k < n0; k++) snap[k] = lst[k];
+    for (int k = 0; k < n0; k++) {
+      size_t ci = (size_t)snap[k] * NP + gp;
+      if (!(d.c_m[ci] > 36 && n < kMaxCells)) continue;
+      int slot = __ffs(~used) - 1;
+      used |= 1u << slot;
+      size_t ni = (size_t)slot * NP + gp;
+      // Cell.split (cell.py:72-85)
+      double x = d.c_x[ci], y = d.c_y[ci];
+      double nm = d.c_m[ci] / 2, nr = radius_of(nm);
+      double ang = atan2(cpy - y, cpx - x);
+      double ca = cos(ang);
+      double sa = sin(ang);
+      double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
+      double svx, svy;
+      int svc;
+      add_momentum(x, y, xp, yp, W, W, d.c_r[ci], svx, svy, svc);
+      d.c_x[ni] = x;
+      d.c_y[ni] = y;
+      d.c_m[ni] = nm;
+      d.c_r[ni] = nr;
+      d.c_vx[ni] = 0;
+      d.c_vy[ni] = 0;
+      d.c_svx[ni] = svx;
+      d.c_svy[ni] = svy;
+      d.c_svc[ni] = svc;
+      d.c_mt[ni] = merge_time_for(1, nm);
+      d.c_flags[ni] = F_ALIVE | F_NEW;
+      double pm = d.c_m[ci] / 2;
+      d.c_m[ci] = pm;
+      d.c_r[ci] = radius_of(pm);
+      lst[n++] = (uint8_t)slot;
+      n_new++;
+    }
+  }
+  if (d.p_eject[gp])  // Player.eject (player.py:54-58)
+    for (int k = 0; k < n; k++) {
+      size_t ci = (size_t)lst[k] * NP + gp;
+      if (d.c_m[ci] >= 35) d.c_flags[ci] |= F_EJECT;
+    }
+  for (int k = 0; k < n; k++) {  // updateCellsMovement
+    size_t ci = (size_t)lst[k] * NP + gp;
+    double x = d.c_x[ci], y = d.c_y[ci], svx = d.c_svx[ci], svy = d.c_svy[ci];
+    update_pos(x, y, d.c_vx[ci], d.c_vy[ci], svx, svy, d.c_svc[ci], W, W);
+    d.c_x[ci] = x;
+    d.c_y[ci] = y;
+    d.c_svx[ci] = svx;
+    d.c_svy[ci] = svy;
+  }
+  int nb = 0;
+  for (int k = 0; k < n; k++) {  // performEjections (field.py:134-146)
+    size_t ci = (size_t)lst[k] * NP + gp;
+    if (!(d.c_flags[ci] & F_EJECT)) continue;
+    d.c_m[ci] = d.c_m[ci] - kEjectMass;  // Cell.eject: radius stays stale (cell.py:90-94)
+    d.c_flags[ci] &= ~F_EJECT;
+    double bx = d.c_x[ci], by = d.c_y[ci], svx, svy;
+    int svc;
+    add_momentum(bx, by, cpx, cpy, W, W, d.c_r[ci], svx, svy, svc);
+    size_t si = (size_t)nb * NP + gp;
+    d.sb_x[si] = bx;
+    d.sb_y[si] = by;
+    d.sb_svx[si] = svx;
+    d.sb_svy[si] = svy;
+    d.sb_slot[si] = lst[k];
+    nb++;
+  }
+  for (int i = 0; i < n; i++) {  // handlePlayerCollisions (field.py:149-159)
+    size_t ci = (size_t)lst[i] * NP + gp;
+    if (d.c_svc[ci] > 0) continue;
+    for (int j = 0; j < n; j++) {
+      size_t cj = (size_t)lst[j] * NP + gp;
+      if (i == j || d.c_svc[cj] > 0 || (d.c_mt[ci] <= 0 && d.c_mt[cj] <= 0)) continue;
+      double x1 = d.c_x[ci], y1 = d.c_y[ci], x2 = d.c_x[cj], y2 = d.c_y[cj];
+      double dist = sqrt((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2));
+      double sr = d.c_r[ci] + d.c_r[cj];
+      if (dist < sr && dist != 0) {  // adjustCellPositions (field.py:161-181)
+        bool one_big = d.c_m[ci] > d.c_m[cj];
+        size_t bi = one_big ? ci : cj, si = one_big ? cj : ci;
+        double bx = d.c_x[bi], by = d.c_y[bi], sx = d.c_x[si], sy = d.c_y[si];
+        double ds = (sr - dist) / dist, mds = d.c_m[si] / d.c_m[bi];
+        double xd = (bx - sx) * ds, yd = (by - sy) * ds;
+        double nbx = bx + xd * mds, nby = by + yd * mds;
+        double nsx = sx - xd * (1 - mds), nsy = sy - yd * (1 - mds);
+        d.c_x[bi] = py_min(W, py_max(0.0, nbx));
+        d.c_y[bi] = py_min(W, py_max(0.0, nby));
+        d.c_x[si] = py_min(W, py_max(0.0, nsx));
+        d.c_y[si] = py_min(W, py_max(0.0, nsy));
+      }
+    }
+  }
+  for (int k = 0; k < n; k++) d.p_list[k * NP + gp] = lst[k];
+  d.p_ncells[gp] = n;
+  d.p_newc[gp] = n_new;
+  d.p_newb[gp] = nb;
+}
+
+// block-wide exclusive scan of a[0..n) into out (1024 threads); returns total
+__device__ int block_scan_excl(const int *in, int *out, int n, int *sh) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  int per = (n + T - 1) / T, lo = min(n, tid * per), hi = min(n, lo + per);
+  int s = 0;
+  for (int i = lo; i < hi; i++) s += in[i];
+  sh[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < T; off <<= 1) {  // Hillis-Steele over per-thread sums
+    int v = (tid >= off) ? sh[tid - off] : 0;
+    __syncthreads();
+    sh[tid] += v;
+    __syncthreads();
+  }
+  int run = sh[tid] - s;
+  int total = sh[T - 1];
+  for (int i = lo; i < hi; i++) {
+    int v = in[i];
+    out[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+// ------------------------------------------------------------ T5/T6
+__global__ void __launch_bounds__(1024) k_scan_players(Dev d) {
+  __shared__ int sh[1024];
+  int a = blockIdx.x;
+  const int B = d.B, base = a * B;
+  // p_newc + p_newb -> seq offsets; p_newb -> blob offsets (use p_seqoff as temp for the sum)
+  for (int p = threadIdx.x; p < B; p += blockDim.x) d.p_seqoff[base + p] = d.p_newc[base + p] + d.p_newb[base + p];
+  __syncthreads();
+  int tot = block_scan_excl(d.p_seqoff + base, d.p_seqoff + base, B, sh);
+  int totb = block_scan_excl(d.p_newb + base, d.p_bloboff + base, B, sh);
+  if (threadIdx.x == 0) {
+    ArenaCtl &c = d.ctl[a];
+    c.seq_base_upd = c.seq_next;
+    c.seq_next += tot;
+    c.n_blob_base = c.n_blob;
+    if (c.n_blob + totb > d.Ecap) {
+      c.err |= ERR_BLOB_CAP;
+      c.n_blob = d.Ecap;
+    } else {
+      c.n_blob += totb;
+    }
+  }
+}
+
+__global__ void k_finalize_players(Dev d) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B;
+  const ArenaCtl &c = d.ctl[a];
+  int n = d.p_ncells[gp], nn = d.p_newc[gp], nb = d.p_newb[gp];
+  int64_t s0 = c.seq_base_upd + d.p_seqoff[gp];
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    if (k >= n - nn) d.c_seq[ci] = s0 + (k - (n - nn));
+    d.c_flags[ci] = (d.c_flags[ci] & ~F_NEW) | F_INHASH;  // updateHashTables inserts every cell
+  }
+  for (int j = 0; j < nb; j++) {
+    int bi = c.n_blob_base + d.p_bloboff[gp] + j;
+    if (bi >= d.Ecap) return;  // ERR_BLOB_CAP already set
+    size_t g = (size_t)a * d.Ecap + bi, si = (size_t)j * NP + gp;
+    const double bm = kEjectMass * 0.8;
+    d.b_x[g] = d.sb_x[si];
+    d.b_y[g] = d.sb_y[si];
+    d.b_m[g] = bm;
+    d.b_r[g] = radius_of(bm);
+    d.b_vx[g] = 0;
+    d.b_vy[g] = 0;
+    d.b_svx[g] = d.sb_svx[si];
+    d.b_svy[g] = d.sb_svy[si];
+    d.b_svc[g] = 15;
+    d.b_seq[g] = s0 + nn + j;
+    d.b_ej[g] = d.c_seq[(size_t)d.sb_slot[si] * NP + gp];
+    d.b_flags[g] = F_ALIVE;
+  }
+}
+
+// ------------------------------------------------------------ grids
+// generic counting sort by centre bucket. kind: 0 cells (pool), 1 blobs, 2 viruses
+template <int KIND>
+__global__ void k_grid_count(Dev d) {
+  int gi = GTID;
+  int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
+  if (gi >= d.A * per) return;
+  int a = gi / per, i = gi - a * per;
+  double x, y, r;
+  int *rank;
+  int *cnt;
+  size_t g;
+  if (KIND == 0) {
+    int slot = i / d.B, p = i - slot * d.B;
+    g = (size_t)slot * d.NP + (size_t)a * d.B + p;
+    if (!(d.c_flags[g] & F_ALIVE)) return;
+    x = d.c_x[g];
+    y = d.c_y[g];
+    r = d.c_r[g];
+    rank = d.c_rank;
+    cnt = d.ccnt;
+    atomic_max_pos(&d.ctl[a].rmax_cell, r);
+  } else if (KIND == 1) {
+    g = (size_t)a * d.Ecap + i;
+    if (i >= d.ctl[a].n_blob || !(d.b_flags[g] & F_ALIVE)) return;
+    x = d.b_x[g];
+    y = d.b_y[g];
+    rank = d.b_rank;
+    cnt = d.bcnt;
+  } else {
+    g = (size_t)a * d.Vcap + i;
+    if (i >= d.ctl[a].n_vir || !(d.v_flags[g] & F_ALIVE)) return;
+    x = d.v_x[g];
+    y = d.v_y[g];
+    r = d.v_r[g];
+    rank = d.v_rank;
+    cnt = d.vcnt;
+    atomic_max_pos(&d.ctl[a].rmax_virus, r);
+  }
+  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+  rank[(size_t)a * per + i] = atomicAdd(&cnt[(size_t)a * (d.H + 1) + b], 1);
+}
+template <int KIND>
+__global__ void k_grid_scatter(Dev d) {
+  int gi = GTID;
+  int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
+  if (gi >= d.A * per) return;
+  int a = gi / per, i = gi - a * per;
+  double x, y;
+  int *rank, *start, *items;
+  int val;
+  if (KIND == 0) {
+    int slot = i / d.B, p = i - slot * d.B;
+    size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
+    if (!(d.c_flags[g] & F_ALIVE)) return;
+    x = d.c_x[g];
+    y = d.c_y[g];
+    rank = d.c_rank;
+    start = d.cstart;
+    items = d.citems;
+    val = (int)g;
+  } else if (KIND == 1) {
+    size_t g = (size_t)a * d.Ecap + i;
+    if (i >= d.ctl[a].n_blob || !(d.b_flags[g] & F_ALIVE)) return;
+    x = d.b_x[g];
+    y = d.b_y[g];
+    rank = d.b_rank;
+    start = d.bstart;
+    items = d.bitems;
+    val = i;
+  } else {
+    size_t g = (size_t)a * d.Vcap + i;
+    if (i >= d.ctl[a].n_vir || !(d.v_flags[g] & F_ALIVE)) return;
+    x = d.v_x[g];
+    y = d.v_y[g];
+    rank = d.v_rank;
+    start = d.vstart;
+    items = d.vitems;
+    val = i;
+  }
+  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+  items[(size_t)a * per + start[(size_t)a * (d.H + 1) + b] + rank[(size_t)a * per + i]] = val;
+}
+// per-arena exclusive scan of H bucket counts into H+1 starts
+__global__ void __launch_bounds__(1024) k_grid_scan(Dev d, int *cnt, int *start) {
+  __shared__ int sh[1024];
+  int a = blockIdx.x;
+  size_t o = (size_t)a * (d.H + 1);
+  int tot = block_scan_excl(cnt + o, start + o, d.H, sh);
+  if (threadIdx.x == 0) start[o + d.H] = tot;
+}
+
+// pellet records: (src buffer [+ dead flags]) U staging -> dst buffer sorted by bucket
+__global__ void k_pgrid_count(Dev d, int src, int use_dead) {
+  int gi = GTID;
+  int per = 2 * d.Pcap;
+  if (gi >= d.A * per) return;
+  int a = gi / per, i = gi - a * per;
+  const ArenaCtl &c = d.ctl[a];
+  double x, y;
+  if (i < c.n_pel) {
+    size_t g = (size_t)a * d.Pcap + i;
+    if (use_dead && d.pel_dead[g]) return;
+    x = d.pel_x[src][g];
+    y = d.pel_y[src][g];
+  } else if (i - c.n_pel < c.n_pnew) {
+    size_t g = (size_t)a * d.Pcap + (i - c.n_pel);
+    x = d.pn_x[g];
+    y = d.pn_y[g];
+  } else {
+    return;
+  }
+  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+  d.pel_rank[(size_t)a * per + i] = atomicAdd(&d.pcnt[(size_t)a * (d.H + 1) + b], 1);
+}
+__global__ void k_pgrid_scatter(Dev d, int src, int use_dead) {
+  int gi = GTID;
+  int per = 2 * d.Pcap;
+  if (gi >= d.A * per) return;
+  int a = gi / per, i = gi - a * per;
+  const ArenaCtl &c = d.ctl[a];
+  double x, y, m;
+  int64_t s;
+  if (i < c.n_pel) {
+    size_t g = (size_t)a * d.Pcap + i;
+    if (use_dead && d.pel_dead[g]) return;
+    x = d.pel_x[src][g];
+    y = d.pel_y[src][g];
+    m = d.pel_m[src][g];
+    s = d.pel_seq[src][g];
+  } else if (i - c.n_pel < c.n_pnew) {
+    size_t g = (size_t)a * d.Pcap + (i - c.n_pel);
+    x = d.pn_x[g];
+    y = d.pn_y[g];
+    m = d.pn_m[g];
+    s = d.pn_seq[g];
+  } else {
+    return;
+  }
+  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+  int pos = d.pstart[(size_t)a * (d.H + 1) + b] + d.pel_rank[(size_t)a * per + i];
+  if (pos >= d.Pcap) {
+    set_err(d, a, ERR_PELLET_CAP);
+    return;
+  }
+  size_t o = (size_t)a * d.Pcap + pos;
+  int dst = src ^ 1;
+  d.pel_x[dst][o] = x;
+  d.pel_y[dst][o] = y;
+  d.pel_m[dst][o] = m;
+  d.pel_seq[dst][o] = s;
+  if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
+}
+__global__ void k_pgrid_finish(Dev d) {
+  int a = GTID;
+  if (a >= d.A) return;
+  ArenaCtl &c = d.ctl[a];
+  c.n_pel = d.pstart[(size_t)a * (d.H + 1) + d.H];
+  if (c.n_pel > d.Pcap) c.n_pel = d.Pcap;
+  c.n_pnew = 0;
+  c.n_pel_eaten = 0;
+}
+
+// ------------------------------------------------------------ T10 merge
+__global__ void k_merge(Dev d) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B;
+  int n = d.p_ncells[gp];
+  uint8_t cs[kMaxCells];
+  int nm = 0;
+  for (int k = 0; k < n; k++) {  // getMergableCells (player.py:144-149)
+    uint8_t s = d.p_list[k * NP + gp];
+    if (d.c_mt[(size_t)s * NP + gp] <= 0) cs[nm++] = s;
+  }
+  if (nm <= 1) return;
+  for (int i = 1; i < nm; i++) {  // stable sort by mass desc
+    uint8_t key = cs[i];
+    double km = d.c_m[(size_t)key * NP + gp];
+    int j = i - 1;
+    while (j >= 0 && km > d.c_m[(size_t)cs[j] * NP + gp]) {
+      cs[j + 1] = cs[j];
+      j--;
+    }
+    cs[j + 1] = key;
+  }
+  uint32_t order = 0;
+  for (int i = 0; i < nm; i++) {
+    size_t c1 = (size_t)cs[i] * NP + gp;
+    if (!(d.c_flags[c1] & F_ALIVE)) continue;
+    for (int j = 0; j < nm; j++) {
+      size_t c2 = (size_t)cs[j] * NP + gp;
+      if (!(d.c_flags[c2] & F_ALIVE) || c2 == c1) continue;
+      if (!overlap(d.c_x[c1], d.c_y[c1], d.c_m[c1], d.c_r[c1], d.c_x[c2], d.c_y[c2], d.c_m[c2], d.c_r[c2]))
+        continue;
+      // mergeCells (field.py:372-380)
+      bool first_big = d.c_m[c1] > d.c_m[c2];
+      size_t bi = first_big ? c1 : c2, si = first_big ? c2 : c1;
+      ev_push(d, a, PH_MERGE, ((uint64_t)(gp - a * d.B) << 20) | order++, 1, d.c_seq[bi], d.c_seq[si]);
+      double m = grow_mass(d.c_m[bi], d.c_m[si]);
+      d.c_m[bi] = m;
+      d.c_r[bi] = radius_of(m);
+      d.c_flags[si] = 0;  // deletePlayerCell: removeCell
+      uint8_t sslot = (uint8_t)(si / NP);
+      int cur = d.p_ncells[gp], w = 0;
+      for (int k = 0; k < cur; k++) {
+        uint8_t s = d.p_list[k * NP + gp];
+        if (s != sslot) d.p_list[(w++) * NP + gp] = s;
+      }
+      d.p_ncells[gp] = w;
+      if (!(d.c_flags[c1] & F_ALIVE)) break;
+    }
+  }
+}
+
+// ------------------------------------------------------------ serial-phase helpers
+// insertion sort of (key, val) pairs, single thread (worklists are short)
+__device__ void isort_kv(int64_t *key, int *val, int n) {
+  for (int i = 1; i < n; i++) {
+    int64_t k = key[i];
+    int v = val[i];
+    int j = i - 1;
+    while (j >= 0 && key[j] > k) {
+      key[j + 1] = key[j];
+      val[j + 1] = val[j];
+      j--;
+    }
+    key[j + 1] = k;
+    val[j + 1] = v;
+  }
+}
+
+// ------------------------------------------------------------ T11 virus <- blob
+__global__ void k_vb_active(Dev d) {
+  int gi = GTID;
+  if (gi >= d.A * d.Vcap) return;
+  int a = gi / d.Vcap, i = gi - a * d.Vcap;
+  if (i == 0) d.ctl[a].n_vir_start = d.ctl[a].n_vir;
+  if (i >= d.ctl[a].n_vir || !(d.v_flags[gi] & F_ALIVE)) return;
+  double vx = d.v_x[gi], vy = d.v_y[gi], vm = d.v_m[gi], vr = d.v_r[gi];
+  Rect q = footprint(vx, vy, vr, d.size);
+  bool any = false;
+  const int *st = d.bstart + (size_t)a * (d.H + 1);
+  const int *it = d.bitems + (size_t)a * d.Ecap;
+  grid_visit(st, it, d.cols, q, 1, [&](int j) {
+    size_t g = (size_t)a * d.Ecap + j;
+    if (any || !(d.b_flags[g] & F_ALIVE)) return;
+    if (!rect_hit(footprint(d.b_x[g], d.b_y[g], d.b_r[g], d.size), q)) return;
+    if (overlap(vx, vy, vm, vr, d.b_x[g], d.b_y[g], d.b_m[g], d.b_r[g])) any = true;
+  });
+  if (any) {
+    int w = atomicAdd(&d.ctl[a].n_pend, 1);
+    if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = i;
+    else set_err(d, a, ERR_WORK_CAP);
+  }
+}
+__global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
+  int a = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  ArenaCtl &c = d.ctl[a];
+  int nw = min(c.n_pend, d.Wcap);
+  c.n_pend = 0;
+  int *w = d.work + (size_t)a * d.Wcap;
+  int64_t *ck = scr_k + (size_t)a * d.Wcap;
+  int *cv = scr_v + (size_t)a * d.Wcap;
+  if (nw == 0) return;
+  // active viruses in list order; viruses appended by splits are visited too
+  for (int k = 0; k < nw; k++) ck[k] = w[k];
+  isort_kv(ck, w, nw);
+  const int *st = d.bstart + (size_t)a * (d.H + 1);
+  const int *it = d.bitems + (size_t)a * d.Ecap;
+  int wk = 0;
+  uint64_t order = 0;
+  const double thr = kVirusBase + 7 * kEjectMass * 0.8;
+  for (int i = w[0]; i < c.n_vir; i++) {
+    if (i < c.n_vir_start) {
+      if (wk < nw && w[wk] == i) wk++;
+      else continue;
+    }
+    size_t gv = (size_t)a * d.Vcap + i;
+    double vx = d.v_x[gv], vy = d.v_y[gv];
+    Rect q = footprint(vx, vy, d.v_r[gv], d.size);
+    int nc = 0;
+    grid_visit(st, it, d.cols, q, 1, [&](int j) {
+      size_t g = (size_t)a * d.Ecap + j;
+      if (!(d.b_flags[g] & F_ALIVE)) return;
+      if (!rect_hit(footprint(d.b_x[g], d.b_y[g], d.b_r[g], d.size), q)) return;
+      if (nc < d.Wcap) {
+        ck[nc] = d.b_seq[g];
+        cv[nc] = j;
+        nc++;
+      }
+    });
+    isort_kv(ck, cv, nc);
+    for (int t = 0; t < nc; t++) {
+      size_t g = (size_t)a * d.Ecap + cv[t];
+      if (!(d.b_flags[g] & F_ALIVE)) continue;
+      if (!overlap(d.v_x[gv], d.v_y[gv], d.v_m[gv], d.v_r[gv], d.b_x[g], d.b_y[g], d.b_m[g], d.b_r[g])) continue;
+      if (i >= c.n_vir_start) c.warn |= WARN_NEW_VIRUS_EATS;  // reference: deleteObject raises
+      ev_push(d, a, PH_VB, order++, 2, d.v_seq[gv], d.b_seq[g]);
+      double m = grow_mass(d.v_m[gv], d.b_m[g]);
+      d.v_m[gv] = m;
+      d.v_r[gv] = radius_of(m);
+      c.rmax_virus = fmax(c.rmax_virus, d.v_r[gv]);
+      d.b_flags[g] = 0;
+      if (m >= thr) {  // virus split (field.py:318-325, cell.py:72-85)
+        if (c.n_vir >= d.Vcap) {
+          c.err |= ERR_VIRUS_CAP;
+          continue;
+        }
+        double ox = 2 * d.v_x[gv] - d.b_x[g], oy = 2 * d.v_y[gv] - d.b_y[g];
+        size_t gn = (size_t)a * d.Vcap + c.n_vir;
+        double x = d.v_x[gv], y = d.v_y[gv], nm = m / 2, nr = radius_of(nm);
+        double ang = atan2(oy - y, ox - x);
+        double ca = cos(ang);
+        double sa = sin(ang);
+        double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
+        double svx, svy;
+        int svc;
+        add_momentum(x, y, xp, yp, (double)d.size, (double)d.size, d.v_r[gv], svx, svy, svc);
+        d.v_x[gn] = x;
+        d.v_y[gn] = y;
+        d.v_m[gn] = nm;
+        d.v_r[gn] = nr;
+        d.v_vx[gn] = 0;
+        d.v_vy[gn] = 0;
+        d.v_svx[gn] = svx;
+        d.v_svy[gn] = svy;
+        d.v_svc[gn] = svc;
+        d.v_seq[gn] = c.seq_next++;
+        d.v_flags[gn] = F_ALIVE;  // addVirus does not hash it
+        double pm = d.v_m[gv] / 2;
+        d.v_m[gv] = pm;
+        d.v_r[gv] = radius_of(pm);
+        ev_push(d, a, PH_VB, order++, 3, d.v_seq[gv], d.v_seq[gn]);
+        c.n_vir++;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ T12 cell <- virus
+__global__ void k_pv_active(Dev d) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B;
+  int n = d.p_ncells[gp];
+  const int *st = d.vstart + (size_t)a * (d.H + 1);
+  const int *it = d.vitems + (size_t)a * d.Vcap;
+  int E = expand_for(d.ctl[a].rmax_virus);
+  bool anyp = false;
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    Rect q = footprint(x, y, r, d.size);
+    bool any = false;
+    grid_visit(st, it, d.cols, q, E, [&](int j) {
+      size_t g = (size_t)a * d.Vcap + j;
+      if (any || (d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
+      if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return;
+      if (overlap(x, y, m, r, d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) && m > 1.25 * d.v_m[g]) any = true;
+    });
+    d.c_active[ci] = any;
+    anyp |= any;
+  }
+  if (anyp) {
+    int w = atomicAdd(&d.ctl[a].n_pend, 1);
+    if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
+    else set_err(d, a, ERR_WORK_CAP);
+  }
+}
+__global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
+  int a = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  ArenaCtl &c = d.ctl[a];
+  int nw = min(c.n_pend, d.Wcap);
+  c.n_pend = 0;
+  if (nw == 0) return;
+  const int NP = d.NP;
+  int *w = d.work + (size_t)a * d.Wcap;
+  int64_t *ck = scr_k + (size_t)a * d.Wcap;
+  int *cv = scr_v + (size_t)a * d.Wcap;
+  for (int k = 0; k < nw; k++) ck[k] = w[k];
+  isort_kv(ck, w, nw);
+  const int *st = d.vstart + (size_t)a * (d.H + 1);
+  const int *it = d.vitems + (size_t)a * d.Vcap;
+  const double W = (double)d.size;
+  uint64_t order = 0;
+  for (int wi = 0; wi < nw; wi++) {
+    int gp = a * d.B + w[wi];
+    if (!d.p_alive[gp]) continue;
+    for (int i = 0; i < d.p_ncells[gp];) {  // live list: explosion children are visited too
+      size_t ci = (size_t)d.p_list[i * NP + gp] * NP + gp;
+      i++;
+      if (!d.c_active[ci] && !(d.c_flags[ci] & F_NEW)) continue;
+      int E = expand_for(c.rmax_virus);
+      Rect q = footprint(d.c_x[ci], d.c_y[ci], d.c_r[ci], d.size);
+      int nc = 0;
+      grid_visit(st, it, d.cols, q, E, [&](int j) {
+        size_t g = (size_t)a * d.Vcap + j;
+        if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
+        if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return;
+        if (nc < d.Wcap) {
+          ck[nc] = d.v_seq[g];
+          cv[nc] = j;
+          nc++;
+        }
+      });
+      isort_kv(ck, cv, nc);
+      for (int t = 0; t < nc; t++) {
+        size_t g = (size_t)a * d.Vcap + cv[t];
+        if (!(d.v_flags[g] & F_ALIVE)) continue;
+        double cm = d.c_m[ci];
+        if (!(overlap(d.c_x[ci], d.c_y[ci], cm, d.c_r[ci], d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) &&
+              cm > 1.25 * d.v_m[g]))
+          continue;
+        // eatVirus -> eatCell(..., isVirus=True) (field.py:333-344)
+        ev_push(d, a, PH_PV, order++, 4, d.c_seq[ci], d.v_seq[g]);
+        double m = grow_mass(cm, d.v_m[g] * kVirusEatFactor);
+        d.c_m[ci] = m;
+        d.c_r[ci] = radius_of(m);
+        d.v_flags[g] = 0;
+        // playerCellAteVirus (field.py:350-370)
+        int ncur = d.p_ncells[gp];
+        int n_new = kMaxCells - ncur;
+        ev_push(d, a, PH_PV, order++, 5, d.c_seq[ci], n_new);
+        if (n_new == 0) continue;
+        double dist = d.c_m[ci] * kExplosionProp;
+        double mpc = dist / n_new;
+        d.c_mt[ci] = merge_time_for(kMergeVirusFactor, d.c_m[ci]);
+        double m2 = grow_mass(d.c_m[ci], -1 * mpc * n_new);
+        d.c_m[ci] = m2;
+        d.c_r[ci] = radius_of(m2);
+        uint32_t used = 0;
+        for (int k = 0; k < ncur; k++) used |= 1u << d.p_list[k * NP + gp];
+        double px = d.c_x[ci], py = d.c_y[ci], pr = d.c_r[ci];
+        for (int k = 0; k < n_new; k++) {
+          int slot = __ffs(~used) - 1;
+          used |= 1u << slot;
+          size_t ni = (size_t)slot * NP + gp;
+          int64_t seq = c.seq_next++;
+          double nr = radius_of(mpc);
+          uint64_t u[4];
+          philox((uint64_t)seq, ST_ANGLE, 0, 0, c.key0, c.key1, u);
+          int64_t deg = (int64_t)mulhi(u[0], 360);
+          double ang = (double)deg * (kPi / 180.0);  // numpy.deg2rad
+          double ca = cos(ang);
+          double sa = sin(ang);
+          double xp = ca * pr * 12 + px, yp = sa * pr * 12 + py;
+          double vx, vy, svx, svy;
+          int svc;
+          set_move_direction(px, py, mpc, nr, xp, yp, vx, vy);
+          add_momentum(px, py, xp, yp, W, W, pr, svx, svy, svc);
+          d.c_x[ni] = px;
+          d.c_y[ni] = py;
+          d.c_m[ni] = mpc;
+          d.c_r[ni] = nr;
+          d.c_vx[ni] = vx;
+          d.c_vy[ni] = vy;
+          d.c_svx[ni] = svx;
+          d.c_svy[ni] = svy;
+          d.c_svc[ni] = svc;
+          d.c_mt[ni] = merge_time_for(0.8, mpc);
+          d.c_seq[ni] = seq;
+          d.c_flags[ni] = F_ALIVE | F_INHASH | F_NEW;  // addPlayerCell hashes it
+          d.c_active[ni] = 0;
+          d.p_list[(ncur + k) * NP + gp] = (uint8_t)slot;
+        }
+        d.p_ncells[gp] = ncur + n_new;
+      }
+    }
+    for (int k = 0; k < d.p_ncells[gp]; k++) d.c_flags[(size_t)d.p_list[k * NP + gp] * NP + gp] &= ~F_NEW;
+  }
+}
+
+// ------------------------------------------------------------ T14/T15 food
+// foods: KIND 0 pellets (eat-phase buffer 1, records sorted by bucket), 1 blobs
+template <int KIND>
+struct Food {
+  const Dev &d;
+  int a;
+  __device__ Food(const Dev &dd, int aa) : d(dd), a(aa) {}
+  __device__ size_t g(int j) const { return (size_t)a * (KIND == 0 ? d.Pcap : d.Ecap) + j; }
+  __device__ double x(int j) const { return KIND == 0 ? d.pel_x[1][g(j)] : d.b_x[g(j)]; }
+  __device__ double y(int j) const { return KIND == 0 ? d.pel_y[1][g(j)] : d.b_y[g(j)]; }
+  __device__ double m(int j) const { return KIND == 0 ? d.pel_m[1][g(j)] : d.b_m[g(j)]; }
+  __device__ double r(int j) const { return KIND == 0 ? radius_of(d.pel_m[1][g(j)]) : d.b_r[g(j)]; }
+  __device__ int64_t seq(int j) const { return KIND == 0 ? d.pel_seq[1][g(j)] : d.b_seq[g(j)]; }
+  __device__ bool alive(int j) const { return KIND == 0 ? !d.pel_dead[g(j)] : (d.b_flags[g(j)] & F_ALIVE); }
+  __device__ int64_t ej(int j) const { return KIND == 0 ? -2 : d.b_ej[g(j)]; }
+  __device__ void kill(int j) const {
+    if (KIND == 0) d.pel_dead[g(j)] = 1;
+    else d.b_flags[g(j)] = 0;
+  }
+  __device__ uint64_t *owner(int j) const { return (KIND == 0 ? d.pel_owner : d.b_owner) + g(j); }
+  __device__ const int *start() const { return (KIND == 0 ? d.pstart : d.bstart) + (size_t)a * (d.H + 1); }
+  __device__ const int *items() const { return KIND == 0 ? nullptr : d.bitems + (size_t)a * d.Ecap; }
+};
+__device__ __forceinline__ uint64_t food_key(uint32_t round, uint32_t prio) {
+  return ((uint64_t)round << 40) | (0xFFFFFFFFFFull - prio);
+}
+constexpr uint32_t kRoundMax = 0xFFFFFF;
+constexpr uint8_t kOverflow = 255;
+
+template <int KIND>
+__global__ void k_food_prep(Dev d) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  Food<KIND> F(d, a);
+  int n = d.p_ncells[gp];
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    uint32_t prio = (uint32_t)p * kMaxCells + k;
+    double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    int64_t cseq = d.c_seq[ci];
+    Rect q = footprint(x, y, r, d.size);
+    double sum = 0;
+    grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
+      if (!F.alive(j) || F.ej(j) == cseq) return;
+      if (!rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q)) return;
+      sum += F.m(j);
+    });
+    // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
+    // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
+    double M = py_min(kMaxMass, (m + sum) * (1 + 1e-9));
+    double Rm = fmax(r, radius_of(M)) * (1 + 1e-9);
+    int *lst = d.f_list + ci * FCAP;
+    int cnt = 0;
+    bool ovf = false;
+    int64_t sk[FCAP];
+    grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
+      if (!F.alive(j) || F.ej(j) == cseq) return;
+      double fm = F.m(j);
+      if (!(M > 1.25 * fm)) return;
+      double fx = F.x(j), fy = F.y(j);
+      if (!((x - fx) * (x - fx) + (y - fy) * (y - fy) < Rm * Rm)) return;
+      if (!rect_hit(footprint(fx, fy, F.r(j), d.size), q)) return;
+      if (cnt == FCAP) {
+        ovf = true;
+        return;
+      }
+      int64_t s = F.seq(j);  // insert sorted by creation sequence
+      int t = cnt++;
+      while (t > 0 && sk[t - 1] > s) {
+        sk[t] = sk[t - 1];
+        lst[t] = lst[t - 1];
+        t--;
+      }
+      sk[t] = s;
+      lst[t] = j;
+    });
+    if (ovf) {  // block every food this cell may touch; resolved by the serial pass
+      d.f_cnt[ci] = kOverflow;
+      d.f_done[ci] = 0;
+      uint64_t key = food_key(kRoundMax, prio);
+      grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
+        if (!F.alive(j)) return;
+        if (!rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q)) return;
+        atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
+      });
+      continue;
+    }
+    d.f_cnt[ci] = (uint8_t)cnt;
+    d.f_done[ci] = (cnt == 0);
+    uint64_t key = food_key(1, prio);
+    for (int t = 0; t < cnt; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
+  }
+}
+template <int KIND>
+__global__ void k_food_reserve(Dev d, int round) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  Food<KIND> F(d, a);
+  int n = d.p_ncells[gp];
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    if (d.f_done[ci] || d.f_cnt[ci] == kOverflow) continue;
+    uint64_t key = food_key(round, (uint32_t)p * kMaxCells + k);
+    const int *lst = d.f_list + ci * FCAP;
+    for (int t = 0; t < d.f_cnt[ci]; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
+  }
+}
+template <int KIND>
+__device__ void food_eat_loop(const Dev &d, const Food<KIND> &F, int a, size_t ci, uint32_t prio, const int *lst,
+                              int cnt) {
+  double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+  int64_t cseq = d.c_seq[ci];
+  int eaten = 0;
+  for (int t = 0; t < cnt; t++) {
+    int j = lst[t];
+    if (!F.alive(j)) continue;
+    double fm = F.m(j);
+    if (!(overlap(x, y, m, r, F.x(j), F.y(j), fm, F.r(j)) && can_eat(m, fm))) continue;
+    ev_push(d, a, KIND == 0 ? PH_PELLET : PH_BLOB, ((uint64_t)prio << 16) | (uint64_t)t, KIND == 0 ? 6 : 7, cseq,
+            F.seq(j));
+    m = grow_mass(m, fm);  // eatCell -> adjustCellSize -> grow (field.py:337-344)
+    r = radius_of(m);
+    F.kill(j);
+    eaten++;
+  }
+  d.c_m[ci] = m;
+  d.c_r[ci] = r;
+  if (KIND == 0 && eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
+}
+template <int KIND>
+__global__ void k_food_commit(Dev d, int round, int last) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  Food<KIND> F(d, a);
+  int n = d.p_ncells[gp];
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    if (d.f_done[ci]) continue;
+    uint32_t prio = (uint32_t)p * kMaxCells + k;
+    int cnt = d.f_cnt[ci];
+    bool own = cnt != kOverflow;
+    const int *lst = d.f_list + ci * FCAP;
+    if (own) {
+      uint64_t key = food_key(round, prio);
+      for (int t = 0; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
+    }
+    if (own) {
+      food_eat_loop<KIND>(d, F, a, ci, prio, lst, cnt);
+      d.f_done[ci] = 1;
+    } else if (last) {
+      int w = atomicAdd(&d.ctl[a].n_pend, 1);
+      if (w < d.Wcap) {
+        d.work[(size_t)a * d.Wcap + w] = (int)ci;
+        d.work2[(size_t)a * d.Wcap + w] = (int)prio;
+      } else {
+        set_err(d, a, ERR_WORK_CAP);
+      }
+    }
+  }
+}
+template <int KIND>
+__global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v) {
+  int a = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  ArenaCtl &c = d.ctl[a];
+  int nw = min(c.n_pend, d.Wcap);
+  c.n_pend = 0;
+  if (nw == 0) return;
+  Food<KIND> F(d, a);
+  int *w = d.work + (size_t)a * d.Wcap;
+  int *wp = d.work2 + (size_t)a * d.Wcap;
+  int64_t *ck = scr_k + (size_t)a * d.Wcap;
+  int *cv = scr_v + (size_t)a * d.Wcap;
+  for (int k = 0; k < nw; k++) ck[k] = wp[k];
+  isort_kv(ck, w, nw);  // priority order (player index, list position)
+  // the sorted priorities now sit in ck[0..nw); move them out of the scratch
+  int *prios = wp;
+  for (int k = 0; k < nw; k++) prios[k] = (int)ck[k];
+  for (int wi = 0; wi < nw; wi++) {
+    size_t ci = (size_t)w[wi];
+    double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci];
+    int64_t cseq = d.c_seq[ci];
+    Rect q = footprint(x, y, r, d.size);
+    int nc = 0;
+    grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
+      if (!F.alive(j) || F.ej(j) == cseq) return;
+      if (!rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q)) return;
+      if (nc < d.Wcap) {
+        ck[nc] = F.seq(j);
+        cv[nc] = j;
+        nc++;
+      } else {
+        set_err(d, a, ERR_CAND_CAP);
+      }
+    });
+    isort_kv(ck, cv, nc);
+    food_eat_loop<KIND>(d, F, a, ci, (uint32_t)prios[wi], cv, nc);
+    d.f_done[ci] = 1;
+  }
+}
+
+// ------------------------------------------------------------ T16 player <- player
+__device__ __forceinline__ Rect cell_rect(const Dev &d, size_t ci) { return footprint(d.c_x[ci], d.c_y[ci], d.c_r[ci], d.size); }
+
+__global__ void k_pp_active(Dev d) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  const int NP = d.NP, a = gp / d.B;
+  const int *st = d.cstart + (size_t)a * (d.H + 1);
+  const int *it = d.citems + (size_t)a * kMaxCells * d.B;
+  int E = expand_for(d.ctl[a].rmax_cell);
+  int n = d.p_ncells[gp];
+  bool anyp = false;
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    Rect q = footprint(x, y, r, d.size);
+    bool any = false;
+    grid_visit(st, it, d.cols, q, E, [&](int e) {
+      if (any || !(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return;
+      if (!rect_hit(cell_rect(d, e), q)) return;
+      if (overlap(x, y, m, r, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) any = true;
+    });
+    d.c_active[ci] = any;
+    anyp |= any;
+  }
+  if (anyp) {
+    int w = atomicAdd(&d.ctl[a].n_pend, 1);
+    if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
+    else set_err(d, a, ERR_WORK_CAP);
+  }
+}
+
+// removes cell e (pool index) from its player's list; returns true if the player died
+__device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order) {
+  const int NP = d.NP;
+  int gp = (int)(e % NP);
+  uint8_t slot = (uint8_t)(e / NP);
+  d.c_flags[e] = 0;
+  int n = d.p_ncells[gp], w = 0;
+  for (int k = 0; k < n; k++) {
+    uint8_t s = d.p_list[k * NP + gp];
+    if (s != slot) d.p_list[(w++) * NP + gp] = s;
+  }
+  d.p_ncells[gp] = w;
+  if (w == 0) {  // deletePlayerCell: last cell -> deadPlayers, setDead (field.py:386-388)
+    ArenaCtl &c = d.ctl[a];
+    d.p_alive[gp] = 0;
+    d.p_respawn[gp] = 1;
+    d.dead[(size_t)a * d.B + c.n_dead++] = gp - a * d.B;
+    ev_push(d, a, PH_PP, order++, 9, gp - a * d.B, d.c_seq[e]);
+    return true;
+  }
+  return false;
+}
+
+__global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *scr_v) {
+  extern __shared__ uint32_t pend[];  // pending-player bitmap (B bits)
+  int a = blockIdx.x;
+  ArenaCtl &c = d.ctl[a];
+  const int B = d.B, NW = (B + 31) / 32;
+  int nw = min(c.n_pend, d.Wcap);
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) pend[i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+    int p = d.work[(size_t)a * d.Wcap + i];
+    atomicOr(&pend[p >> 5], 1u << (p & 31));
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  c.n_pend = 0;
+  if (nw == 0) return;
+  const int NP = d.NP;
+  const int *st = d.cstart + (size_t)a * (d.H + 1);
+  const int *it = d.citems + (size_t)a * kMaxCells * B;
+  int64_t *ck = scr_k + (size_t)a * d.Wcap;
+  int *cv = scr_v + (size_t)a * d.Wcap;
+  uint64_t order = 0;
+  double rmax = c.rmax_cell;
+  int P = -1;
+  for (;;) {
+    // next pending player > P
+    int q = P + 1, found = -1;
+    for (int wd = q >> 5; wd < NW && found < 0; wd++) {
+      uint32_t bits = pend[wd];
+      if (wd == (q >> 5)) bits &= (q & 31) ? ~((1u << (q & 31)) - 1) : 0xFFFFFFFFu;
+      if (bits) found = wd * 32 + __ffs(bits) - 1;
+    }
+    if (found < 0) break;
+    P = found;
+    pend[P >> 5] &= ~(1u << (P & 31));
+    int gp = a * B + P;
+    if (!d.p_alive[gp]) continue;
+    for (int i = 0; i < d.p_ncells[gp];) {  // for playerCell in player.getCells(): live list
+      size_t pc = (size_t)d.p_list[i * NP + gp] * NP + gp;
+      i++;
+      if (!d.c_active[pc]) continue;
+      d.c_active[pc] = 0;
+      Rect q0 = cell_rect(d, pc);
+      int nc = 0;
+      grid_visit(st, it, d.cols, q0, expand_for(rmax), [&](int e) {
+        if (!(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return;
+        if (!rect_hit(cell_rect(d, e), q0)) return;
+        if (nc < d.Wcap) {
+          ck[nc] = d.c_seq[e];
+          cv[nc] = e;
+          nc++;
+        } else {
+          c.err |= ERR_CAND_CAP;
+        }
+      });
+      isort_kv(ck, cv, nc);
+      for (int t = 0; t < nc; t++) {
+        size_t o = (size_t)cv[t];
+        if (!(d.c_flags[o] & F_ALIVE)) continue;
+        if (!overlap(d.c_x[pc], d.c_y[pc], d.c_m[pc], d.c_r[pc], d.c_x[o], d.c_y[o], d.c_m[o], d.c_r[o])) continue;
+        size_t g, v;
+        bool pc_eats = can_eat(d.c_m[pc], d.c_m[o]);
+        if (pc_eats) {
+          g = pc;
+          v = o;
+        } else if (can_eat(d.c_m[o], d.c_m[pc])) {
+          g = o;
+          v = pc;
+        } else {
+          continue;
+        }
+        // eatPlayerCell (field.py:346-348)
+        ev_push(d, a, PH_PP, order++, 8, d.c_seq[g], d.c_seq[v]);
+        double m = grow_mass(d.c_m[g], d.c_m[v]);
+        d.c_m[g] = m;
+        d.c_r[g] = radius_of(m);
+        rmax = fmax(rmax, d.c_r[g]);
+        remove_cell(d, a, v, order);
+        // re-activate every later turn whose outcome the growth of g may change
+        int gpl = (int)(g % NP);
+        Rect qg = cell_rect(d, g);
+        double gx = d.c_x[g], gy = d.c_y[g], gm = d.c_m[g], gr = d.c_r[g];
+        grid_visit(st, it, d.cols, qg, expand_for(rmax), [&](int e) {
+          if (!(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
+          if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;
+          d.c_active[e] = 1;
+          int pe = (int)(e % NP) - a * B;
+          if (pe > P) pend[pe >> 5] |= 1u << (pe & 31);
+        });
+        d.c_active[g] = 1;
+        if (gpl - a * B > P) pend[(gpl - a * B) >> 5] |= 1u << ((gpl - a * B) & 31);
+        if (!pc_eats) break;
+      }
+    }
+  }
+  c.rmax_cell = rmax;
+}
+
+// ------------------------------------------------------------ T17 occupancy
+__global__ void k_occupancy(Dev d) {
+  int gi = GTID;
+  int per = kMaxCells * d.B;
+  if (gi >= d.A * per) return;
+  int a = gi / per, i = gi - a * per;
+  int slot = i / d.B, p = i - slot * d.B;
+  size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
+  if (!(d.c_flags[g] & F_ALIVE)) return;
+  atomic_max_pos(&d.ctl[a].rmax_cell, d.c_r[g]);
+  Rect r = cell_rect(d, g);
+  unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
+  for (int by = r.y0; by <= r.y1; by++)
+    for (int bx = r.x0; bx <= r.x1; bx++) {
+      int b = by * d.cols + bx;
+      atomicOr(&occ[b >> 6], 1ull << (b & 63));
+    }
+}
+
+// ------------------------------------------------------------ T18 spawn
+// getSpawnPos (field.py:283-301) with the player-hash occupancy bitmap
+__device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4], double &ox, double &oy) {
+  const int cols = d.cols, total = d.H;
+  const unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
+  int sb = (int)mulhi(u[0], (uint64_t)total);
+  int found = -1;
+  // first non-occupied bucket at or after sb, cyclically
+  for (int pass = 0; pass < 2 && found < 0; pass++) {
+    int lo = pass == 0 ? sb : 0, hi = pass == 0 ? total : sb;
+    for (int b = lo; b < hi && found < 0;) {
+      int wd = b >> 6;
+      unsigned long long free_bits = ~occ[wd];
+      free_bits &= (~0ull) << (b & 63);
+      int wend = (wd + 1) << 6;
+      if (wend > hi) free_bits &= (hi - (wd << 6)) >= 64 ? ~0ull : ((1ull << (hi - (wd << 6))) - 1);
+      if (free_bits) found = (wd << 6) + __ffsll((long long)free_bits) - 1;
+      b = wend;
+    }
+  }
+  int64_t xp, yp;
+  if (found < 0) {
+    xp = ph_randint(u[1], 0, d.size);
+    yp = ph_randint(u[2], 0, d.size);
+  } else {
+    int64_t x = found % cols;
+    double y = (double)(found - x) / cols;
+    int64_t left = (x - 1) * kBucket;
+    double top = y * kBucket;
+    xp = ph_randint(u[1], left + radius, (double)(left + kBucket) - radius);
+    yp = ph_randint(u[2], top + radius, top + kBucket - radius);
+  }
+  ox = (double)xp;
+  oy = (double)yp;
+}
+
+__global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
+  __shared__ int sflag[1024];
+  int a = blockIdx.x;
+  ArenaCtl &c = d.ctl[a];
+  const int T = blockDim.x, tid = threadIdx.x;
+  // order-preserving compaction of viruses and blobs (list order == creation order)
+  for (int kind = 0; kind < 2; kind++) {
+    int n = kind == 0 ? c.n_vir : c.n_blob;
+    int cap = kind == 0 ? d.Vcap : d.Ecap;
+    int out = 0;
+    for (int base = 0; base < n; base += T) {
+      int i = base + tid;
+      size_t g = (size_t)a * cap + i;
+      bool alive = i < n && ((kind == 0 ? d.v_flags[g] : d.b_flags[g]) & F_ALIVE);
+      double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, f6 = 0, f7 = 0;
+      int svc = 0;
+      int64_t s = 0, e = 0;
+      uint32_t fl = 0;
+      if (alive) {
+        if (kind == 0) {
+          f0 = d.v_x[g]; f1 = d.v_y[g]; f2 = d.v_m[g]; f3 = d.v_r[g]; f4 = d.v_vx[g]; f5 = d.v_vy[g];
+          f6 = d.v_svx[g]; f7 = d.v_svy[g]; svc = d.v_svc[g]; s = d.v_seq[g]; fl = d.v_flags[g];
+        } else {
+          f0 = d.b_x[g]; f1 = d.b_y[g]; f2 = d.b_m[g]; f3 = d.b_r[g]; f4 = d.b_vx[g]; f5 = d.b_vy[g];
+          f6 = d.b_svx[g]; f7 = d.b_svy[g]; svc = d.b_svc[g]; s = d.b_seq[g]; e = d.b_ej[g]; fl = d.b_flags[g];
+        }
+      }
+      sflag[tid] = alive;
+      __syncthreads();
+      // Hillis-Steele inclusive prefix of the alive flags
+      for (int off = 1; off < T; off <<= 1) {
+        int v = (tid >= off) ? sflag[tid - off] : 0;
+        __syncthreads();
+        sflag[tid] += v;
+        __syncthreads();
+      }
+      int pos = out + sflag[tid] - (alive ? 1 : 0);
+      int chunk = sflag[T - 1];
+      __syncthreads();
+      if (alive) {
+        size_t o = (size_t)a * cap + pos;
+        if (kind == 0) {
+          d.v_x[o] = f0; d.v_y[o] = f1; d.v_m[o] = f2; d.v_r[o] = f3; d.v_vx[o] = f4; d.v_vy[o] = f5;
+          d.v_svx[o] = f6; d.v_svy[o] = f7; d.v_svc[o] = svc; d.v_seq[o] = s; d.v_flags[o] = fl;
+        } else {
+          d.b_x[o] = f0; d.b_y[o] = f1; d.b_m[o] = f2; d.b_r[o] = f3; d.b_vx[o] = f4; d.b_vy[o] = f5;
+          d.b_svx[o] = f6; d.b_svy[o] = f7; d.b_svc[o] = svc; d.b_seq[o] = s; d.b_ej[o] = e; d.b_flags[o] = fl;
+        }
+      }
+      out += chunk;
+      __syncthreads();
+    }
+    // clear the tail flags
+    for (int i = out + tid; i < n; i += T) {
+      size_t g = (size_t)a * cap + i;
+      if (kind == 0) d.v_flags[g] = 0;
+      else d.b_flags[g] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (kind == 0) c.n_vir = out;
+      else c.n_blob = out;
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  // spawnPellets: while len(pellets) < maxCollectibleCount
+  int alive_p = c.n_pel - c.n_pel_eaten + c.n_pnew;
+  int kp = 0;
+  if ((double)alive_p < d.max_pellets) kp = (int)ceil(d.max_pellets) - alive_p;
+  if (alive_p + kp > d.Pcap || c.n_pnew + kp > d.Pcap) {
+    c.err |= ERR_PELLET_CAP;
+    kp = max(0, min(d.Pcap - alive_p, d.Pcap - c.n_pnew));
+  }
+  c.seq_base_spawn = c.seq_next;
+  c.seq_next += kp;
+  c.ctr_pellet_base = c.ctr_pellet;
+  c.ctr_pellet += kp;
+  c.n_spawn_p = kp;
+  // spawnViruses
+  int kv = 0;
+  if (d.virus_enabled && (double)c.n_vir < d.max_viruses) kv = (int)ceil(d.max_viruses) - c.n_vir;
+  if (c.n_vir + kv > d.Vcap) {
+    c.err |= ERR_VIRUS_CAP;
+    kv = d.Vcap - c.n_vir;
+  }
+  c.seq_next += kv;
+  c.ctr_virus_base = c.ctr_virus;
+  c.ctr_virus += kv;
+  c.vir_base_spawn = c.n_vir;
+  c.n_spawn_v = kv;
+  c.n_vir += kv;
+  // spawnPlayers: deadPlayers in order, respawnTime == 0
+  int np = 0, w = 0;
+  int *dl = d.dead + (size_t)a * d.B;
+  int *rl = d.respawn_list + (size_t)a * d.B;
+  if (init) {
+    for (int p = 0; p < d.B; p++) rl[np++] = p;
+  } else {
+    for (int i = 0; i < c.n_dead; i++) {
+      int p = dl[i];
+      if (d.p_respawn[(size_t)a * d.B + p] == 0) rl[np++] = p;
+      else dl[w++] = p;
+    }
+    c.n_dead = w;
+  }
+  c.n_spawn_pl = np;
+  if (!init) c.seq_next += np;  // at initialize() players already own seqs 0..B-1
+}
+
+__global__ void k_pnew_commit(Dev d) {
+  int a = GTID;
+  if (a >= d.A) return;
+  d.ctl[a].n_pnew += d.ctl[a].n_spawn_p;
+}
+__global__ void k_reset_rmax(Dev d, int kind) {
+  int a = GTID;
+  if (a >= d.A) return;
+  if (kind == 0) d.ctl[a].rmax_cell = 0;
+  else d.ctl[a].rmax_virus = 0;
+}
+
+__global__ void k_spawn_pellets(Dev d) {
+  int gi = GTID;
+  if (gi >= d.A * d.Pcap) return;
+  int a = gi / d.Pcap, j = gi - a * d.Pcap;
+  ArenaCtl &c = d.ctl[a];
+  if (j >= c.n_spawn_p) return;
+  uint64_t u[4];
+  philox(c.ctr_pellet_base + j, ST_PELLET, 0, 0, c.key0, c.key1, u);
+  int64_t x = (int64_t)mulhi(u[0], (uint64_t)d.size), y = (int64_t)mulhi(u[1], (uint64_t)d.size);
+  int64_t sr = (int64_t)mulhi(u[2], 50);
+  double m = (sr > 50 - 4) ? (double)(50 - sr) : 1.0;  // randomSize (field.py:20-26)
+  size_t o = (size_t)a * d.Pcap + c.n_pnew + j;
+  d.pn_x[o] = (double)x;
+  d.pn_y[o] = (double)y;
+  d.pn_m[o] = m;
+  d.pn_seq[o] = c.seq_base_spawn + j;
+}
+__global__ void k_spawn_viruses(Dev d) {
+  int gi = GTID;
+  if (gi >= d.A * d.Vcap) return;
+  int a = gi / d.Vcap, j = gi - a * d.Vcap;
+  ArenaCtl &c = d.ctl[a];
+  if (j >= c.n_spawn_v) return;
+  uint64_t u[4], u2[4];
+  philox(c.ctr_virus_base + j, ST_VIRUS, 0, 0, c.key0, c.key1, u);
+  philox(c.ctr_virus_base + j, ST_VIRUS, 1, 0, c.key0, c.key1, u2);
+  const double vr = radius_of(kVirusBase);
+  double x, y;
+  spawn_pos(d, a, vr, u, x, y);
+  double rng = kBucket - vr;
+  x += (double)ph_randint(u2[0], (-1) * rng / 2, rng / 2);
+  y += (double)ph_randint(u2[1], (-1) * rng / 2, rng / 2);
+  size_t o = (size_t)a * d.Vcap + c.vir_base_spawn + j;
+  d.v_x[o] = x;
+  d.v_y[o] = y;
+  d.v_m[o] = kVirusBase;
+  d.v_r[o] = vr;
+  d.v_vx[o] = 0;
+  d.v_vy[o] = 0;
+  d.v_svx[o] = 0;
+  d.v_svy[o] = 0;
+  d.v_svc[o] = 0;
+  d.v_seq[o] = c.seq_base_spawn + c.n_spawn_p + j;
+  d.v_flags[o] = F_ALIVE;  // addVirus: not hashed until the next rebuild
+}
+__global__ void k_spawn_players(Dev d, int init) {
+  int gi = GTID;
+  if (gi >= d.NP) return;
+  int a = gi / d.B, j = gi - a * d.B;
+  ArenaCtl &c = d.ctl[a];
+  if (j >= c.n_spawn_pl) return;
+  int p = d.respawn_list[(size_t)a * d.B + j];
+  int gp = a * d.B + p;
+  const int NP = d.NP;
+  uint64_t u[4];
+  if (init) philox((uint64_t)p, ST_INIT_PLAYER, 0, 0, c.key0, c.key1, u);
+  else philox((uint64_t)p, ST_PLAYER, (uint64_t)c.tick, 0, c.key0, c.key1, u);
+  const double sr = radius_of(kStartMass);
+  double x, y;
+  spawn_pos(d, a, sr, u, x, y);
+  int64_t seq = init ? (int64_t)j : c.seq_base_spawn + c.n_spawn_p + c.n_spawn_v + j;
+  if (init) seq = (int64_t)j;  // Field.initialize: players first
+  for (int k = 0; k < kMaxCells; k++) d.c_flags[(size_t)k * NP + gp] = 0;
+  size_t ci = (size_t)gp;  // slot 0
+  d.c_x[ci] = x;
+  d.c_y[ci] = y;
+  d.c_m[ci] = kStartMass;
+  d.c_r[ci] = sr;
+  d.c_vx[ci] = 0;
+  d.c_vy[ci] = 0;
+  d.c_svx[ci] = 0;
+  d.c_svy[ci] = 0;
+  d.c_svc[ci] = 0;
+  d.c_mt[ci] = 0;
+  d.c_seq[ci] = seq;
+  d.c_flags[ci] = F_ALIVE;  // initializePlayer does not hash the cell
+  d.p_list[gp] = 0;
+  d.p_ncells[gp] = 1;
+  d.p_alive[gp] = 1;
+  d.p_respawn[gp] = 0;
+  if (!init) ev_push(d, a, PH_SPAWN, (uint64_t)j, 10, p, seq);
+}
+
+__global__ void k_tick_end(Dev d) {
+  int a = GTID;
+  if (a >= d.A) return;
+  d.ctl[a].tick += 1;
+}
+
+// ------------------------------------------------------------ init helpers
+__global__ void k_init_ctl(Dev d, uint64_t seed) {
+  int a = GTID;
+  if (a >= d.A) return;
+  ArenaCtl &c = d.ctl[a];
+  c.seq_next = d.B;  // players take 0..B-1 (Field.initialize order)
+  c.tick = 0;
+  c.key0 = seed;
+  c.key1 = ((uint64_t)a << 32) | 0x9E3779B9ull;
+  c.ctr_pellet = c.ctr_virus = 0;
+  c.n_pel = c.n_pnew = c.n_pel_eaten = 0;
+  c.n_blob = c.n_blob_base = 0;
+  c.n_vir = c.n_vir_start = 0;
+  c.n_dead = 0;
+  c.n_ev = 0;
+  c.n_pend = c.n_pend2 = 0;
+  c.err = c.warn = 0;
+  c.rmax_cell = radius_of(kStartMass);
+  c.rmax_virus = radius_of(kVirusBase);
+}
+
+// ------------------------------------------------------------ launch sequences
+static inline int nblk(long n, int t) { return (int)((n + t - 1) / t); }
+
+struct Scratch {
+  int64_t *k;
+  int *v;
+};
+
+void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead) {
+  (void)hipMemsetAsync(d.pcnt, 0, sizeof(int) * (size_t)d.A * (d.H + 1), s);
+  long n = (long)d.A * 2 * d.Pcap;
+  hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
+  hipLaunchKernelGGL(k_grid_scan, dim3(d.A), dim3(1024), 0, s, d, d.pcnt, d.pstart);
+  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
+  hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+}
+
+template <int KIND>
+static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start) {
+  int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
+  long n = (long)d.A * per;
+  (void)hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)d.A * (d.H + 1), s);
+  if (KIND != 1) hipLaunchKernelGGL(k_reset_rmax, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, KIND == 0 ? 0 : 1);
+  hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_grid_scan, dim3(d.A), dim3(1024), 0, s, d, cnt, start);
+  hipLaunchKernelGGL(k_grid_scatter<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
+}
+
+template <int KIND>
+static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
+  size_t cap = KIND == 0 ? (size_t)d.Pcap : (size_t)d.Ecap;
+  (void)hipMemsetAsync(KIND == 0 ? d.pel_owner : d.b_owner, 0, sizeof(uint64_t) * d.A * cap, s);
+  int g = nblk(d.NP, 256);
+  hipLaunchKernelGGL(k_food_prep<KIND>, dim3(g), dim3(256), 0, s, d);
+  for (int r = 1; r <= rounds; r++) {
+    if (r > 1) hipLaunchKernelGGL(k_food_reserve<KIND>, dim3(g), dim3(256), 0, s, d, r);
+    hipLaunchKernelGGL(k_food_commit<KIND>, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
+  }
+  hipLaunchKernelGGL(k_food_serial<KIND>, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v);
+}
+
+void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v) {
+  Scratch scr{scr_k, scr_v};
+  const int gP = nblk(d.NP, 256);
+  if (d.virus_enabled) hipLaunchKernelGGL(k_update_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_update_blobs, dim3(nblk((long)d.A * d.Ecap, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_update_players, dim3(gP), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
+  hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
+  launch_pellet_rebuild(d, s, 0, 0);  // P0 U conversions -> P1 (eat-phase buffer)
+  launch_grid<1>(d, s, d.bcnt, d.bstart);
+  if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart);
+  hipLaunchKernelGGL(k_merge, dim3(gP), dim3(256), 0, s, d);
+  if (d.virus_enabled) {
+    hipLaunchKernelGGL(k_vb_active, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_vb_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
+    hipLaunchKernelGGL(k_pv_active, dim3(gP), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
+  }
+  launch_grid<0>(d, s, d.ccnt, d.cstart);
+  launch_food<0>(d, s, rounds, scr);
+  launch_food<1>(d, s, rounds, scr);
+  hipLaunchKernelGGL(k_pp_active, dim3(gP), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
+  (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
+  hipLaunchKernelGGL(k_occupancy, dim3(nblk((long)d.A * kMaxCells * d.B, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);
+  hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
+  if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_spawn_players, dim3(gP), dim3(256), 0, s, d, 0);
+  hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+  launch_pellet_rebuild(d, s, 1, 1);  // P1 survivors U spawns -> P0
+  // the virus list was compacted by k_spawn_plan: re-index the virus grid for the
+  // observations (membership stays the F_INHASH flag: spawned viruses are not hashed)
+  if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart);
+  hipLaunchKernelGGL(k_tick_end, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+}
+
+// Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty
+// player hash), then spawnStuff's pellets and viruses.
+void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
+  (void)hipMemsetAsync(d.c_flags, 0, sizeof(uint32_t) * (size_t)kMaxCells * d.NP, s);
+  (void)hipMemsetAsync(d.v_flags, 0, sizeof(uint32_t) * (size_t)d.A * d.Vcap, s);
+  (void)hipMemsetAsync(d.b_flags, 0, sizeof(uint32_t) * (size_t)d.A * d.Ecap, s);
+  (void)hipMemsetAsync(d.p_split, 0, sizeof(int) * d.NP, s);
+  (void)hipMemsetAsync(d.p_eject, 0, sizeof(int) * d.NP, s);
+  (void)hipMemsetAsync(d.ev, 0, sizeof(int64_t) * 5, s);
+  hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
+  (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1);
+  hipLaunchKernelGGL(k_spawn_players, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, 1);
+  hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
+  if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+  launch_pellet_rebuild(d, s, 1, 0);  // staging -> P0
+}
+
+}  // namespace aigar

@@ -183,6 +183,10 @@ int aigar_sync(aigar_handle *h);
 int aigar_profile(aigar_handle *h, int enable);
 int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *launches);
 
+/* Diagnostics: evaluate the device's correctly rounded pow (aigar_math.h) on
+ * host arrays of n (x, y) pairs -- used by the parity tests. */
+int aigar_selftest_pow(const double *x, const double *y, double *out, int n);
+
 #ifdef __cplusplus
 }
 #endif
