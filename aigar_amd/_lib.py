@@ -16,6 +16,26 @@ SO_PATH = os.path.join(HERE, "libaigar_hip.so")
 _lib = None
 
 
+def _preload_single_hip_runtime():
+    """torch ships its own libamdhip64.so (same SONAME as /opt/rocm's).  Two HIP
+    runtimes in one process break each other (and make torch streams invalid
+    handles for us), so when torch is installed we bind to ITS runtime: preload
+    it by path, before our library resolves libamdhip64.so.7.  torch imported
+    later resolves to the same file."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        C.CDLL(cand, mode=C.RTLD_GLOBAL)
+        return cand
+    return None
+
+
 def load(build_if_missing=False):
     global _lib
     if _lib is not None:
@@ -27,6 +47,7 @@ def load(build_if_missing=False):
         else:
             raise RuntimeError("libaigar_hip.so not found at %s: build it with `python -m aigar_amd._build` "
                                "(hipcc --offload-arch=gfx950)" % SO_PATH)
+    _preload_single_hip_runtime()
     L = C.CDLL(SO_PATH)
     vp, i32, u64, dp = C.c_void_p, C.c_int, C.c_uint64, C.POINTER(C.c_double)
     L.aigar_last_error.restype = C.c_char_p

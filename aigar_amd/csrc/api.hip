@@ -53,8 +53,9 @@ struct aigar_handle {
   std::vector<void *> allocs;
   bool profile = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double obs_ms = 0, tick_ms = 0;
-  int obs_launches = 0, tick_launches = 0;
+  // timer name -> recorded (start, stop) event pairs, resolved lazily
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> marks;
+  std::vector<hipEvent_t> event_pool;
   hipGraphExec_t graph = nullptr;
   bool use_graph = false;
   uint64_t policy_calls = 0;
@@ -90,8 +91,41 @@ static void free_all(aigar_handle *h) {
   h->allocs.clear();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
+  for (auto &m : h->marks) {
+    (void)hipEventDestroy(m.second.first);
+    (void)hipEventDestroy(m.second.second);
+  }
+  for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
   if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
 }
+
+static hipEvent_t pool_event(aigar_handle *h) {
+  hipEvent_t e = nullptr;
+  if (!h->event_pool.empty()) {
+    e = h->event_pool.back();
+    h->event_pool.pop_back();
+  } else {
+    (void)hipEventCreate(&e);
+  }
+  return e;
+}
+struct Mark {  // records a (start, stop) event pair around a launch group when profiling
+  aigar_handle *h;
+  const char *name;
+  hipEvent_t a = nullptr;
+  Mark(aigar_handle *hh, const char *n) : h(hh), name(n) {
+    if (h->profile) {
+      a = pool_event(h);
+      (void)hipEventRecord(a, h->stream);
+    }
+  }
+  ~Mark() {
+    if (!a) return;
+    hipEvent_t b = pool_event(h);
+    (void)hipEventRecord(b, h->stream);
+    h->marks.push_back({name, {a, b}});
+  }
+};
 
 extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   if (!cfg || !out) return fail("aigar_create: null argument");
@@ -261,6 +295,7 @@ extern "C" int aigar_set_commands(aigar_handle *h, const double *cmd, int on_dev
 
 extern "C" int aigar_policy_random(aigar_handle *h, double p_split, double p_eject, uint64_t seed) {
   if (!h) return fail("null handle");
+  Mark m(h, "policy");
   launch_policy(h->d, h->stream, p_split, p_eject, seed + (h->policy_calls++ << 20));
   HIPCHK(hipGetLastError());
   return 0;
@@ -277,16 +312,8 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
   HIPCHK(hipSetDevice(h->cfg.device));
   hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
   for (int t = 0; t < n_ticks; t++) {
-    if (h->profile) HIPCHK(hipEventRecord(h->ev0, h->stream));
+    Mark m(h, "tick");
     launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
-    if (h->profile) {
-      HIPCHK(hipEventRecord(h->ev1, h->stream));
-      HIPCHK(hipEventSynchronize(h->ev1));
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
-      h->tick_ms += ms;
-      h->tick_launches++;
-    }
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -299,15 +326,9 @@ extern "C" int aigar_observe(aigar_handle *h, void *out, int dtype, int on_devic
   if (dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
   HIPCHK(hipSetDevice(h->cfg.device));
   void *dst = on_device ? out : h->d_obs;
-  if (h->profile) HIPCHK(hipEventRecord(h->ev0, h->stream));
-  launch_observe(h->d, h->stream, dst, dtype);
-  if (h->profile) {
-    HIPCHK(hipEventRecord(h->ev1, h->stream));
-    HIPCHK(hipEventSynchronize(h->ev1));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
-    h->obs_ms += ms;
-    h->obs_launches++;
+  {
+    Mark m(h, "observe");
+    launch_observe(h->d, h->stream, dst, dtype);
   }
   HIPCHK(hipGetLastError());
   if (!on_device) {
@@ -368,22 +389,31 @@ extern "C" int aigar_sync(aigar_handle *h) {
 
 extern "C" int aigar_profile(aigar_handle *h, int enable) {
   if (!h) return fail("null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (auto &m : h->marks) {
+    h->event_pool.push_back(m.second.first);
+    h->event_pool.push_back(m.second.second);
+  }
+  h->marks.clear();
   h->profile = enable != 0;
-  h->obs_ms = h->tick_ms = 0;
-  h->obs_launches = h->tick_launches = 0;
   return 0;
 }
+// total HIP-event time (ms) and launch count of a timer since aigar_profile(h, 1):
+// "tick" (one Field.update), "observe" (k_observe), "policy" (k_policy_random)
 extern "C" int aigar_kernel_time(aigar_handle *h, const char *name, double *ms, int *launches) {
   if (!h || !name || !ms || !launches) return fail("null argument");
-  if (!strcmp(name, "observe")) {
-    *ms = h->obs_ms;
-    *launches = h->obs_launches;
-  } else if (!strcmp(name, "tick")) {
-    *ms = h->tick_ms;
-    *launches = h->tick_launches;
-  } else {
-    return fail("unknown timer '%s' (observe | tick)", name);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  double tot = 0;
+  int n = 0;
+  for (auto &m : h->marks) {
+    if (m.first != name) continue;
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, m.second.first, m.second.second));
+    tot += t;
+    n++;
   }
+  *ms = tot;
+  *launches = n;
   return 0;
 }
 

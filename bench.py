@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/sec of the agar.io stepper (BASELINE.json metric).
+
+One step = one synthetic-population policy pass + Field.update() for the
+whole arena + the grid observation for every bot.
+env-steps = bots x steps.  Default workload = BASELINE.json configs[2] (C3):
+4096 bots, 100k pellets, 1152 viruses, split + eject on, field 4800, on one
+MI355X.  For N > 1 (launched by torch.distributed.run, one rank per GPU) each
+rank steps its own C3 arena (independent replicas, weak scaling, no collective
+in the data path); the timed region is bracketed by barrier + synchronize and
+the max over ranks is taken.
+
+Prints ONE JSON line (rank 0).  Extra objects: "roofline" for the dominant
+kernel (k_observe, HIP-event timed live on the stepper's stream) and
+"cpu_baseline" (the C oracle, i.e. a single-thread CPU port of the reference,
+timed on a bounded sample of the same workload on this host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from aigar_amd import _abi  # noqa: E402
+
+# C3 observation config: VIRUS_SPAWN + ENABLE_SPLIT (networkParameters.py:76-96)
+C3_CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
+         | _abi.OBS_ENEMY_LF)
+C3_EX = _abi.EX_LAST_FOV | _abi.EX_FOV | _abi.EX_MASS | _abi.EX_LAST_ACT
+
+WORKLOADS = {
+    # name: (bots, field, pellets, virus, p_split, p_eject, channels, extras)
+    "c3": (4096, 4800, 100000.0, True, 2.5e-3, 1e-2, C3_CH, C3_EX),
+    "c2": (256, 1200, 10000.0, False, 0.0, 0.0, _abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY,
+           _abi.EX_FOV | _abi.EX_MASS),
+}
+
+
+def make_cfg(name, device=0, flags=0):
+    bots, field, pellets, virus, _, _, ch, ex = WORKLOADS[name]
+    c = _abi.Config()
+    c.n_arenas, c.bots_per_arena, c.field_size = 1, bots, field
+    c.virus_enabled = int(virus)
+    c.max_pellets, c.max_viruses = pellets, -1.0
+    c.grid_squares, c.obs_channels, c.obs_extras = 11, ch, ex
+    c.rng_mode, c.device, c.flags = _abi.RNG_PHILOX, device, flags
+    return c
+
+
+def obs_bytes_per_bot(L, p_fov, c_fov, v_fov, n_cells=1.2):
+    """Algorithmic HBM bytes k_observe moves per bot:
+    own cells (x, y, m, r + list slot), visible pellet records (x, y, m, seq = 32 B),
+    visible cells (x, y, m, r, flags = 36 B), viruses (x, y, m, r, seq, flags = 44 B),
+    history grids read+write (2 x 2 x 121 x 8 B), output row (L x 8 B)."""
+    return n_cells * 33 + p_fov * 32 + c_fov * 36 + v_fov * 44 + 2 * 2 * 121 * 8 + L * 8
+
+
+def cpu_baseline(name, budget_s=12.0, seed=1):
+    """Single-thread C oracle (CPU port of the reference) on the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle  # test infrastructure: the checker / CPU baseline only
+    bots, field, pellets, virus, ps, pe, ch, ex = WORKLOADS[name]
+    cfg = make_cfg(name, flags=0)
+    o = Oracle(cfg)
+    o.reset(seed)
+    rng = np.random.default_rng(seed)
+
+    def commands():
+        st = o.player_stats()
+        cmd = np.zeros((bots, 4))
+        fx, fy, fs = st[:, 2], st[:, 3], st[:, 4]
+        ok = st[:, 0] > 0
+        x, y = np.trunc(np.nan_to_num(fx)), np.trunc(np.nan_to_num(fy))
+        half, size = np.trunc(np.nan_to_num(fs) / 2), np.trunc(np.nan_to_num(fs))
+        cmd[:, 0] = np.where(ok, x - half + rng.random(bots) * size, -1)
+        cmd[:, 1] = np.where(ok, y - half + rng.random(bots) * size, -1)
+        cmd[:, 2] = rng.random(bots) < ps
+        cmd[:, 3] = rng.random(bots) < pe
+        return cmd
+
+    for _ in range(2):  # warm-up
+        o.set_commands(commands())
+        o.step(1)
+        o.observe()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        o.set_commands(commands())
+        o.step(1)
+        o.observe()
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": bots * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "%s world, %d steps (policy + Field.update + obs for all %d bots) after 2 warm-up steps, "
+                      "oracle/oracle.c single thread, %.1f s" % (name.upper(), n, bots, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--seed", type=int, default=1234)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    else:
+        torch.cuda.set_device(0)
+    from aigar_amd import _lib  # raises if libaigar_hip.so is missing: no fallback
+
+    name = args.workload
+    bots, field, pellets, virus, ps, pe, ch, ex = WORKLOADS[name]
+    stp = _lib.Stepper(make_cfg(name, device=local))
+    stream = torch.cuda.current_stream()
+    stp.set_stream(stream.cuda_stream)
+    obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
+    stp.reset(args.seed + 7919 * rank)
+
+    def one_step():
+        stp.policy_random(ps, pe, args.seed)
+        stp.step(1)
+        stp.observe(obs)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    stp.sync()
+    stats = stp.player_stats()
+    stp.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    obs_ms, obs_n = stp.kernel_time("observe")
+    tick_ms, tick_n = stp.kernel_time("tick")
+    pol_ms, pol_n = stp.kernel_time("policy")
+    stp.profile(False)
+    stp.sync()  # raises on any device-side capacity error
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = stp.get_state()
+    n_total = bots * args.steps * world
+    value = n_total / elapsed
+
+    # roofline of the dominant kernel (k_observe): algorithmic bytes per launch / avg duration
+    alive = int(np.sum(stats[:, 0] > 0))
+    fs = np.nan_to_num(stats[:, 4])
+    area = float(np.mean((fs + 2.0) ** 2))  # FOV box incl. object radii
+    dens_p = st["n_pellets"] / float(field * field)
+    dens_c = st["n_cells"] / float(field * field)
+    dens_v = st["n_viruses"] / float(field * field)
+    per_bot = obs_bytes_per_bot(stp.obs_len, dens_p * area, dens_c * area, dens_v * area,
+                                n_cells=st["n_cells"] / max(1, alive))
+    obs_bytes_launch = per_bot * alive
+    obs_avg_s = (obs_ms / max(1, obs_n)) / 1e3
+    achieved = obs_bytes_launch / obs_avg_s / 1e9
+    peak = 8000.0
+    roofline = {"bound": "hbm", "kernel": "k_observe", "achieved": round(achieved, 2), "peak": peak,
+                "unit": "GB/s", "frac": achieved / peak, "traffic": None,
+                "bytes_per_launch": int(obs_bytes_launch), "avg_launch_ms": obs_avg_s * 1e3}
+
+    out = {
+        "metric": "env-steps/sec at 4096 bots x 100k pellets; 1/2/4/8 MI355X scaling",
+        "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox bot population, random-action policy)",
+        "config": {"workload": "%s: %d bots, %d pellets, %s viruses, split p=%g, eject p=%g, field %d, "
+                               "obs %d floats/bot" % (name.upper(), bots, int(pellets),
+                                                      "1152" if virus else "no", ps, pe, field, stp.obs_len),
+                   "parallelism": "replicas%d" % world if world > 1 else "single-gpu"},
+        "roofline": roofline,
+        "breakdown_ms_per_step": {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
+                                  "observe": obs_ms / max(1, obs_n)},
+        "world": {"pellets": st["n_pellets"], "cells": st["n_cells"], "viruses": st["n_viruses"],
+                  "blobs": st["n_blobs"], "alive_bots": alive, "tick": int(st["tick"])},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    stp.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
