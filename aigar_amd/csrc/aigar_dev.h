@@ -42,7 +42,9 @@ struct ArenaCtl {
   uint32_t err;   // sticky error bits (capacity overflow ...)
   uint32_t warn;  // sticky quirk bits (reference would raise)
   double rmax_cell, rmax_virus;
-  uint64_t ev_order;  // serial-phase event counter
+  uint64_t ev_order;     // serial-phase event counter
+  uint32_t food_round;   // reservation epoch (grows every eat phase)
+  uint32_t pad0;
 };
 
 enum : uint32_t {

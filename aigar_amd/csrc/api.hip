@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -57,7 +58,8 @@ struct aigar_handle {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> marks;
   std::vector<hipEvent_t> event_pool;
   hipGraphExec_t graph = nullptr;
-  bool use_graph = false;
+  bool use_graph = true;  // AIGAR_NO_GRAPH=1 disables (direct launches)
+  bool graph_failed = false;
   uint64_t policy_calls = 0;
 };
 
@@ -143,6 +145,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   HIPCHK(hipSetDevice(cfg->device));
   aigar_handle *h = new aigar_handle();
   h->cfg = *cfg;
+  if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
   Dev &d = h->d;
   d.A = cfg->n_arenas;
   d.B = cfg->bots_per_arena;
@@ -154,9 +157,10 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.max_pellets = cfg->max_pellets >= 0 ? cfg->max_pellets : (double)d.size * d.size * 0.015;
   d.max_viruses = cfg->max_viruses >= 0 ? cfg->max_viruses : (double)d.size * d.size * 0.00005;
   if (!d.virus_enabled) d.max_viruses = 0;
-  d.Ecap = cfg->blob_cap > 0 ? cfg->blob_cap : 4 * d.B + 256;
-  d.Pcap = cfg->pellet_cap > 0 ? cfg->pellet_cap : (int)std::ceil(d.max_pellets) + d.Ecap + 64;
-  d.Vcap = cfg->virus_cap > 0 ? cfg->virus_cap : 2 * (int)std::ceil(d.max_viruses) + 64;
+  auto r64 = [](int v) { return (v + 63) / 64 * 64; };  // a wavefront never straddles two arenas
+  d.Ecap = r64(cfg->blob_cap > 0 ? cfg->blob_cap : 4 * d.B + 256);
+  d.Pcap = r64(cfg->pellet_cap > 0 ? cfg->pellet_cap : (int)std::ceil(d.max_pellets) + d.Ecap + 64);
+  d.Vcap = r64(cfg->virus_cap > 0 ? cfg->virus_cap : 2 * (int)std::ceil(d.max_viruses) + 64);
   d.Wcap = std::max(kMaxCells * d.B, std::max(d.Ecap, 4096));
   d.EVcap = cfg->event_cap > 0 ? cfg->event_cap : 65536;
   d.G = G;
@@ -311,9 +315,26 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
   if (n_ticks < 0) return fail("n_ticks < 0");
   HIPCHK(hipSetDevice(h->cfg.device));
   hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  if (h->use_graph && !h->graph && !h->graph_failed && n_ticks > 0) {
+    // capture one Field.update() (~40 kernel launches) once; replay it per tick
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (ok) {
+      launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
+      ok = hipStreamEndCapture(h->stream, &g) == hipSuccess && g;
+    }
+    if (ok) ok = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok) {
+      h->graph = nullptr;
+      h->graph_failed = true;
+      (void)hipGetLastError();
+    }
+  }
   for (int t = 0; t < n_ticks; t++) {
     Mark m(h, "tick");
-    launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
+    if (h->graph) HIPCHK(hipGraphLaunch(h->graph, h->stream));
+    else launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -718,6 +739,9 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   c.n_dead = st->n_dead;
   c.rmax_cell = std::max(rmax_c, std::sqrt(10.0 / 3.141592653589793));
   c.rmax_virus = std::max(rmax_v, std::sqrt(100.0 / 3.141592653589793));
+  c.food_round = 1;  // reservation epochs restart: clear this arena's keys
+  HIPCHK(hipMemsetAsync(d.pel_owner + (size_t)arena * d.Pcap, 0, 8 * (size_t)d.Pcap, h->stream));
+  HIPCHK(hipMemsetAsync(d.b_owner + (size_t)arena * d.Ecap, 0, 8 * (size_t)d.Ecap, h->stream));
   HIPCHK(hipMemcpyAsync(d.ctl + arena, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
   // bot-side observation history restarts (NN bot reset, bot.py:151-158)
   HIPCHK(hipMemsetAsync(d.o_lastfov + p0, 0, 8 * B, h->stream));

@@ -50,6 +50,19 @@ __device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int
 __device__ __forceinline__ void atomic_max_pos(double *addr, double v) {  // v >= 0
   atomicMax((unsigned long long *)addr, (unsigned long long)__double_as_longlong(v));
 }
+// max over the wavefront, then one atomic per wave (all lanes must call; invalid
+// lanes pass 0).  A wave whose lanes target different arenas falls back to per-lane atomics.
+__device__ __forceinline__ void wave_atomic_max_pos(double *addr, double v) {
+  unsigned long long ad = (unsigned long long)addr, a0 = __shfl(ad, 0);
+  if (__all(ad == a0)) {
+    double m = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    if (__lane_id() == 0 && m > 0) atomic_max_pos(addr, m);
+  } else if (v > 0) {
+    atomic_max_pos(addr, v);
+  }
+}
 
 // centre-bucket grid iteration: every entity whose centre bucket lies in the
 // query rectangle grown by E buckets (E covers the largest footprint).
@@ -117,6 +130,8 @@ __global__ void k_update_blobs(Dev d) {
 // ------------------------------------------------------------ T4 players
 __global__ void __launch_bounds__(256) k_update_players(Dev d) {
   int gp = GTID;
+  // clear the player-hash occupancy bitmap for this tick's spawns (k_occupancy refills it)
+  for (size_t w = (size_t)gp; w < (size_t)d.A * d.occ_words; w += (size_t)gridDim.x * blockDim.x) d.occ[w] = 0;
   if (gp >= d.NP) return;
   const int NP = d.NP;
   d.p_newc[gp] = 0;
@@ -355,39 +370,45 @@ template <int KIND>
 __global__ void k_grid_count(Dev d) {
   int gi = GTID;
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
-  if (gi >= d.A * per) return;
-  int a = gi / per, i = gi - a * per;
-  double x, y, r;
-  int *rank;
-  int *cnt;
-  size_t g;
+  bool in = gi < d.A * per;
+  int a = in ? gi / per : 0, i = in ? gi - a * per : 0;
+  double x = 0, y = 0, r = 0;
+  bool ok = false;
+  int *rank, *cnt;
   if (KIND == 0) {
     int slot = i / d.B, p = i - slot * d.B;
-    g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-    if (!(d.c_flags[g] & F_ALIVE)) return;
-    x = d.c_x[g];
-    y = d.c_y[g];
-    r = d.c_r[g];
+    size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
+    ok = in && (d.c_flags[g] & F_ALIVE);
+    if (ok) {
+      x = d.c_x[g];
+      y = d.c_y[g];
+      r = d.c_r[g];
+    }
     rank = d.c_rank;
     cnt = d.ccnt;
-    atomic_max_pos(&d.ctl[a].rmax_cell, r);
   } else if (KIND == 1) {
-    g = (size_t)a * d.Ecap + i;
-    if (i >= d.ctl[a].n_blob || !(d.b_flags[g] & F_ALIVE)) return;
-    x = d.b_x[g];
-    y = d.b_y[g];
+    size_t g = (size_t)a * d.Ecap + i;
+    ok = in && i < d.ctl[a].n_blob && (d.b_flags[g] & F_ALIVE);
+    if (ok) {
+      x = d.b_x[g];
+      y = d.b_y[g];
+    }
     rank = d.b_rank;
     cnt = d.bcnt;
   } else {
-    g = (size_t)a * d.Vcap + i;
-    if (i >= d.ctl[a].n_vir || !(d.v_flags[g] & F_ALIVE)) return;
-    x = d.v_x[g];
-    y = d.v_y[g];
-    r = d.v_r[g];
+    size_t g = (size_t)a * d.Vcap + i;
+    ok = in && i < d.ctl[a].n_vir && (d.v_flags[g] & F_ALIVE);
+    if (ok) {
+      x = d.v_x[g];
+      y = d.v_y[g];
+      r = d.v_r[g];
+    }
     rank = d.v_rank;
     cnt = d.vcnt;
-    atomic_max_pos(&d.ctl[a].rmax_virus, r);
   }
+  if (KIND == 0) wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? r : 0.0);
+  if (KIND == 2) wave_atomic_max_pos(&d.ctl[a].rmax_virus, ok ? r : 0.0);
+  if (!ok) return;
   int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
   rank[(size_t)a * per + i] = atomicAdd(&cnt[(size_t)a * (d.H + 1) + b], 1);
 }
@@ -432,13 +453,73 @@ __global__ void k_grid_scatter(Dev d) {
   int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
   items[(size_t)a * per + start[(size_t)a * (d.H + 1) + b] + rank[(size_t)a * per + i]] = val;
 }
-// per-arena exclusive scan of H bucket counts into H+1 starts
+// block-wide exclusive scan of one int per thread (1024 threads); returns the
+// exclusive prefix and writes the block total to *total (shared)
+__device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  int inc = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    int v = lane < nw ? wsum[lane] : 0, vi = v;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      int y = __shfl_up(vi, off);
+      if (lane >= off) vi += y;
+    }
+    if (lane < nw) wsum[lane] = vi - v;  // exclusive wave offsets
+    if (lane == nw - 1) *total = vi;
+  }
+  __syncthreads();
+  return inc - x + wsum[w];
+}
+
+// per-arena exclusive scan of H bucket counts into H+1 starts.  One 1024-thread
+// block per arena; tiles of 16 Ki counts are staged through LDS with coalesced
+// loads/stores (padded 1 word per 32 against bank conflicts), each thread scans
+// 16 consecutive counts.  The counts are re-zeroed for the next counting pass.
+constexpr int SCAN_TILE = 16384, SCAN_PER = SCAN_TILE / 1024;
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 5); }
 __global__ void __launch_bounds__(1024) k_grid_scan(Dev d, int *cnt, int *start) {
-  __shared__ int sh[1024];
-  int a = blockIdx.x;
-  size_t o = (size_t)a * (d.H + 1);
-  int tot = block_scan_excl(cnt + o, start + o, d.H, sh);
-  if (threadIdx.x == 0) start[o + d.H] = tot;
+  __shared__ int lds[SCAN_TILE + SCAN_TILE / 32];
+  __shared__ int wsum[16];
+  __shared__ int total;
+  const int a = blockIdx.x, tid = threadIdx.x, n = d.H;
+  int *c = cnt + (size_t)a * (d.H + 1);
+  int *o = start + (size_t)a * (d.H + 1);
+  int carry = 0;
+  for (int base = 0; base < n; base += SCAN_TILE) {
+    int len = min(SCAN_TILE, n - base);
+    for (int i = tid; i < len; i += 1024) {
+      lds[scan_pad(i)] = c[base + i];
+      c[base + i] = 0;
+    }
+    __syncthreads();
+    int lo = tid * SCAN_PER, sum = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_PER; j++) {
+      int i = lo + j;
+      int v = i < len ? lds[scan_pad(i)] : 0;
+      if (i < len) lds[scan_pad(i)] = sum;
+      sum += v;
+    }
+    int ex = block_excl_1024(sum, wsum, &total) + carry;
+#pragma unroll
+    for (int j = 0; j < SCAN_PER; j++) {
+      int i = lo + j;
+      if (i < len) lds[scan_pad(i)] += ex;
+    }
+    __syncthreads();
+    for (int i = tid; i < len; i += 1024) o[base + i] = lds[scan_pad(i)];
+    carry += total;
+    __syncthreads();
+  }
+  if (tid == 0) o[n] = carry;
 }
 
 // pellet records: (src buffer [+ dead flags]) U staging -> dst buffer sorted by bucket
@@ -691,8 +772,28 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
 }
 
 // ------------------------------------------------------------ T12 cell <- virus
-__global__ void k_pv_active(Dev d) {
-  int gp = GTID;
+// wave-wide "does any entity in the grid rows around q satisfy pred"
+template <class Pred>
+__device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items, int cols, Rect q, int E, Pred pred) {
+  if (q.x1 < q.x0 || q.y1 < q.y0) return false;
+  int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
+  int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
+  const int lane = threadIdx.x & 63;
+  for (int by = by0; by <= by1; by++) {
+    int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
+    for (int t0 = lo; t0 < hi; t0 += 64) {
+      int t = t0 + lane;
+      bool hit = t < hi && pred(items ? items[t] : t);
+      if (__ballot(hit)) return true;
+    }
+  }
+  return false;
+}
+
+// one wavefront per player: cells that overlap an edible virus at phase start
+__global__ void __launch_bounds__(256) k_pv_active(Dev d) {
+  const int lane = threadIdx.x & 63;
+  const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gp >= d.NP || !d.p_alive[gp]) return;
   const int NP = d.NP, a = gp / d.B;
   int n = d.p_ncells[gp];
@@ -704,17 +805,16 @@ __global__ void k_pv_active(Dev d) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     Rect q = footprint(x, y, r, d.size);
-    bool any = false;
-    grid_visit(st, it, d.cols, q, E, [&](int j) {
+    bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int j) {
       size_t g = (size_t)a * d.Vcap + j;
-      if (any || (d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
-      if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return;
-      if (overlap(x, y, m, r, d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) && m > 1.25 * d.v_m[g]) any = true;
+      if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return false;
+      if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return false;
+      return overlap(x, y, m, r, d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) && m > 1.25 * d.v_m[g];
     });
-    d.c_active[ci] = any;
+    if (lane == 0) d.c_active[ci] = any;
     anyp |= any;
   }
-  if (anyp) {
+  if (anyp && lane == 0) {
     int w = atomicAdd(&d.ctl[a].n_pend, 1);
     if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
     else set_err(d, a, ERR_WORK_CAP);
@@ -847,18 +947,48 @@ struct Food {
   __device__ const int *start() const { return (KIND == 0 ? d.pstart : d.bstart) + (size_t)a * (d.H + 1); }
   __device__ const int *items() const { return KIND == 0 ? nullptr : d.bitems + (size_t)a * d.Ecap; }
 };
+// reservation key: higher round wins, within a round the lower priority wins.
+// Rounds are global per arena and only grow (ArenaCtl::food_round), so stale
+// keys of earlier phases never need clearing.
 __device__ __forceinline__ uint64_t food_key(uint32_t round, uint32_t prio) {
-  return ((uint64_t)round << 40) | (0xFFFFFFFFFFull - prio);
+  return ((uint64_t)round << 32) | (0xFFFFFFFFull - prio);
 }
-constexpr uint32_t kRoundMax = 0xFFFFFF;
 constexpr uint8_t kOverflow = 255;
 
+// wave-level helpers (one player per wavefront; no block barriers inside)
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// For every cell, the foods it could possibly eat this phase (R set, sorted by
+// creation sequence) and the round-1 reservation.  One wavefront per player:
+// lanes scan the candidate buckets in parallel, ballot-compact into LDS, rank
+// by sequence.  Cells with more than PREP_CAND candidates or FCAP foods in
+// reach reserve everything they may touch with a key that dominates all rounds
+// and are resolved by the serial pass.
+constexpr int PREP_CAND = 128;
 template <int KIND>
-__global__ void k_food_prep(Dev d) {
-  int gp = GTID;
-  if (gp >= d.NP || !d.p_alive[gp]) return;
+__global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
+  __shared__ int64_t s_seq[4][PREP_CAND];
+  __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
+  __shared__ int s_idx[4][PREP_CAND];
+  __shared__ uint8_t s_sel[4][PREP_CAND];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gp = blockIdx.x * 4 + w;
+  if (gp >= d.NP || !d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   Food<KIND> F(d, a);
+  const uint32_t base = d.ctl[a].food_round;
+  const int cols = d.cols;
+  const int *st = F.start();
+  const int *items = F.items();
   int n = d.p_ncells[gp];
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
@@ -866,56 +996,100 @@ __global__ void k_food_prep(Dev d) {
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     int64_t cseq = d.c_seq[ci];
     Rect q = footprint(x, y, r, d.size);
-    double sum = 0;
-    grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
-      if (!F.alive(j) || F.ej(j) == cseq) return;
-      if (!rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q)) return;
-      sum += F.m(j);
-    });
+    int cnt = 0;
+    double lsum = 0;
+    if (q.x1 >= q.x0 && q.y1 >= q.y0) {
+      int bx0 = max(0, q.x0 - 1), bx1 = min(cols - 1, q.x1 + 1);
+      int by0 = max(0, q.y0 - 1), by1 = min(cols - 1, q.y1 + 1);
+      for (int by = by0; by <= by1; by++) {
+        int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
+        for (int t0 = lo; t0 < hi; t0 += 64) {
+          int t = t0 + lane;
+          bool keep = false;
+          int j = -1;
+          double fx = 0, fy = 0, fm = 0;
+          if (t < hi) {
+            j = items ? items[t] : t;
+            if (F.alive(j) && F.ej(j) != cseq) {
+              fx = F.x(j);
+              fy = F.y(j);
+              fm = F.m(j);
+              keep = rect_hit(footprint(fx, fy, F.r(j), d.size), q);
+            }
+          }
+          unsigned long long bal = __ballot(keep);
+          int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
+          if (keep) {
+            lsum += fm;
+            if (slot < PREP_CAND) {
+              s_seq[w][slot] = F.seq(j);
+              s_x[w][slot] = fx;
+              s_y[w][slot] = fy;
+              s_m[w][slot] = fm;
+              s_idx[w][slot] = j;
+            }
+          }
+          cnt += __popcll(bal);
+        }
+      }
+    }
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
+    double sum = wave_sum(lsum);
     double M = py_min(kMaxMass, (m + sum) * (1 + 1e-9));
     double Rm = fmax(r, radius_of(M)) * (1 + 1e-9);
-    int *lst = d.f_list + ci * FCAP;
-    int cnt = 0;
-    bool ovf = false;
-    int64_t sk[FCAP];
-    grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
-      if (!F.alive(j) || F.ej(j) == cseq) return;
-      double fm = F.m(j);
-      if (!(M > 1.25 * fm)) return;
-      double fx = F.x(j), fy = F.y(j);
-      if (!((x - fx) * (x - fx) + (y - fy) * (y - fy) < Rm * Rm)) return;
-      if (!rect_hit(footprint(fx, fy, F.r(j), d.size), q)) return;
-      if (cnt == FCAP) {
-        ovf = true;
-        return;
+    wave_sync_lds();
+    int nsel = 0;
+    bool ovf = cnt > PREP_CAND;
+    if (!ovf) {
+      for (int i0 = 0; i0 < cnt; i0 += 64) {
+        int i = i0 + lane;
+        bool sel = false;
+        if (i < cnt) {
+          double fx = s_x[w][i], fy = s_y[w][i];
+          sel = (M > 1.25 * s_m[w][i]) && ((x - fx) * (x - fx) + (y - fy) * (y - fy) < Rm * Rm);
+          s_sel[w][i] = sel;
+        }
+        nsel += __popcll(__ballot(sel));
       }
-      int64_t s = F.seq(j);  // insert sorted by creation sequence
-      int t = cnt++;
-      while (t > 0 && sk[t - 1] > s) {
-        sk[t] = sk[t - 1];
-        lst[t] = lst[t - 1];
-        t--;
+      ovf = nsel > FCAP;
+    }
+    wave_sync_lds();
+    if (ovf) {  // reserve everything the cell may touch, resolved serially in priority order
+      uint64_t key = food_key(base + rounds + 1, prio);
+      if (lane == 0) {
+        d.f_cnt[ci] = kOverflow;
+        d.f_done[ci] = 0;
       }
-      sk[t] = s;
-      lst[t] = j;
-    });
-    if (ovf) {  // block every food this cell may touch; resolved by the serial pass
-      d.f_cnt[ci] = kOverflow;
-      d.f_done[ci] = 0;
-      uint64_t key = food_key(kRoundMax, prio);
-      grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
-        if (!F.alive(j)) return;
-        if (!rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q)) return;
-        atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
-      });
+      int bx0 = max(0, q.x0 - 1), bx1 = min(cols - 1, q.x1 + 1);
+      int by0 = max(0, q.y0 - 1), by1 = min(cols - 1, q.y1 + 1);
+      for (int by = by0; by <= by1; by++) {
+        int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
+        for (int t = lo + lane; t < hi; t += 64) {
+          int j = items ? items[t] : t;
+          if (F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q))
+            atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
+        }
+      }
       continue;
     }
-    d.f_cnt[ci] = (uint8_t)cnt;
-    d.f_done[ci] = (cnt == 0);
-    uint64_t key = food_key(1, prio);
-    for (int t = 0; t < cnt; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
+    int *lst = d.f_list + ci * FCAP;
+    uint64_t key = food_key(base + 1, prio);
+    for (int i0 = 0; i0 < cnt; i0 += 64) {
+      int i = i0 + lane;
+      if (i < cnt && s_sel[w][i]) {
+        int64_t sq = s_seq[w][i];
+        int rk = 0;
+        for (int jj = 0; jj < cnt; jj++) rk += (s_sel[w][jj] && s_seq[w][jj] < sq);
+        lst[rk] = s_idx[w][i];
+        atomicMax((unsigned long long *)F.owner(s_idx[w][i]), (unsigned long long)key);
+      }
+    }
+    if (lane == 0) {
+      d.f_cnt[ci] = (uint8_t)nsel;
+      d.f_done[ci] = (nsel == 0);
+    }
+    wave_sync_lds();
   }
 }
 template <int KIND>
@@ -928,7 +1102,7 @@ __global__ void k_food_reserve(Dev d, int round) {
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     if (d.f_done[ci] || d.f_cnt[ci] == kOverflow) continue;
-    uint64_t key = food_key(round, (uint32_t)p * kMaxCells + k);
+    uint64_t key = food_key(d.ctl[a].food_round + round, (uint32_t)p * kMaxCells + k);
     const int *lst = d.f_list + ci * FCAP;
     for (int t = 0; t < d.f_cnt[ci]; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
   }
@@ -970,7 +1144,7 @@ __global__ void k_food_commit(Dev d, int round, int last) {
     bool own = cnt != kOverflow;
     const int *lst = d.f_list + ci * FCAP;
     if (own) {
-      uint64_t key = food_key(round, prio);
+      uint64_t key = food_key(d.ctl[a].food_round + round, prio);
       for (int t = 0; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
     }
     if (own) {
@@ -988,12 +1162,13 @@ __global__ void k_food_commit(Dev d, int round, int last) {
   }
 }
 template <int KIND>
-__global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v) {
+__global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
   int a = blockIdx.x;
   if (threadIdx.x != 0) return;
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
+  c.food_round += rounds + 2;  // next phase's keys dominate every key written in this one
   if (nw == 0) return;
   Food<KIND> F(d, a);
   int *w = d.work + (size_t)a * d.Wcap;
@@ -1031,8 +1206,10 @@ __global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v) {
 // ------------------------------------------------------------ T16 player <- player
 __device__ __forceinline__ Rect cell_rect(const Dev &d, size_t ci) { return footprint(d.c_x[ci], d.c_y[ci], d.c_r[ci], d.size); }
 
-__global__ void k_pp_active(Dev d) {
-  int gp = GTID;
+// one wavefront per player: cells with an overlapping enemy cell at phase start
+__global__ void __launch_bounds__(256) k_pp_active(Dev d) {
+  const int lane = threadIdx.x & 63;
+  const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gp >= d.NP || !d.p_alive[gp]) return;
   const int NP = d.NP, a = gp / d.B;
   const int *st = d.cstart + (size_t)a * (d.H + 1);
@@ -1044,16 +1221,15 @@ __global__ void k_pp_active(Dev d) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     Rect q = footprint(x, y, r, d.size);
-    bool any = false;
-    grid_visit(st, it, d.cols, q, E, [&](int e) {
-      if (any || !(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return;
-      if (!rect_hit(cell_rect(d, e), q)) return;
-      if (overlap(x, y, m, r, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) any = true;
+    bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int e) {
+      if (!(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return false;
+      if (!rect_hit(cell_rect(d, e), q)) return false;
+      return overlap(x, y, m, r, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e]);
     });
-    d.c_active[ci] = any;
+    if (lane == 0) d.c_active[ci] = any;
     anyp |= any;
   }
-  if (anyp) {
+  if (anyp && lane == 0) {
     int w = atomicAdd(&d.ctl[a].n_pend, 1);
     if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
     else set_err(d, a, ERR_WORK_CAP);
@@ -1185,12 +1361,13 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
 __global__ void k_occupancy(Dev d) {
   int gi = GTID;
   int per = kMaxCells * d.B;
-  if (gi >= d.A * per) return;
-  int a = gi / per, i = gi - a * per;
+  bool in = gi < d.A * per;
+  int a = in ? gi / per : 0, i = in ? gi - a * per : 0;
   int slot = i / d.B, p = i - slot * d.B;
   size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-  if (!(d.c_flags[g] & F_ALIVE)) return;
-  atomic_max_pos(&d.ctl[a].rmax_cell, d.c_r[g]);
+  bool ok = in && (d.c_flags[g] & F_ALIVE);
+  wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? d.c_r[g] : 0.0);
+  if (!ok) return;
   Rect r = cell_rect(d, g);
   unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
   for (int by = r.y0; by <= r.y1; by++)
@@ -1466,6 +1643,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.err = c.warn = 0;
   c.rmax_cell = radius_of(kStartMass);
   c.rmax_virus = radius_of(kVirusBase);
+  c.food_round = 1;
 }
 
 // ------------------------------------------------------------ launch sequences
@@ -1477,7 +1655,6 @@ struct Scratch {
 };
 
 void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead) {
-  (void)hipMemsetAsync(d.pcnt, 0, sizeof(int) * (size_t)d.A * (d.H + 1), s);
   long n = (long)d.A * 2 * d.Pcap;
   hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
   hipLaunchKernelGGL(k_grid_scan, dim3(d.A), dim3(1024), 0, s, d, d.pcnt, d.pstart);
@@ -1489,7 +1666,6 @@ template <int KIND>
 static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start) {
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
   long n = (long)d.A * per;
-  (void)hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)d.A * (d.H + 1), s);
   if (KIND != 1) hipLaunchKernelGGL(k_reset_rmax, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, KIND == 0 ? 0 : 1);
   hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_grid_scan, dim3(d.A), dim3(1024), 0, s, d, cnt, start);
@@ -1498,15 +1674,13 @@ static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start) {
 
 template <int KIND>
 static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
-  size_t cap = KIND == 0 ? (size_t)d.Pcap : (size_t)d.Ecap;
-  (void)hipMemsetAsync(KIND == 0 ? d.pel_owner : d.b_owner, 0, sizeof(uint64_t) * d.A * cap, s);
   int g = nblk(d.NP, 256);
-  hipLaunchKernelGGL(k_food_prep<KIND>, dim3(g), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_food_prep<KIND>, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d, rounds);
   for (int r = 1; r <= rounds; r++) {
     if (r > 1) hipLaunchKernelGGL(k_food_reserve<KIND>, dim3(g), dim3(256), 0, s, d, r);
     hipLaunchKernelGGL(k_food_commit<KIND>, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
   }
-  hipLaunchKernelGGL(k_food_serial<KIND>, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v);
+  hipLaunchKernelGGL(k_food_serial<KIND>, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
 }
 
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v) {
@@ -1524,15 +1698,14 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   if (d.virus_enabled) {
     hipLaunchKernelGGL(k_vb_active, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_vb_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
-    hipLaunchKernelGGL(k_pv_active, dim3(gP), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
   }
   launch_grid<0>(d, s, d.ccnt, d.cstart);
   launch_food<0>(d, s, rounds, scr);
   launch_food<1>(d, s, rounds, scr);
-  hipLaunchKernelGGL(k_pp_active, dim3(gP), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
-  (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
   hipLaunchKernelGGL(k_occupancy, dim3(nblk((long)d.A * kMaxCells * d.B, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
@@ -1554,7 +1727,8 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.b_flags, 0, sizeof(uint32_t) * (size_t)d.A * d.Ecap, s);
   (void)hipMemsetAsync(d.p_split, 0, sizeof(int) * d.NP, s);
   (void)hipMemsetAsync(d.p_eject, 0, sizeof(int) * d.NP, s);
-  (void)hipMemsetAsync(d.ev, 0, sizeof(int64_t) * 5, s);
+  (void)hipMemsetAsync(d.pel_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Pcap, s);
+  (void)hipMemsetAsync(d.b_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Ecap, s);
   hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
   (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1);
