@@ -44,7 +44,9 @@ struct ArenaCtl {
   double rmax_cell, rmax_virus;
   uint64_t ev_order;     // serial-phase event counter
   uint32_t food_round;   // reservation epoch (grows every eat phase)
-  uint32_t pad0;
+  uint32_t scan_epoch;   // decoupled look-back epoch (grows every scan launch)
+  int scan_ticket;
+  int pad1;
 };
 
 enum : uint32_t {
@@ -122,6 +124,9 @@ struct Dev {
   double *o_lastfov;                             // [NP]
   double *o_self_lf, *o_self_slf, *o_en_lf, *o_en_slf;  // [NP][G*G]
   double *o_act_cur, *o_act_prev;                // [NP][4]
+  // decoupled look-back tile states [A][scan_tiles]
+  unsigned long long *scan_state;
+  int scan_tiles;
   // observation overflow pool (bots that see more objects than their LDS lists hold)
   int OBcap;
   int *ob_used;

@@ -169,6 +169,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.obs_ex = cfg->obs_extras;
   d.flags = cfg->flags;
   d.occ_words = (d.H + 63) / 64;
+  d.scan_tiles = (d.H + 2047) / 2048;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return fail("hipStreamCreate failed");
@@ -214,6 +215,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(o_en_lf, double, NP * GG); AL(o_en_slf, double, NP * GG); AL(o_act_cur, double, NP * 4);
   AL(o_act_prev, double, NP * 4);
   d.OBcap = (int)std::min<size_t>(std::max<size_t>(1u << 20, 64 * NP), (size_t)1 << 24);
+  AL(scan_state, unsigned long long, A * d.scan_tiles);
   AL(ob_used, int, 1); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
 #undef AL
@@ -742,6 +744,8 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   c.food_round = 1;  // reservation epochs restart: clear this arena's keys
   HIPCHK(hipMemsetAsync(d.pel_owner + (size_t)arena * d.Pcap, 0, 8 * (size_t)d.Pcap, h->stream));
   HIPCHK(hipMemsetAsync(d.b_owner + (size_t)arena * d.Ecap, 0, 8 * (size_t)d.Ecap, h->stream));
+  // look-back epochs restart too: clear this arena's tile states
+  HIPCHK(hipMemsetAsync(d.scan_state + (size_t)arena * d.scan_tiles, 0, 8 * (size_t)d.scan_tiles, h->stream));
   HIPCHK(hipMemcpyAsync(d.ctl + arena, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
   // bot-side observation history restarts (NN bot reset, bot.py:151-158)
   HIPCHK(hipMemsetAsync(d.o_lastfov + p0, 0, 8 * B, h->stream));

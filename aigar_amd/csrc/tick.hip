@@ -334,6 +334,10 @@ __global__ void __launch_bounds__(1024) k_scan_players(Dev d) {
 
 __global__ void k_finalize_players(Dev d) {
   int gp = GTID;
+  if (gp < d.NP && gp % d.B == 0) {  // grid radius bounds restart (re-maxed by every grid build)
+    d.ctl[gp / d.B].rmax_cell = 0;
+    d.ctl[gp / d.B].rmax_virus = 0;
+  }
   if (gp >= d.NP || !d.p_alive[gp]) return;
   const int NP = d.NP, a = gp / d.B;
   const ArenaCtl &c = d.ctl[a];
@@ -365,13 +369,16 @@ __global__ void k_finalize_players(Dev d) {
 }
 
 // ------------------------------------------------------------ grids
+__device__ void pgrid_finish(const Dev &d, int a, int fix);
+
 // generic counting sort by centre bucket. kind: 0 cells (pool), 1 blobs, 2 viruses
 template <int KIND>
-__global__ void k_grid_count(Dev d) {
+__global__ void k_grid_count(Dev d, int fix) {
   int gi = GTID;
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
   bool in = gi < d.A * per;
   int a = in ? gi / per : 0, i = in ? gi - a * per : 0;
+  if (fix && in && i == 0) pgrid_finish(d, a, fix);
   double x = 0, y = 0, r = 0;
   bool ok = false;
   int *rank, *cnt;
@@ -522,6 +529,119 @@ __global__ void __launch_bounds__(1024) k_grid_scan(Dev d, int *cnt, int *start)
   if (tid == 0) o[n] = carry;
 }
 
+// Single-pass multi-block exclusive scan with decoupled look-back.  Grid
+// (tiles, arenas), 256 threads, LB_TILE counts per block.  Each tile publishes
+// one self-contained 64-bit word {status:2 | epoch:30 | value:32} with an
+// agent-scope store; successors read it with agent-scope loads (L1 bypass), so
+// no other data needs ordering.  The epoch (ArenaCtl::scan_epoch, bumped by the
+// last block of every launch) makes stale words of earlier launches invisible,
+// so the state array is never cleared -- graph replays stay valid.
+constexpr int LB_TILE = 2048, LB_PER = LB_TILE / 256;
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
+__device__ __forceinline__ unsigned long long lb_word(unsigned long long st, uint32_t ep, uint32_t v) {
+  return st | ((unsigned long long)(ep & 0x3FFFFFFFu) << 32) | v;
+}
+__global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start) {
+  __shared__ int wsum[4];
+  __shared__ int s_total, s_prefix;
+  __shared__ uint32_t s_epoch;
+  const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = d.H, ntiles = gridDim.x;
+  int *c = cnt + (size_t)a * (d.H + 1);
+  int *o = start + (size_t)a * (d.H + 1);
+  unsigned long long *st = d.scan_state + (size_t)a * d.scan_tiles;
+  ArenaCtl &ctl = d.ctl[a];
+  if (tid == 0) s_epoch = __hip_atomic_load(&ctl.scan_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int base = tile * LB_TILE + tid * LB_PER;
+  int v[LB_PER], sum = 0;
+#pragma unroll
+  for (int j = 0; j < LB_PER; j++) {
+    int i = base + j;
+    v[j] = i < n ? c[i] : 0;
+    sum += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < LB_PER; j++)
+    if (base + j < n) c[base + j] = 0;  // counts re-zeroed for the next counting pass
+  // block exclusive scan of per-thread sums (4 waves)
+  int inc = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    int t0 = wsum[0], t1 = wsum[1], t2 = wsum[2], t3 = wsum[3];
+    wsum[0] = 0;
+    wsum[1] = t0;
+    wsum[2] = t0 + t1;
+    wsum[3] = t0 + t1 + t2;
+    s_total = t0 + t1 + t2 + t3;
+  }
+  __syncthreads();
+  const uint32_t ep = s_epoch;
+  const int total = s_total;
+  if (w == 0) {
+    if (tile == 0) {
+      if (lane == 0) {
+        __hip_atomic_store(&st[0], lb_word(LB_INC, ep, (uint32_t)total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = 0;
+      }
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(&st[tile], lb_word(LB_AGG, ep, (uint32_t)total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      // parallel look-back over a window of up to 64 predecessors
+      int run = 0, hi = tile - 1;
+      for (;;) {
+        int t = hi - lane;
+        unsigned long long word = 0;
+        bool ready = true;
+        if (t >= 0) {
+          word = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ready = (word >> 62) != 0 && (uint32_t)((word >> 32) & 0x3FFFFFFFu) == (ep & 0x3FFFFFFFu);
+        }
+        if (!__all(ready)) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        bool is_inc = t >= 0 && (word >> 62) == 2;
+        unsigned long long incmask = __ballot(is_inc);
+        int stop = incmask ? __ffsll((long long)incmask) - 1 : 64;  // nearest inclusive predecessor
+        int val = (t >= 0 && lane <= stop) ? (int)(uint32_t)word : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
+        run += val;
+        if (incmask || hi - 63 < 0) break;
+        hi -= 64;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(&st[tile], lb_word(LB_INC, ep, (uint32_t)(run + total)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = run;
+      }
+    }
+  }
+  __syncthreads();
+  int run = s_prefix + (inc - sum) + wsum[w];
+#pragma unroll
+  for (int j = 0; j < LB_PER; j++) {
+    int i = base + j;
+    if (i < n) o[i] = run;
+    run += v[j];
+  }
+  if (tile == ntiles - 1 && tid == 0) o[n] = s_prefix + total;
+  if (tid == 0) {  // last block of this launch bumps the epoch
+    int tk = atomicAdd(&ctl.scan_ticket, 1);
+    if (tk == ntiles - 1) {
+      ctl.scan_ticket = 0;
+      __hip_atomic_fetch_add(&ctl.scan_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // pellet records: (src buffer [+ dead flags]) U staging -> dst buffer sorted by bucket
 __global__ void k_pgrid_count(Dev d, int src, int use_dead) {
   int gi = GTID;
@@ -583,14 +703,19 @@ __global__ void k_pgrid_scatter(Dev d, int src, int use_dead) {
   d.pel_seq[dst][o] = s;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
-__global__ void k_pgrid_finish(Dev d) {
-  int a = GTID;
-  if (a >= d.A) return;
+// pellet-rebuild epilogue (also folded into the next grid-count kernel: fix 1;
+// fix 2 additionally closes the tick)
+__device__ void pgrid_finish(const Dev &d, int a, int fix) {
   ArenaCtl &c = d.ctl[a];
+  if (fix == 2) c.tick += 1;
   c.n_pel = d.pstart[(size_t)a * (d.H + 1) + d.H];
   if (c.n_pel > d.Pcap) c.n_pel = d.Pcap;
   c.n_pnew = 0;
   c.n_pel_eaten = 0;
+}
+__global__ void k_pgrid_finish(Dev d, int fix) {
+  int a = GTID;
+  if (a < d.A) pgrid_finish(d, a, fix);
 }
 
 // ------------------------------------------------------------ T10 merge
@@ -1093,21 +1218,6 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
   }
 }
 template <int KIND>
-__global__ void k_food_reserve(Dev d, int round) {
-  int gp = GTID;
-  if (gp >= d.NP || !d.p_alive[gp]) return;
-  const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
-  Food<KIND> F(d, a);
-  int n = d.p_ncells[gp];
-  for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    if (d.f_done[ci] || d.f_cnt[ci] == kOverflow) continue;
-    uint64_t key = food_key(d.ctl[a].food_round + round, (uint32_t)p * kMaxCells + k);
-    const int *lst = d.f_list + ci * FCAP;
-    for (int t = 0; t < d.f_cnt[ci]; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
-  }
-}
-template <int KIND>
 __device__ void food_eat_loop(const Dev &d, const Food<KIND> &F, int a, size_t ci, uint32_t prio, const int *lst,
                               int cnt) {
   double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
@@ -1150,6 +1260,14 @@ __global__ void k_food_commit(Dev d, int round, int last) {
     if (own) {
       food_eat_loop<KIND>(d, F, a, ci, prio, lst, cnt);
       d.f_done[ci] = 1;
+    } else if (!last && cnt != kOverflow) {
+      // reserve for the next round right away.  Safe without a separate pass: a
+      // cell that still has to wait for a lower-priority neighbour made its
+      // round-(r+1) reservation no later than this kernel, so the neighbour's
+      // key dominates at the next commit; a cell whose round-r check races with
+      // a round-(r+1) key only loses a round (it re-reserves and wins next time).
+      uint64_t key = food_key(d.ctl[a].food_round + round + 1, prio);
+      for (int t = 0; t < cnt; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
     } else if (last) {
       int w = atomicAdd(&d.ctl[a].n_pend, 1);
       if (w < d.Wcap) {
@@ -1528,12 +1646,6 @@ __global__ void k_pnew_commit(Dev d) {
   if (a >= d.A) return;
   d.ctl[a].n_pnew += d.ctl[a].n_spawn_p;
 }
-__global__ void k_reset_rmax(Dev d, int kind) {
-  int a = GTID;
-  if (a >= d.A) return;
-  if (kind == 0) d.ctl[a].rmax_cell = 0;
-  else d.ctl[a].rmax_virus = 0;
-}
 
 __global__ void k_spawn_pellets(Dev d) {
   int gi = GTID;
@@ -1585,7 +1697,9 @@ __global__ void k_spawn_players(Dev d, int init) {
   if (gi >= d.NP) return;
   int a = gi / d.B, j = gi - a * d.B;
   ArenaCtl &c = d.ctl[a];
-  if (j >= c.n_spawn_pl) return;
+  const int nsp = c.n_spawn_pl;
+  if (!init && j == 0) c.n_pnew += c.n_spawn_p;  // this tick's pellet spawns join the staging list
+  if (j >= nsp) return;
   int p = d.respawn_list[(size_t)a * d.B + j];
   int gp = a * d.B + p;
   const int NP = d.NP;
@@ -1618,11 +1732,6 @@ __global__ void k_spawn_players(Dev d, int init) {
   if (!init) ev_push(d, a, PH_SPAWN, (uint64_t)j, 10, p, seq);
 }
 
-__global__ void k_tick_end(Dev d) {
-  int a = GTID;
-  if (a >= d.A) return;
-  d.ctl[a].tick += 1;
-}
 
 // ------------------------------------------------------------ init helpers
 __global__ void k_init_ctl(Dev d, uint64_t seed) {
@@ -1644,6 +1753,8 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.rmax_cell = radius_of(kStartMass);
   c.rmax_virus = radius_of(kVirusBase);
   c.food_round = 1;
+  c.scan_epoch = 0;
+  c.scan_ticket = 0;
 }
 
 // ------------------------------------------------------------ launch sequences
@@ -1657,18 +1768,17 @@ struct Scratch {
 void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead) {
   long n = (long)d.A * 2 * d.Pcap;
   hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
-  hipLaunchKernelGGL(k_grid_scan, dim3(d.A), dim3(1024), 0, s, d, d.pcnt, d.pstart);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart);
   hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
-  hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+  // epilogue (pgrid_finish) is run by the caller's next kernel
 }
 
 template <int KIND>
-static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start) {
+static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start, int fix = 0) {
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
   long n = (long)d.A * per;
-  if (KIND != 1) hipLaunchKernelGGL(k_reset_rmax, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, KIND == 0 ? 0 : 1);
-  hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_grid_scan, dim3(d.A), dim3(1024), 0, s, d, cnt, start);
+  hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d, fix);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, cnt, start);
   hipLaunchKernelGGL(k_grid_scatter<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
 }
 
@@ -1677,7 +1787,6 @@ static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
   int g = nblk(d.NP, 256);
   hipLaunchKernelGGL(k_food_prep<KIND>, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d, rounds);
   for (int r = 1; r <= rounds; r++) {
-    if (r > 1) hipLaunchKernelGGL(k_food_reserve<KIND>, dim3(g), dim3(256), 0, s, d, r);
     hipLaunchKernelGGL(k_food_commit<KIND>, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
   }
   hipLaunchKernelGGL(k_food_serial<KIND>, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
@@ -1692,7 +1801,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
   launch_pellet_rebuild(d, s, 0, 0);  // P0 U conversions -> P1 (eat-phase buffer)
-  launch_grid<1>(d, s, d.bcnt, d.bstart);
+  launch_grid<1>(d, s, d.bcnt, d.bstart, 1);
   if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart);
   hipLaunchKernelGGL(k_merge, dim3(gP), dim3(256), 0, s, d);
   if (d.virus_enabled) {
@@ -1710,13 +1819,12 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_spawn_players, dim3(gP), dim3(256), 0, s, d, 0);
-  hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+  hipLaunchKernelGGL(k_spawn_players, dim3(gP), dim3(256), 0, s, d, 0);  // + n_pnew commit
   launch_pellet_rebuild(d, s, 1, 1);  // P1 survivors U spawns -> P0
   // the virus list was compacted by k_spawn_plan: re-index the virus grid for the
   // observations (membership stays the F_INHASH flag: spawned viruses are not hashed)
-  if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart);
-  hipLaunchKernelGGL(k_tick_end, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
+  if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart, 2);
+  else hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, 2);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty
@@ -1729,6 +1837,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.p_eject, 0, sizeof(int) * d.NP, s);
   (void)hipMemsetAsync(d.pel_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Pcap, s);
   (void)hipMemsetAsync(d.b_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Ecap, s);
+  (void)hipMemsetAsync(d.scan_state, 0, sizeof(unsigned long long) * (size_t)d.A * d.scan_tiles, s);
   hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
   (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1);
@@ -1737,6 +1846,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
   launch_pellet_rebuild(d, s, 1, 0);  // staging -> P0
+  hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, 0);
 }
 
 }  // namespace aigar
