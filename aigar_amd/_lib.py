@@ -71,6 +71,7 @@ def load(build_if_missing=False):
         "aigar_profile": [vp, i32],
         "aigar_kernel_time": [vp, C.c_char_p, dp, C.POINTER(i32)],
         "aigar_selftest_pow": [dp, dp, dp, i32],
+        "aigar_counters": [vp, i32, C.POINTER(C.c_int64), i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -174,6 +175,13 @@ class Stepper:
             self._chk(self.L.aigar_get_events(self.h, arena, out.ctypes.data_as(C.POINTER(C.c_int64)), n.value,
                                               C.byref(n)))
         return out
+
+    COUNTERS = ("vb_serial", "pv_serial", "pellet_serial", "blob_serial", "pp_serial_players", "-", "-", "ticks")
+
+    def counters(self, arena=0):
+        out = np.zeros(8, np.int64)
+        self._chk(self.L.aigar_counters(self.h, arena, out.ctypes.data_as(C.POINTER(C.c_int64)), 8))
+        return {k: int(v) for k, v in zip(self.COUNTERS, out) if k != "-"}
 
     def set_stream(self, stream_ptr):
         self._chk(self.L.aigar_set_stream(self.h, C.c_void_p(int(stream_ptr))))

@@ -47,6 +47,9 @@ struct ArenaCtl {
   uint32_t scan_epoch;   // decoupled look-back epoch (grows every scan launch)
   int scan_ticket;
   int pad1;
+  // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
+  // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
+  int64_t stat[8];
 };
 
 enum : uint32_t {
@@ -70,6 +73,7 @@ struct Dev {
   // players [NP]
   int *p_alive, *p_respawn, *p_ncells, *p_split, *p_eject, *p_pend;
   double *p_cmdx, *p_cmdy;
+  double *p_fx, *p_fy, *p_fs, *p_mass;  // FOV cache (getFovPos/getFovSize/getTotalMass at tick end)
   uint8_t *p_list;  // [16][NP]
   int *p_newc, *p_newb, *p_seqoff, *p_bloboff;
   // cells [16*NP]
@@ -88,7 +92,8 @@ struct Dev {
   int64_t *pn_seq;
   uint8_t *pel_dead;  // [A*Pcap] for the eat-phase buffer
   int *pel_rank;      // scratch [A*(Pcap)]
-  int *pcnt, *pstart; // [A*(H+1)] counts / bucket starts (pellets)
+  int *pcnt, *pstart; // [A*(H+1)] survivor counts / bucket starts (pellets)
+  int *pncnt;         // [A*(H+1)] staged-record counts (pellets)
   uint64_t *pel_owner;  // reservation keys [A*Pcap]
   // blobs [A*Ecap]
   double *b_x, *b_y, *b_m, *b_r, *b_vx, *b_vy, *b_svx, *b_svy;
@@ -129,7 +134,7 @@ struct Dev {
   int scan_tiles;
   // observation overflow pool (bots that see more objects than their LDS lists hold)
   int OBcap;
-  int *ob_used;
+  unsigned long long *ob_used;  // {observe call epoch:32 | overflow slots taken:32}
   int64_t *ob_seq;
   double *ob_m, *ob_r;
   uint32_t *ob_mask;

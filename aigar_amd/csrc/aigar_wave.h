@@ -1,0 +1,89 @@
+// aigar_wave.h -- wavefront-level helpers shared by the tick and observation
+// kernels (one 64-lane wavefront cooperating on one query).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "aigar_dev.h"
+#include "aigar_math.h"
+#include "aigar_sem.h"
+
+namespace aigar {
+
+// Wave-parallel walk over the grid rows around q (expanded by E): the rows'
+// item ranges are loaded by one lane each and flattened with a prefix sum, so
+// 64 items are inspected per step whatever the row layout.  f(valid, item) is
+// called by every lane (it may ballot); valid is false on padding lanes.
+template <class F>
+__device__ __forceinline__ void wave_grid_for(const int *st, const int *items, int cols, Rect q, int E, F f) {
+  if (q.x1 < q.x0 || q.y1 < q.y0) return;
+  const int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
+  const int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
+  const int lane = threadIdx.x & 63, nrows = by1 - by0 + 1;
+  for (int r0 = 0; r0 < nrows; r0 += 64) {
+    const int r = r0 + lane, nr = min(64, nrows - r0);
+    int lo = 0, len = 0;
+    if (r < nrows) {
+      int b = (by0 + r) * cols;
+      lo = st[b + bx0];
+      len = st[b + bx1 + 1] - lo;
+    }
+    int inc = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    const int excl = inc - len, total = __shfl(inc, 63);
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      const int t = t0 + lane;
+      int row = 0;
+      for (int k = 1; k < nr; k++) row = (__shfl(excl, k) <= t) ? k : row;
+      const int idx = __shfl(lo, row) + (t - __shfl(excl, row));
+      const bool valid = t < total;
+      f(valid, valid ? (items ? items[idx] : idx) : -1);
+    }
+  }
+}
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// getFovSize / getFovPos / getTotalMass of one player (player.py:129,156-167),
+// sequential over its cells in list order (numpy pairwise sums below 128)
+struct Fov {
+  double fx, fy, fs, mass;
+  int n;
+};
+__device__ inline Fov player_fov(const Dev &d, int gp) {
+  const int NP = d.NP;
+  Fov f;
+  int n = d.p_ncells[gp];
+  f.n = n;
+  double ms[kMaxCells], xs[kMaxCells], ys[kMaxCells];
+  double rb = -1;
+  for (int k = 0; k < n; k++) {
+    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    double m = d.c_m[ci], r = d.c_r[ci];
+    ms[k] = m;
+    xs[k] = d.c_x[ci] * m;
+    ys[k] = d.c_y[ci] * m;
+    if (k == 0 || r > rb) rb = r;
+  }
+  f.mass = n ? np_sum(ms, n) : 0.0;
+  f.fs = aigar_math::pow_cr(rb, 0.475) * aigar_math::pow_cr((double)n, 0.32) * 35;
+  f.fx = np_sum(xs, n) / f.mass;
+  f.fy = np_sum(ys, n) / f.mass;
+  return f;
+}
+// per-player FOV cache, refreshed once the world state of a tick is final
+__device__ inline void store_player_fov(const Dev &d, int gp) {
+  if (!d.p_alive[gp]) return;
+  Fov f = player_fov(d, gp);
+  d.p_fx[gp] = f.fx;
+  d.p_fy[gp] = f.fy;
+  d.p_fs[gp] = f.fs;
+  d.p_mass[gp] = f.mass;
+}
+
+}  // namespace aigar

@@ -17,9 +17,10 @@
 namespace aigar {
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
-void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype);
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch);
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
 void launch_player_stats(const Dev &d, hipStream_t s, double *out);
+void launch_player_fov(const Dev &d, hipStream_t s);
 void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd);
 }  // namespace aigar
 
@@ -46,7 +47,8 @@ struct aigar_handle {
   Dev d;
   hipStream_t stream = nullptr;
   bool own_stream = true;
-  int rounds = 4;
+  uint32_t obs_calls = 0;
+  int rounds = 2;  // parallel reservation rounds before the serial fallback (tools/micro/exp1.sh)
   int64_t *scr_k = nullptr;
   int *scr_v = nullptr;
   double *d_cmd = nullptr, *d_stats = nullptr;
@@ -146,6 +148,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   aigar_handle *h = new aigar_handle();
   h->cfg = *cfg;
   if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
+  if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(1, std::min(16, atoi(r)));  // tuning knob
   Dev &d = h->d;
   d.A = cfg->n_arenas;
   d.B = cfg->bots_per_arena;
@@ -194,7 +197,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
     AL(pel_x[b], double, P); AL(pel_y[b], double, P); AL(pel_m[b], double, P); AL(pel_seq[b], int64_t, P);
   }
   AL(pn_x, double, P); AL(pn_y, double, P); AL(pn_m, double, P); AL(pn_seq, int64_t, P);
-  AL(pel_dead, uint8_t, P); AL(pel_rank, int, 2 * P); AL(pcnt, int, A * H1); AL(pstart, int, A * H1);
+  AL(pel_dead, uint8_t, P); AL(pel_rank, int, 2 * P); AL(pcnt, int, A * H1); AL(pncnt, int, A * H1); AL(pstart, int, A * H1);
   AL(pel_owner, uint64_t, P);
   const size_t E = A * d.Ecap, V = A * d.Vcap;
   AL(b_x, double, E); AL(b_y, double, E); AL(b_m, double, E); AL(b_r, double, E); AL(b_vx, double, E);
@@ -216,7 +219,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(o_act_prev, double, NP * 4);
   d.OBcap = (int)std::min<size_t>(std::max<size_t>(1u << 20, 64 * NP), (size_t)1 << 24);
   AL(scan_state, unsigned long long, A * d.scan_tiles);
-  AL(ob_used, int, 1); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
+  AL(ob_used, unsigned long long, 1);
+  AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
 #undef AL
   h->scr_k = dalloc<int64_t>(h, A * d.Wcap);
@@ -316,7 +320,8 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
   if (!h) return fail("null handle");
   if (n_ticks < 0) return fail("n_ticks < 0");
   HIPCHK(hipSetDevice(h->cfg.device));
-  hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every step
+    hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
   if (h->use_graph && !h->graph && !h->graph_failed && n_ticks > 0) {
     // capture one Field.update() (~40 kernel launches) once; replay it per tick
     hipGraph_t g = nullptr;
@@ -351,7 +356,7 @@ extern "C" int aigar_observe(aigar_handle *h, void *out, int dtype, int on_devic
   void *dst = on_device ? out : h->d_obs;
   {
     Mark m(h, "observe");
-    launch_observe(h->d, h->stream, dst, dtype);
+    launch_observe(h->d, h->stream, dst, dtype, ++h->obs_calls);
   }
   HIPCHK(hipGetLastError());
   if (!on_device) {
@@ -751,7 +756,20 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   HIPCHK(hipMemsetAsync(d.o_lastfov + p0, 0, 8 * B, h->stream));
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
     HIPCHK(hipMemsetAsync(p + p0 * GG, 0, 8 * B * GG, h->stream));
+  launch_player_fov(d, h->stream);  // FOV cache of the loaded players
   HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n) {
+  if (!h) return fail("null handle");
+  if (arena < 0 || arena >= h->d.A) return fail("arena out of range");
+  if (!out || n < 0 || n > 8) return fail("counters: need 0 <= n <= 8 and an output array");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  ArenaCtl c;
+  HIPCHK(hipMemcpyAsync(&c, h->d.ctl + arena, sizeof c, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int k = 0; k < n; k++) out[k] = c.stat[k];
   return 0;
 }
 

@@ -15,42 +15,15 @@
 
 #include "aigar_dev.h"
 #include "aigar_sem.h"
+#include "aigar_wave.h"
 
 namespace aigar {
 
 #define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
 
-constexpr int OBS_PCAP = 512;  // visible pellets per bot kept in LDS
-constexpr int OBS_CCAP = 128;  // visible player cells
-constexpr int OBS_VCAP = 64;   // visible viruses
-
-struct Fov {
-  double fx, fy, fs, mass;
-  int n;
-};
-
-// getFovSize / getFovPos / getTotalMass for one player (sequential)
-__device__ Fov player_fov(const Dev &d, int gp) {
-  const int NP = d.NP;
-  Fov f;
-  int n = d.p_ncells[gp];
-  f.n = n;
-  double ms[kMaxCells], xs[kMaxCells], ys[kMaxCells];
-  double rb = -1;
-  for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    double m = d.c_m[ci], r = d.c_r[ci];
-    ms[k] = m;
-    xs[k] = d.c_x[ci] * m;
-    ys[k] = d.c_y[ci] * m;
-    if (k == 0 || r > rb) rb = r;
-  }
-  f.mass = n ? np_sum(ms, n) : 0.0;
-  f.fs = aigar_math::pow_cr(rb, 0.475) * aigar_math::pow_cr((double)n, 0.32) * 35;
-  f.fx = np_sum(xs, n) / f.mass;
-  f.fy = np_sum(ys, n) / f.mass;
-  return f;
-}
+constexpr int OBS_PCAP = 256;  // visible pellets per bot kept in LDS
+constexpr int OBS_CCAP = 64;   // visible player cells
+constexpr int OBS_VCAP = 32;   // visible viruses
 
 // x / y index masks of the reference's float-hash insertion loops
 __device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, double lim) {
@@ -61,8 +34,6 @@ __device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, dou
   for (double x = bl; x <= lx; x += gs) m |= 1u << min(31, (int)(x / gs));
   return m;
 }
-
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // One list of visible objects (structure of arrays).  Lives in LDS; when a
 // bot sees more objects than the LDS list holds, the same scan is repeated
@@ -82,15 +53,10 @@ struct Cand {
   uint8_t own;
 };
 
-// wave-wide append (ballot + prefix count); *count keeps the true total
-__device__ __forceinline__ void list_append(const Cand &c, ObjList &L, int cap, int *count) {
+// wave-wide append (ballot + prefix count); count is wave-uniform and keeps the true total
+__device__ __forceinline__ void list_append(const Cand &c, ObjList &L, int cap, int &count) {
   unsigned long long bal = __ballot(c.keep);
-  int before = __popcll(bal & ((1ull << lane_id()) - 1));
-  int base = *count;
-  int slot = base + before;
-  __syncthreads();  // the block is one wavefront: a cheap s_barrier
-  if (lane_id() == 0) *count = base + __popcll(bal);
-  __syncthreads();
+  int slot = count + __popcll(bal & ((1ull << __lane_id()) - 1));
   if (c.keep && slot < cap) {
     if (L.seq) L.seq[slot] = c.seq;
     if (L.m) L.m[slot] = c.m;
@@ -98,25 +64,24 @@ __device__ __forceinline__ void list_append(const Cand &c, ObjList &L, int cap, 
     L.mask[slot] = c.mask;
     if (L.own) L.own[slot] = c.own;
   }
+  count += __popcll(bal);
 }
 
-// rows [by0, by1] x buckets [bx0, bx1] of a centre-bucket grid, one candidate per lane
-template <class F>
-__device__ __forceinline__ void scan_rows(const int *st, const int *items, int cols, Rect Q, int E, F f) {
-  if (Q.x1 < Q.x0 || Q.y1 < Q.y0) return;
-  int bx0 = max(0, Q.x0 - E), bx1 = min(cols - 1, Q.x1 + E);
-  int by0 = max(0, Q.y0 - E), by1 = min(cols - 1, Q.y1 + E);
-  for (int by = by0; by <= by1; by++) {
-    int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
-    for (int t0 = lo; t0 < hi; t0 += 64) {
-      int t = t0 + lane_id();
-      f(t < hi ? (items ? items[t] : t) : -1);
-    }
-  }
+// claim n overflow slots; the pool word carries the observe-call epoch, so the
+// first claim of a call restarts it (no reset pass, no end-of-launch ticket)
+__device__ __forceinline__ int obs_claim(const Dev &d, uint32_t epoch, int n) {
+  unsigned long long old = *(volatile unsigned long long *)d.ob_used, assumed;
+  do {
+    assumed = old;
+    unsigned long long used = ((uint32_t)(assumed >> 32) == epoch) ? (assumed & 0xFFFFFFFFull) : 0;
+    unsigned long long nv = ((unsigned long long)epoch << 32) | (used + (unsigned long long)n);
+    old = atomicCAS(d.ob_used, assumed, nv);
+  } while (old != assumed);
+  return ((uint32_t)(assumed >> 32) == epoch) ? (int)(assumed & 0xFFFFFFFFull) : 0;
 }
 
 template <typename OutT>
-__global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
+__global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch) {
   __shared__ int64_t p_seq[OBS_PCAP];
   __shared__ double p_m[OBS_PCAP];
   __shared__ uint32_t p_mask[OBS_PCAP];
@@ -127,8 +92,6 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
   __shared__ double v_rad[OBS_VCAP], v_mass[OBS_VCAP];
   __shared__ int64_t v_seqs[OBS_VCAP];
   __shared__ uint32_t v_mask[OBS_VCAP];
-  __shared__ int cnt, gbase;
-  __shared__ Fov sf;
 
   const int gp = blockIdx.x, lane = threadIdx.x;
   const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
@@ -137,9 +100,9 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
     for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
     return;
   }
-  if (lane == 0) sf = player_fov(d, gp);
-  __syncthreads();
-  const double fx = sf.fx, fy = sf.fy, fs = sf.fs;
+  // FOV cache written at the end of the tick (store_player_fov)
+  const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
+  const int ncell = d.p_ncells[gp];
   const double left = fx - fs / 2, top = fy - fs / 2, gs = fs / G;
   const int cols = (int)ceil(fs / gs);
   const double lim = fs - 1;
@@ -148,32 +111,24 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
 
   // collect(run, L, cap): run the scan into the LDS list; on overflow claim a
   // slice of the global pool and rerun the scan into it.  Returns the count.
-  auto collect = [&](auto run, ObjList &Lst, int cap, ObjList G) -> int {
-    if (lane == 0) cnt = 0;
-    __syncthreads();
-    run(Lst, cap);
-    __syncthreads();
-    int n = cnt;
+  auto collect = [&](auto run, ObjList &Lst, int cap, ObjList Gp) -> int {
+    int n = run(Lst, cap);
     if (n <= cap) return n;
-    if (lane == 0) {
-      int b = atomicAdd(d.ob_used, n);
-      gbase = (b + n <= d.OBcap) ? b : -1;
-      if (gbase < 0) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
-      cnt = 0;
+    int b = 0;
+    if (lane == 0) b = obs_claim(d, epoch, n);
+    b = __shfl(b, 0);
+    if (b + n > d.OBcap) {
+      if (lane == 0) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
+      return 0;
     }
-    __syncthreads();
-    if (gbase < 0) return 0;
-    ObjList Gl = G;
-    int b = gbase;
-    if (Gl.seq) Gl.seq += b;
-    if (Gl.m) Gl.m += b;
-    if (Gl.r) Gl.r += b;
-    Gl.mask += b;
-    if (Gl.own) Gl.own += b;
-    if (Gl.perm) Gl.perm += b;
-    run(Gl, n);
-    __syncthreads();
-    Lst = Gl;
+    if (Gp.seq) Gp.seq += b;
+    if (Gp.m) Gp.m += b;
+    if (Gp.r) Gp.r += b;
+    Gp.mask += b;
+    if (Gp.own) Gp.own += b;
+    if (Gp.perm) Gp.perm += b;
+    run(Gp, n);
+    Lst = Gp;
     return n;
   };
   const ObjList Gpool{d.ob_seq, d.ob_m, d.ob_r, d.ob_mask, d.ob_own, d.ob_perm};
@@ -183,10 +138,11 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
   int np = 0;
   if (d.obs_ch & AIGAR_OBS_PELLET) {
     const int *st = d.pstart + (size_t)a * (d.H + 1);
-    auto run = [&](ObjList &Lst, int cap) {
-      scan_rows(st, nullptr, d.cols, Q, 1, [&](int t) {
+    auto run = [&](ObjList &Lst, int cap) -> int {
+      int n = 0;
+      wave_grid_for(st, nullptr, d.cols, Q, 1, [&](bool valid, int t) {
         Cand c{false, 0, 0, 0, 0, 0};
-        if (t >= 0) {
+        if (valid) {
           size_t g = (size_t)a * d.Pcap + t;
           double px = d.pel_x[0][g], py = d.pel_y[0][g], pm = d.pel_m[0][g];
           double pr = radius_of(pm);
@@ -195,8 +151,9 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
             if (ix && iy) c = Cand{true, d.pel_seq[0][g], pm, pr, ix | (iy << 16), 0};
           }
         }
-        list_append(c, Lst, cap, &cnt);
+        list_append(c, Lst, cap, n);
       });
+      return n;
     };
     np = collect(run, PL, OBS_PCAP, ObjList{Gpool.seq, Gpool.m, nullptr, Gpool.mask, nullptr, Gpool.perm});
   }
@@ -208,9 +165,10 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
     const int *st = d.cstart + (size_t)a * (d.H + 1);
     const int *it = d.citems + (size_t)a * kMaxCells * d.B;
     int E = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
-    auto run = [&](ObjList &Lst, int cap) {
+    auto run = [&](ObjList &Lst, int cap) -> int {
+      int n = 0;
       Cand c{false, 0, 0, 0, 0, 1};
-      if (lane < sf.n) {
+      if (lane < ncell) {
         size_t ci = (size_t)d.p_list[lane * NP + gp] * NP + gp;
         double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci];
         if (in_fov(x, y, r, fx, fy, fs)) {
@@ -218,18 +176,19 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
           if (ix && iy) c = Cand{true, 0, d.c_m[ci], r, ix | (iy << 16), 1};
         }
       }
-      list_append(c, Lst, cap, &cnt);
-      scan_rows(st, it, d.cols, Q, E, [&](int e) {
+      list_append(c, Lst, cap, n);
+      wave_grid_for(st, it, d.cols, Q, E, [&](bool valid, int e) {
         Cand q{false, 0, 0, 0, 0, 0};
-        if (e >= 0 && (d.c_flags[e] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && (e % NP) != gp) {
+        if (valid && (d.c_flags[e] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && (e % NP) != gp) {
           double x = d.c_x[e], y = d.c_y[e], r = d.c_r[e];
           if (rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs)) {
             uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
             if (ix && iy) q = Cand{true, 0, d.c_m[e], r, ix | (iy << 16), 0};
           }
         }
-        list_append(q, Lst, cap, &cnt);
+        list_append(q, Lst, cap, n);
       });
+      return n;
     };
     nc = collect(run, CL, OBS_CCAP, ObjList{nullptr, Gpool.m, nullptr, Gpool.mask, Gpool.own, nullptr});
   }
@@ -240,10 +199,11 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
     const int *st = d.vstart + (size_t)a * (d.H + 1);
     const int *it = d.vitems + (size_t)a * d.Vcap;
     int E = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
-    auto run = [&](ObjList &Lst, int cap) {
-      scan_rows(st, it, d.cols, Q, E, [&](int j) {
+    auto run = [&](ObjList &Lst, int cap) -> int {
+      int n = 0;
+      wave_grid_for(st, it, d.cols, Q, E, [&](bool valid, int j) {
         Cand c{false, 0, 0, 0, 0, 0};
-        if (j >= 0) {
+        if (valid) {
           size_t g = (size_t)a * d.Vcap + j;
           if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH)) {
             double x = d.v_x[g], y = d.v_y[g], vr = d.v_r[g];
@@ -253,11 +213,13 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
             }
           }
         }
-        list_append(c, Lst, cap, &cnt);
+        list_append(c, Lst, cap, n);
       });
+      return n;
     };
     nv = collect(run, VL, OBS_VCAP, ObjList{Gpool.seq, Gpool.m, Gpool.r, Gpool.mask, nullptr, nullptr});
   }
+  wave_fence();  // lists written by all lanes -> read by all lanes
   // rank pellets by creation sequence (the sum order of the reference)
   for (int i = lane; i < np; i += 64) {
     int64_t sq = PL.seq[i];
@@ -265,7 +227,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
     for (int j = 0; j < np; j++) rk += (PL.seq[j] < sq);
     PL.perm[rk] = i;
   }
-  __syncthreads();
+  wave_fence();
 
   // ---- per grid square (bot.py:387-456); lane owns squares t = lane + 64*j
   const uint32_t ch = d.obs_ch;
@@ -366,7 +328,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out) {
       d.o_lastfov[gp] = fs;
       row[o++] = (OutT)fs;
     }
-    if (ex & AIGAR_EX_MASS) row[o++] = (OutT)sf.mass;
+    if (ex & AIGAR_EX_MASS) row[o++] = (OutT)d.p_mass[gp];
     if (ex & AIGAR_EX_LAST_ACT)
       for (int k = 0; k < 4; k++) row[o++] = (OutT)d.o_act_cur[(size_t)gp * 4 + k];
     if (ex & AIGAR_EX_2LAST_ACT)
@@ -380,7 +342,7 @@ __global__ void k_policy_random(Dev d, double p_split, double p_eject, uint64_t 
   int gp = GTID;
   if (gp >= d.NP || !d.p_alive[gp]) return;
   int a = gp / d.B;
-  Fov f = player_fov(d, gp);
+  const Fov f{d.p_fx[gp], d.p_fy[gp], d.p_fs[gp], d.p_mass[gp], 0};
   uint64_t u[4];
   philox((uint64_t)gp, ST_POLICY, (uint64_t)d.ctl[a].tick, salt, d.ctl[a].key0, d.ctl[a].key1, u);
   double a0 = u01(u[0]), a1 = u01(u[1]);
@@ -403,7 +365,7 @@ __global__ void k_player_stats(Dev d, double *out) {
     o[2] = o[3] = o[4] = __builtin_nan("");
     return;
   }
-  Fov f = player_fov(d, gp);
+  const Fov f{d.p_fx[gp], d.p_fy[gp], d.p_fs[gp], d.p_mass[gp], 0};
   o[0] = 1;
   o[1] = f.mass;
   o[2] = f.fx;
@@ -420,10 +382,16 @@ __global__ void k_set_commands(Dev d, const double *cmd) {
   d.p_eject[gp] = cmd[4 * (size_t)gp + 3] != 0;
 }
 
-void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype) {
-  (void)hipMemsetAsync(d.ob_used, 0, sizeof(int), s);
-  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out);
-  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out);
+__global__ void k_player_fov(Dev d) {
+  int gp = GTID;
+  if (gp < d.NP) store_player_fov(d, gp);
+}
+void launch_player_fov(const Dev &d, hipStream_t s) {
+  hipLaunchKernelGGL(k_player_fov, dim3((d.NP + 255) / 256), dim3(256), 0, s, d);
+}
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch) {
+  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch);
+  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch);
 }
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt) {
   hipLaunchKernelGGL(k_policy_random, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, ps, pe, salt);

@@ -25,6 +25,7 @@
 
 #include "aigar_dev.h"
 #include "aigar_sem.h"
+#include "aigar_wave.h"
 
 namespace aigar {
 
@@ -486,48 +487,6 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
   return inc - x + wsum[w];
 }
 
-// per-arena exclusive scan of H bucket counts into H+1 starts.  One 1024-thread
-// block per arena; tiles of 16 Ki counts are staged through LDS with coalesced
-// loads/stores (padded 1 word per 32 against bank conflicts), each thread scans
-// 16 consecutive counts.  The counts are re-zeroed for the next counting pass.
-constexpr int SCAN_TILE = 16384, SCAN_PER = SCAN_TILE / 1024;
-__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 5); }
-__global__ void __launch_bounds__(1024) k_grid_scan(Dev d, int *cnt, int *start) {
-  __shared__ int lds[SCAN_TILE + SCAN_TILE / 32];
-  __shared__ int wsum[16];
-  __shared__ int total;
-  const int a = blockIdx.x, tid = threadIdx.x, n = d.H;
-  int *c = cnt + (size_t)a * (d.H + 1);
-  int *o = start + (size_t)a * (d.H + 1);
-  int carry = 0;
-  for (int base = 0; base < n; base += SCAN_TILE) {
-    int len = min(SCAN_TILE, n - base);
-    for (int i = tid; i < len; i += 1024) {
-      lds[scan_pad(i)] = c[base + i];
-      c[base + i] = 0;
-    }
-    __syncthreads();
-    int lo = tid * SCAN_PER, sum = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_PER; j++) {
-      int i = lo + j;
-      int v = i < len ? lds[scan_pad(i)] : 0;
-      if (i < len) lds[scan_pad(i)] = sum;
-      sum += v;
-    }
-    int ex = block_excl_1024(sum, wsum, &total) + carry;
-#pragma unroll
-    for (int j = 0; j < SCAN_PER; j++) {
-      int i = lo + j;
-      if (i < len) lds[scan_pad(i)] += ex;
-    }
-    __syncthreads();
-    for (int i = tid; i < len; i += 1024) o[base + i] = lds[scan_pad(i)];
-    carry += total;
-    __syncthreads();
-  }
-  if (tid == 0) o[n] = carry;
-}
 
 // Single-pass multi-block exclusive scan with decoupled look-back.  Grid
 // (tiles, arenas), 256 threads, LB_TILE counts per block.  Each tile publishes
@@ -541,13 +500,14 @@ constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
 __device__ __forceinline__ unsigned long long lb_word(unsigned long long st, uint32_t ep, uint32_t v) {
   return st | ((unsigned long long)(ep & 0x3FFFFFFFu) << 32) | v;
 }
-__global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start) {
+__global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, int *cnt2) {
   __shared__ int wsum[4];
   __shared__ int s_total, s_prefix;
   __shared__ uint32_t s_epoch;
   const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = d.H, ntiles = gridDim.x;
   int *c = cnt + (size_t)a * (d.H + 1);
+  int *c2 = cnt2 ? cnt2 + (size_t)a * (d.H + 1) : nullptr;  // optional second count array (summed, re-zeroed)
   int *o = start + (size_t)a * (d.H + 1);
   unsigned long long *st = d.scan_state + (size_t)a * d.scan_tiles;
   ArenaCtl &ctl = d.ctl[a];
@@ -557,12 +517,15 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start) {
 #pragma unroll
   for (int j = 0; j < LB_PER; j++) {
     int i = base + j;
-    v[j] = i < n ? c[i] : 0;
+    v[j] = i < n ? c[i] + (c2 ? c2[i] : 0) : 0;
     sum += v[j];
   }
 #pragma unroll
   for (int j = 0; j < LB_PER; j++)
-    if (base + j < n) c[base + j] = 0;  // counts re-zeroed for the next counting pass
+    if (base + j < n) {
+      if (c2) c2[base + j] = 0;  // pellets: survivor counts are rewritten whole, staged counts re-zeroed
+      else c[base + j] = 0;      // counts re-zeroed for the next counting pass
+    }
   // block exclusive scan of per-thread sums (4 waves)
   int inc = sum;
 #pragma unroll
@@ -642,55 +605,69 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start) {
   }
 }
 
-// pellet records: (src buffer [+ dead flags]) U staging -> dst buffer sorted by bucket
-__global__ void k_pgrid_count(Dev d, int src, int use_dead) {
-  int gi = GTID;
-  int per = 2 * d.Pcap;
+// Pellet records: (src buffer [- dead]) U staging -> dst buffer, sorted by
+// centre bucket.  The source is itself bucket-sorted (it is the output of the
+// previous rebuild, or of load_state's host sort) and pstart still describes
+// it, so survivors need no atomics: one thread per bucket ranks the live
+// records of its (short) range and writes the bucket's survivor count.  Staged
+// records (blob conversions, spawns) take atomic ranks in pncnt and fill their
+// bucket from the end.  Order inside a bucket carries no meaning: every
+// consumer ranks candidates by creation sequence.
+__global__ void k_pgrid_count(Dev d, int src, int use_dead, int fov) {
+  const int gi = GTID;
+  if (fov && gi < d.NP) store_player_fov(d, gi);  // player state is final here (end of tick / reset)
+  const int per = d.H + d.Pcap;
   if (gi >= d.A * per) return;
-  int a = gi / per, i = gi - a * per;
+  const int a = gi / per, i = gi - a * per;
   const ArenaCtl &c = d.ctl[a];
-  double x, y;
-  if (i < c.n_pel) {
-    size_t g = (size_t)a * d.Pcap + i;
-    if (use_dead && d.pel_dead[g]) return;
-    x = d.pel_x[src][g];
-    y = d.pel_y[src][g];
-  } else if (i - c.n_pel < c.n_pnew) {
-    size_t g = (size_t)a * d.Pcap + (i - c.n_pel);
-    x = d.pn_x[g];
-    y = d.pn_y[g];
-  } else {
+  const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
+  if (i < d.H) {  // bucket i of the source layout
+    const int lo = min(d.pstart[H1 + i], c.n_pel), hi = min(d.pstart[H1 + i + 1], c.n_pel);  // (empty source at reset)
+    int k = 0;
+    for (int t = lo; t < hi; t++) {
+      if (use_dead && d.pel_dead[(size_t)a * d.Pcap + t]) continue;
+      d.pel_rank[R0 + t] = k++;
+    }
+    d.pcnt[H1 + i] = k;
     return;
   }
-  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-  d.pel_rank[(size_t)a * per + i] = atomicAdd(&d.pcnt[(size_t)a * (d.H + 1) + b], 1);
+  const int j = i - d.H;  // staged record j
+  if (j >= c.n_pnew) return;
+  const size_t g = (size_t)a * d.Pcap + j;
+  const int b = center_bucket_coord(d.pn_y[g], d.cols) * d.cols + center_bucket_coord(d.pn_x[g], d.cols);
+  d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + b], 1);
 }
 __global__ void k_pgrid_scatter(Dev d, int src, int use_dead) {
-  int gi = GTID;
-  int per = 2 * d.Pcap;
+  const int gi = GTID;
+  const int per = 2 * d.Pcap;
   if (gi >= d.A * per) return;
-  int a = gi / per, i = gi - a * per;
+  const int a = gi / per, i = gi - a * per;
   const ArenaCtl &c = d.ctl[a];
+  const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
   double x, y, m;
   int64_t s;
-  if (i < c.n_pel) {
+  int pos;
+  if (i < d.Pcap) {
+    if (i >= c.n_pel) return;
     size_t g = (size_t)a * d.Pcap + i;
     if (use_dead && d.pel_dead[g]) return;
     x = d.pel_x[src][g];
     y = d.pel_y[src][g];
     m = d.pel_m[src][g];
     s = d.pel_seq[src][g];
-  } else if (i - c.n_pel < c.n_pnew) {
-    size_t g = (size_t)a * d.Pcap + (i - c.n_pel);
+    int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+    pos = d.pstart[H1 + b] + d.pel_rank[R0 + i];
+  } else {
+    int j = i - d.Pcap;
+    if (j >= c.n_pnew) return;
+    size_t g = (size_t)a * d.Pcap + j;
     x = d.pn_x[g];
     y = d.pn_y[g];
     m = d.pn_m[g];
     s = d.pn_seq[g];
-  } else {
-    return;
+    int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+    pos = d.pstart[H1 + b + 1] - 1 - d.pel_rank[R0 + d.Pcap + j];
   }
-  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-  int pos = d.pstart[(size_t)a * (d.H + 1) + b] + d.pel_rank[(size_t)a * per + i];
   if (pos >= d.Pcap) {
     set_err(d, a, ERR_PELLET_CAP);
     return;
@@ -817,6 +794,7 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
+  c.stat[0] += nw;
   int *w = d.work + (size_t)a * d.Wcap;
   int64_t *ck = scr_k + (size_t)a * d.Wcap;
   int *cv = scr_v + (size_t)a * d.Wcap;
@@ -903,12 +881,28 @@ __device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items
   if (q.x1 < q.x0 || q.y1 < q.y0) return false;
   int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
   int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
-  const int lane = threadIdx.x & 63;
-  for (int by = by0; by <= by1; by++) {
-    int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
-    for (int t0 = lo; t0 < hi; t0 += 64) {
-      int t = t0 + lane;
-      bool hit = t < hi && pred(items ? items[t] : t);
+  const int lane = threadIdx.x & 63, nrows = by1 - by0 + 1;
+  for (int r0 = 0; r0 < nrows; r0 += 64) {  // rows flattened as in wave_grid_for
+    const int r = r0 + lane, nr = min(64, nrows - r0);
+    int lo = 0, len = 0;
+    if (r < nrows) {
+      int b = (by0 + r) * cols;
+      lo = st[b + bx0];
+      len = st[b + bx1 + 1] - lo;
+    }
+    int inc = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    const int excl = inc - len, total = __shfl(inc, 63);
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      const int t = t0 + lane;
+      int row = 0;
+      for (int k = 1; k < nr; k++) row = (__shfl(excl, k) <= t) ? k : row;
+      const int idx = __shfl(lo, row) + (t - __shfl(excl, row));
+      bool hit = t < total && pred(items ? items[idx] : idx);
       if (__ballot(hit)) return true;
     }
   }
@@ -951,6 +945,7 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
+  c.stat[1] += nw;
   if (nw == 0) return;
   const int NP = d.NP;
   int *w = d.work + (size_t)a * d.Wcap;
@@ -1123,41 +1118,29 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
     Rect q = footprint(x, y, r, d.size);
     int cnt = 0;
     double lsum = 0;
-    if (q.x1 >= q.x0 && q.y1 >= q.y0) {
-      int bx0 = max(0, q.x0 - 1), bx1 = min(cols - 1, q.x1 + 1);
-      int by0 = max(0, q.y0 - 1), by1 = min(cols - 1, q.y1 + 1);
-      for (int by = by0; by <= by1; by++) {
-        int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
-        for (int t0 = lo; t0 < hi; t0 += 64) {
-          int t = t0 + lane;
-          bool keep = false;
-          int j = -1;
-          double fx = 0, fy = 0, fm = 0;
-          if (t < hi) {
-            j = items ? items[t] : t;
-            if (F.alive(j) && F.ej(j) != cseq) {
-              fx = F.x(j);
-              fy = F.y(j);
-              fm = F.m(j);
-              keep = rect_hit(footprint(fx, fy, F.r(j), d.size), q);
-            }
-          }
-          unsigned long long bal = __ballot(keep);
-          int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
-          if (keep) {
-            lsum += fm;
-            if (slot < PREP_CAND) {
-              s_seq[w][slot] = F.seq(j);
-              s_x[w][slot] = fx;
-              s_y[w][slot] = fy;
-              s_m[w][slot] = fm;
-              s_idx[w][slot] = j;
-            }
-          }
-          cnt += __popcll(bal);
+    wave_grid_for(st, items, cols, q, 1, [&](bool valid, int j) {
+      bool keep = false;
+      double fx = 0, fy = 0, fm = 0;
+      if (valid && F.alive(j) && F.ej(j) != cseq) {
+        fx = F.x(j);
+        fy = F.y(j);
+        fm = F.m(j);
+        keep = rect_hit(footprint(fx, fy, F.r(j), d.size), q);
+      }
+      unsigned long long bal = __ballot(keep);
+      int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
+      if (keep) {
+        lsum += fm;
+        if (slot < PREP_CAND) {
+          s_seq[w][slot] = F.seq(j);
+          s_x[w][slot] = fx;
+          s_y[w][slot] = fy;
+          s_m[w][slot] = fm;
+          s_idx[w][slot] = j;
         }
       }
-    }
+      cnt += __popcll(bal);
+    });
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
     double sum = wave_sum(lsum);
@@ -1286,6 +1269,7 @@ __global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
+  c.stat[2 + KIND] += nw;
   c.food_round += rounds + 2;  // next phase's keys dominate every key written in this one
   if (nw == 0) return;
   Food<KIND> F(d, a);
@@ -1342,7 +1326,10 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
     bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int e) {
       if (!(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return false;
       if (!rect_hit(cell_rect(d, e), q)) return false;
-      return overlap(x, y, m, r, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e]);
+      // a pair where neither side can eat stays inert until one of them grows,
+      // and every growth re-activates the cells overlapping the grown one
+      double me = d.c_m[e];
+      return overlap(x, y, m, r, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(m, me) || can_eat(me, m));
     });
     if (lane == 0) d.c_active[ci] = any;
     anyp |= any;
@@ -1355,7 +1342,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
 }
 
 // removes cell e (pool index) from its player's list; returns true if the player died
-__device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order) {
+__device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool writer = true) {
   const int NP = d.NP;
   int gp = (int)(e % NP);
   uint8_t slot = (uint8_t)(e / NP);
@@ -1371,33 +1358,51 @@ __device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order) {
     d.p_alive[gp] = 0;
     d.p_respawn[gp] = 1;
     d.dead[(size_t)a * d.B + c.n_dead++] = gp - a * d.B;
-    ev_push(d, a, PH_PP, order++, 9, gp - a * d.B, d.c_seq[e]);
+    if (writer) ev_push(d, a, PH_PP, order, 9, gp - a * d.B, d.c_seq[e]);
+    order++;
     return true;
   }
   return false;
 }
 
+__device__ __forceinline__ uint8_t active_ld(const Dev &d, size_t i) {
+  return __hip_atomic_load(&d.c_active[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void active_st(const Dev &d, size_t i, uint8_t v) {
+  __hip_atomic_store(&d.c_active[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// playerPlayerOverlap (field.py:233-244) for the players k_pp_active marked, in
+// player order, one wavefront per arena.  The sequential semantics (live cell
+// list, skip-next after a removal, break when the current cell is eaten) are
+// executed uniformly by all 64 lanes -- every lane performs the same loads and
+// stores, so program order alone orders them -- while the grid queries
+// (candidate gathering, re-activation after growth) are spread over the lanes.
+// Cross-lane data: the LDS candidate lists, the pending bitmap and c_active.
+constexpr int PP_LCAP = 1024;
 __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *scr_v) {
   extern __shared__ uint32_t pend[];  // pending-player bitmap (B bits)
-  int a = blockIdx.x;
+  __shared__ int64_t s_key[PP_LCAP];
+  __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
+  const int a = blockIdx.x, lane = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int B = d.B, NW = (B + 31) / 32;
-  int nw = min(c.n_pend, d.Wcap);
-  for (int i = threadIdx.x; i < NW; i += blockDim.x) pend[i] = 0;
-  __syncthreads();
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+  const int nw = min(c.n_pend, d.Wcap);
+  for (int i = lane; i < NW; i += 64) pend[i] = 0;
+  wave_fence();
+  for (int i = lane; i < nw; i += 64) {
     int p = d.work[(size_t)a * d.Wcap + i];
     atomicOr(&pend[p >> 5], 1u << (p & 31));
   }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+  wave_fence();
   c.n_pend = 0;
+  c.stat[4] += nw;
+  c.stat[7] += 1;
   if (nw == 0) return;
   const int NP = d.NP;
   const int *st = d.cstart + (size_t)a * (d.H + 1);
   const int *it = d.citems + (size_t)a * kMaxCells * B;
-  int64_t *ck = scr_k + (size_t)a * d.Wcap;
-  int *cv = scr_v + (size_t)a * d.Wcap;
+  const unsigned long long lt = (1ull << lane) - 1;
   uint64_t order = 0;
   double rmax = c.rmax_cell;
   int P = -1;
@@ -1411,34 +1416,46 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
     }
     if (found < 0) break;
     P = found;
-    pend[P >> 5] &= ~(1u << (P & 31));
-    int gp = a * B + P;
+    wave_fence();
+    if (lane == 0) pend[P >> 5] &= ~(1u << (P & 31));
+    wave_fence();
+    const int gp = a * B + P;
     if (!d.p_alive[gp]) continue;
     for (int i = 0; i < d.p_ncells[gp];) {  // for playerCell in player.getCells(): live list
-      size_t pc = (size_t)d.p_list[i * NP + gp] * NP + gp;
+      const size_t pc = (size_t)d.p_list[i * NP + gp] * NP + gp;
       i++;
-      if (!d.c_active[pc]) continue;
-      d.c_active[pc] = 0;
-      Rect q0 = cell_rect(d, pc);
+      if (!active_ld(d, pc)) continue;
+      active_st(d, pc, 0);
+      const Rect q0 = cell_rect(d, pc);
       int nc = 0;
-      grid_visit(st, it, d.cols, q0, expand_for(rmax), [&](int e) {
-        if (!(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return;
-        if (!rect_hit(cell_rect(d, e), q0)) return;
-        if (nc < d.Wcap) {
-          ck[nc] = d.c_seq[e];
-          cv[nc] = e;
-          nc++;
-        } else {
-          c.err |= ERR_CAND_CAP;
+      wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
+        bool keep = valid && (d.c_flags[e] & F_ALIVE) && (e % NP) != gp && rect_hit(cell_rect(d, e), q0);
+        unsigned long long bal = __ballot(keep);
+        int slot = nc + __popcll(bal & lt);
+        if (keep && slot < PP_LCAP) {
+          s_key[slot] = d.c_seq[e];
+          s_val[slot] = e;
         }
+        nc += __popcll(bal);
       });
-      isort_kv(ck, cv, nc);
+      if (nc > PP_LCAP) {
+        set_err(d, a, ERR_CAND_CAP);
+        nc = PP_LCAP;
+      }
+      wave_fence();
+      for (int x = lane; x < nc; x += 64) {  // rank by creation sequence (keys are unique)
+        int64_t k = s_key[x];
+        int rk = 0;
+        for (int y = 0; y < nc; y++) rk += s_key[y] < k;
+        s_srt[rk] = s_val[x];
+      }
+      wave_fence();
       for (int t = 0; t < nc; t++) {
-        size_t o = (size_t)cv[t];
+        const size_t o = (size_t)s_srt[t];
         if (!(d.c_flags[o] & F_ALIVE)) continue;
         if (!overlap(d.c_x[pc], d.c_y[pc], d.c_m[pc], d.c_r[pc], d.c_x[o], d.c_y[o], d.c_m[o], d.c_r[o])) continue;
         size_t g, v;
-        bool pc_eats = can_eat(d.c_m[pc], d.c_m[o]);
+        const bool pc_eats = can_eat(d.c_m[pc], d.c_m[o]);
         if (pc_eats) {
           g = pc;
           v = o;
@@ -1449,25 +1466,26 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
           continue;
         }
         // eatPlayerCell (field.py:346-348)
-        ev_push(d, a, PH_PP, order++, 8, d.c_seq[g], d.c_seq[v]);
+        if (lane == 0) ev_push(d, a, PH_PP, order, 8, d.c_seq[g], d.c_seq[v]);
+        order++;
         double m = grow_mass(d.c_m[g], d.c_m[v]);
         d.c_m[g] = m;
         d.c_r[g] = radius_of(m);
         rmax = fmax(rmax, d.c_r[g]);
-        remove_cell(d, a, v, order);
+        remove_cell(d, a, v, order, lane == 0);
         // re-activate every later turn whose outcome the growth of g may change
-        int gpl = (int)(g % NP);
-        Rect qg = cell_rect(d, g);
-        double gx = d.c_x[g], gy = d.c_y[g], gm = d.c_m[g], gr = d.c_r[g];
-        grid_visit(st, it, d.cols, qg, expand_for(rmax), [&](int e) {
-          if (!(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
+        const int gpl = (int)(g % NP);
+        const double gx = d.c_x[g], gy = d.c_y[g], gm = d.c_m[g], gr = d.c_r[g];
+        wave_grid_for(st, it, d.cols, cell_rect(d, g), expand_for(rmax), [&](bool valid, int e) {
+          if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
           if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;
-          d.c_active[e] = 1;
+          active_st(d, (size_t)e, 1);
           int pe = (int)(e % NP) - a * B;
-          if (pe > P) pend[pe >> 5] |= 1u << (pe & 31);
+          if (pe > P) atomicOr(&pend[pe >> 5], 1u << (pe & 31));
         });
-        d.c_active[g] = 1;
-        if (gpl - a * B > P) pend[(gpl - a * B) >> 5] |= 1u << ((gpl - a * B) & 31);
+        active_st(d, g, 1);
+        if (gpl - a * B > P && lane == 0) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
+        wave_fence();
         if (!pc_eats) break;
       }
     }
@@ -1755,6 +1773,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.food_round = 1;
   c.scan_epoch = 0;
   c.scan_ticket = 0;
+  for (int k = 0; k < 8; k++) c.stat[k] = 0;
 }
 
 // ------------------------------------------------------------ launch sequences
@@ -1765,11 +1784,11 @@ struct Scratch {
   int *v;
 };
 
-void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead) {
-  long n = (long)d.A * 2 * d.Pcap;
-  hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart);
-  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, d, src, use_dead);
+void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead, int fov) {
+  long nc = std::max((long)d.A * (d.H + d.Pcap), (long)d.NP), ns = (long)d.A * 2 * d.Pcap;
+  hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, src, use_dead, fov);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt);
+  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, src, use_dead);
   // epilogue (pgrid_finish) is run by the caller's next kernel
 }
 
@@ -1778,7 +1797,7 @@ static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start, int f
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
   long n = (long)d.A * per;
   hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d, fix);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, cnt, start);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, cnt, start, nullptr);
   hipLaunchKernelGGL(k_grid_scatter<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
 }
 
@@ -1800,7 +1819,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   hipLaunchKernelGGL(k_update_players, dim3(gP), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
-  launch_pellet_rebuild(d, s, 0, 0);  // P0 U conversions -> P1 (eat-phase buffer)
+  launch_pellet_rebuild(d, s, 0, 0, 0);  // P0 U conversions -> P1 (eat-phase buffer)
   launch_grid<1>(d, s, d.bcnt, d.bstart, 1);
   if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart);
   hipLaunchKernelGGL(k_merge, dim3(gP), dim3(256), 0, s, d);
@@ -1820,7 +1839,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_spawn_players, dim3(gP), dim3(256), 0, s, d, 0);  // + n_pnew commit
-  launch_pellet_rebuild(d, s, 1, 1);  // P1 survivors U spawns -> P0
+  launch_pellet_rebuild(d, s, 1, 1, 1);  // P1 survivors U spawns -> P0 (+ FOV cache)
   // the virus list was compacted by k_spawn_plan: re-index the virus grid for the
   // observations (membership stays the F_INHASH flag: spawned viruses are not hashed)
   if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart, 2);
@@ -1845,7 +1864,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
-  launch_pellet_rebuild(d, s, 1, 0);  // staging -> P0
+  launch_pellet_rebuild(d, s, 1, 0, 1);  // staging -> P0 (+ FOV cache)
   hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, 0);
 }
 

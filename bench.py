@@ -166,6 +166,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = stp.get_state()
+    work = stp.counters()
     n_total = bots * args.steps * world
     value = n_total / elapsed
 
@@ -199,7 +200,9 @@ def main():
         "breakdown_ms_per_step": {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
                                   "observe": obs_ms / max(1, obs_n)},
         "world": {"pellets": st["n_pellets"], "cells": st["n_cells"], "viruses": st["n_viruses"],
-                  "blobs": st["n_blobs"], "alive_bots": alive, "tick": int(st["tick"])},
+                  "blobs": st["n_blobs"], "alive_bots": alive, "tick": int(st["tick"]),
+                  "serial_work_per_tick": {k: round(v / max(1, work["ticks"]), 3) for k, v in work.items()
+                                           if k != "ticks"}},
     }
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget)

@@ -183,6 +183,11 @@ int aigar_sync(aigar_handle *h);
 int aigar_profile(aigar_handle *h, int enable);
 int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *launches);
 
+/* Diagnostics: per-arena work counters accumulated since reset/load_state --
+ * out[0..n) of: serial work-list entries of virusBlobOverlap, playerVirusOverlap,
+ * pellet eating, blob eating, playerPlayerOverlap (players), -, -, ticks.  n <= 8. */
+int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n);
+
 /* Diagnostics: evaluate the device's correctly rounded pow (aigar_math.h) on
  * host arrays of n (x, y) pairs -- used by the parity tests. */
 int aigar_selftest_pow(const double *x, const double *y, double *out, int n);
