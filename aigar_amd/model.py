@@ -1,0 +1,574 @@
+"""Python facade with the reference's object API over the device stepper.
+
+Mirrors the names and behaviour of the reference's hot-path objects so its
+drivers keep working:
+
+  Field   src/model/field.py     (addPlayer, initialize, reset, update, FOV/list getters)
+  Player  src/model/player.py    (setCommands, getCells, getFovPos/Size, getTotalMass, ...)
+  Cell    src/model/cell.py      (read-only view: getters and predicates)
+  Bot     src/model/bot.py       (Random / NN bots: makeMove, set_command_point,
+                                  getStateRepresentation)
+  Model   src/model/model.py     (createPlayer, createBot, initialize, resetModel, update)
+
+The world lives on the GPU.  `Field.update()` pushes every player's command and
+runs one `aigar_step`; getters read a snapshot (`aigar_get_state`) taken lazily
+once per tick, so the per-object API is a compatibility path.  The batched
+fast path is `Field.set_commands(cmd[B,4])`, `Field.step(n)` and
+`Field.observe_all(out)` (device tensors accepted).
+
+Differences a caller can see:
+ - object identity: Cell views are rebuilt each tick (compare `getId()`, the
+   creation sequence number, instead of `is`);
+ - canonical order: every set-derived list (FOV queries) is ordered by creation
+   sequence instead of CPython object addresses;
+ - randomness comes from the device's Philox stream (seeded by `seed`), not from
+   numpy's global MT19937 (colours are not modelled);
+ - Greedy bots are not available yet (device greedy policy is the next item,
+   SURVEY.md §8f).
+"""
+import math
+
+import numpy as np
+
+from . import _abi
+from ._lib import Stepper
+
+HASH_BUCKET_SIZE = 20  # parameters.py: HASH_BUCKET_SIZE
+START_MASS = 10
+MAX_COLLECTIBLE_DENSITY = 0.015
+MAX_VIRUS_DENSITY = 0.00005
+SIZE_INCREASE_PER_PLAYER = 75
+
+# reference flag name -> observation channel bit (stacking order bot.py:459-495)
+_CHANNEL_FLAGS = (
+    ("PELLET_GRID", _abi.OBS_PELLET), ("SELF_GRID", _abi.OBS_SELF), ("WALL_GRID", _abi.OBS_WALL),
+    ("ENEMY_GRID", _abi.OBS_ENEMY), ("ALL_PLAYER_GRID", _abi.OBS_ALL), ("VIRUS_GRID", _abi.OBS_VIRUS),
+    ("SELF_GRID_SLF", _abi.OBS_SELF_SLF), ("SELF_GRID_LF", _abi.OBS_SELF_LF),
+    ("ENEMY_GRID_SLF", _abi.OBS_ENEMY_SLF), ("ENEMY_GRID_LF", _abi.OBS_ENEMY_LF),
+)
+_EXTRA_FLAGS = (
+    ("USE_LAST_FOVSIZE", _abi.EX_LAST_FOV), ("USE_FOVSIZE", _abi.EX_FOV), ("USE_TOTALMASS", _abi.EX_MASS),
+    ("USE_LAST_ACTION", _abi.EX_LAST_ACT), ("USE_SECOND_LAST_ACTION", _abi.EX_2LAST_ACT),
+)
+
+
+def obs_masks(parameters):
+    """(channels, extras, grid squares) of a reference networkParameters-like object."""
+    if parameters is None:  # networkParameters.py defaults for one NN bot
+        return _abi.OBS_PELLET, _abi.EX_FOV | _abi.EX_MASS, 11
+    if getattr(parameters, "SIZE_GRID", False):
+        raise NotImplementedError("SIZE_GRID observations are not implemented")
+    if getattr(parameters, "CNN_REPR", False):
+        raise NotImplementedError("CNN observations are not implemented (grid view only)")
+    ch = 0
+    for name, bit in _CHANNEL_FLAGS:
+        if getattr(parameters, name, False):
+            ch |= bit
+    if ch & _abi.OBS_ALL:  # networkParameters.py: ALL_PLAYER_GRID disables SELF/ENEMY
+        ch &= ~(_abi.OBS_SELF | _abi.OBS_ENEMY)
+    ex = 0
+    if getattr(parameters, "EXTRA_INPUT", True):
+        for name, bit in _EXTRA_FLAGS:
+            if getattr(parameters, name, False):
+                ex |= bit
+    return ch, ex, int(getattr(parameters, "GRID_SQUARES_PER_FOV", 11))
+
+
+def _footprint(x, y, r, size):
+    """Bucket rectangle of spatialHashTable.getIdsForArea (int variant,
+    spatialHashTable.py:70-83); arrays in, (x0, x1, y0, y1) out (x1 < x0: empty)."""
+    b = HASH_BUCKET_SIZE
+    cl, ct = np.maximum(0.0, x - r), np.maximum(0.0, y - r)
+    bl = np.trunc(cl - np.mod(cl, b)).astype(np.int64)
+    bt = np.trunc(ct - np.mod(ct, b)).astype(np.int64)
+    lx = np.trunc(np.minimum(float(size), x + r + 1)).astype(np.int64)
+    ly = np.trunc(np.minimum(float(size), y + r + 1)).astype(np.int64)
+    x0, y0 = bl // b, bt // b
+    x1 = np.where(lx > bl, (bl + b * ((lx - 1 - bl) // b)) // b, x0 - 1)
+    y1 = np.where(ly > bt, (bt + b * ((ly - 1 - bt) // b)) // b, y0 - 1)
+    return x0, x1, y0, y1
+
+
+def _in_area(x, y, r, size, fov_pos, fov_size):
+    """hash.getNearbyObjectsInArea(pos, fov/2) then Cell.isInFov (field.py:422-456,
+    cell.py:169-177), as a boolean mask."""
+    if len(x) == 0:
+        return np.zeros(0, bool)
+    qx0, qx1, qy0, qy1 = _footprint(np.float64(fov_pos[0]), np.float64(fov_pos[1]), np.float64(fov_size / 2), size)
+    x0, x1, y0, y1 = _footprint(x, y, r, size)
+    near = (x0 <= x1) & (y0 <= y1) & (qx0 <= qx1) & (qy0 <= qy1) & (x0 <= qx1) & (qx0 <= x1) & (y0 <= qy1) & \
+        (qy0 <= y1)
+    h = fov_size / 2
+    inside = ~((x + r < fov_pos[0] - h) | (x - r > fov_pos[0] + h) | (y + r < fov_pos[1] - h) |
+               (y - r > fov_pos[1] + h))
+    return near & inside
+
+
+class Cell:
+    """Read-only view of one entity of a tick snapshot (cell.py:7-260)."""
+    __slots__ = ("x", "y", "mass", "radius", "velocity", "splitVelocity", "splitVelocityCounter", "mergeTime",
+                 "player", "id", "kind", "alive", "pos")
+
+    def __init__(self, kind, f, seq, svc, player=None, merge_time=0.0):
+        self.kind = kind
+        self.x, self.y, self.mass, self.radius = float(f[0]), float(f[1]), float(f[2]), float(f[3])
+        self.pos = [self.x, self.y]
+        self.velocity = [float(f[4]), float(f[5])] if len(f) > 5 else [0.0, 0.0]
+        self.splitVelocity = [float(f[6]), float(f[7])] if len(f) > 7 else [0.0, 0.0]
+        self.splitVelocityCounter = int(svc)
+        self.mergeTime = float(merge_time)
+        self.player = player
+        self.id = int(seq)
+        self.alive = True
+
+    def __repr__(self):
+        return "Cell(%s #%d m=%.3f @ %.2f,%.2f)" % (self.kind, self.id, self.mass, self.x, self.y)
+
+    # getters (cell.py:222-260)
+    def getX(self): return self.x
+    def getY(self): return self.y
+    def getPos(self): return self.pos
+    def getMass(self): return self.mass
+    def getRadius(self): return self.radius
+    def getPlayer(self): return self.player
+    def getId(self): return self.id
+    def getMergeTime(self): return self.mergeTime
+    def getSplitVelocityCounter(self): return self.splitVelocityCounter
+    def getVelocity(self): return self.velocity
+    def getSplitVelocity(self): return self.splitVelocity
+    def getReducedSpeed(self): return 3.0 * math.pow(self.mass, -0.35)
+    def getName(self): return self.player.getName() if self.player is not None else ""
+    def getColor(self): return (0, 0, 0)
+
+    # predicates (cell.py:143-189)
+    def isAlive(self): return self.alive
+    def justEjected(self): return self.splitVelocityCounter > 0
+    def canSplit(self): return self.mass > 36
+    def canEject(self): return self.mass >= 35
+    def canMerge(self): return self.mergeTime <= 0
+    def canEat(self, cell): return self.mass > 1.25 * cell.getMass()
+
+    def squaredDistance(self, cell):
+        p = cell.getPos()
+        return (self.x - p[0]) * (self.x - p[0]) + (self.y - p[1]) * (self.y - p[1])
+
+    def overlap(self, cell):
+        big, small = (self, cell) if self.getMass() > cell.getMass() else (cell, self)
+        return big.squaredDistance(small) * 1.1 < big.getRadius() * big.getRadius()
+
+    def isInFov(self, fovPos, fovSize):
+        h = fovSize / 2
+        return not (self.x + self.radius < fovPos[0] - h or self.x - self.radius > fovPos[0] + h or
+                    self.y + self.radius < fovPos[1] - h or self.y - self.radius > fovPos[1] + h)
+
+
+class Player:
+    """player.py:4-184 -- commands go to the device at the next Field.update()."""
+
+    def __init__(self, name):
+        self.name = name
+        self.field = None
+        self.index = -1
+        self.exploring = False
+        self.selected = False
+        self.commandPoint = [-1, -1]
+        self.doSplit = False
+        self.doEject = False
+        self._alive = False
+
+    def __repr__(self):
+        return "Player(%s)" % self.name
+
+    def setCommands(self, x, y, split, eject):  # player.py:99-102
+        self.commandPoint = [x, y]
+        self.doSplit = bool(split)
+        self.doEject = bool(eject)
+        if self.field is not None and self.field.stepper is not None:
+            self.field._cmd[self.index] = (x, y, float(bool(split)), float(bool(eject)))
+
+    def setSplit(self, val): self.setCommands(self.commandPoint[0], self.commandPoint[1], val, self.doEject)
+    def setEject(self, val): self.setCommands(self.commandPoint[0], self.commandPoint[1], self.doSplit, val)
+    def setMoveTowards(self, pos): self.setCommands(pos[0], pos[1], self.doSplit, self.doEject)
+    def setExploring(self, val): self.exploring = val
+    def setSelected(self, val): self.selected = val
+    def setAlive(self): self._alive = True
+
+    def _stats(self):
+        return self.field._player_stats()[self.index]
+
+    def getIsAlive(self):
+        if self.field is None or self.field.stepper is None:
+            return self._alive
+        return bool(self._stats()[0] > 0)
+
+    def getTotalMass(self):  # player.py:129-130
+        return float(self._stats()[1]) if self.getIsAlive() else 0.0
+
+    def getFovPos(self):  # player.py:156-161
+        s = self._stats()
+        return [float(s[2]), float(s[3])]
+
+    def getFovSize(self):  # player.py:163-167
+        return float(self._stats()[4])
+
+    def getFov(self):
+        return self.getFovPos(), self.getFovSize()
+
+    def getCells(self):
+        return self.field._player_cells(self.index)
+
+    def getMergableCells(self):
+        return [c for c in self.getCells() if c.canMerge()]
+
+    def getCanSplit(self):
+        cells = self.getCells()
+        return len(cells) < 16 and any(c.canSplit() for c in cells)
+
+    def getCanEject(self):
+        return any(c.canEject() for c in self.getCells())
+
+    def getRespawnTime(self):
+        return int(self.field._snapshot()["players_i"][self.index][1])
+
+    def getCommandPoint(self): return self.commandPoint
+    def getName(self): return self.name
+    def getSelected(self): return self.selected
+    def isExploring(self): return self.exploring
+    def getColor(self): return (0, 0, 0)
+
+
+class Field:
+    """field.py:28-487 over one device arena."""
+
+    def __init__(self, virusEnabled, parameters=None, seed=0, device=0, field_size=0, max_pellets=-1.0,
+                 max_viruses=-1.0, record_events=False):
+        self.virusEnabled = bool(virusEnabled)
+        self.parameters = parameters
+        self.seed = int(seed)
+        self.device = device
+        self.field_size = field_size
+        self.max_pellets, self.max_viruses = max_pellets, max_viruses
+        self.record_events = record_events
+        self.players = []
+        self.stepper = None
+        self.size = 0
+        self._resets = 0
+        self._cache = {}
+
+    # ---- lifecycle
+    def addPlayer(self, player):  # field.py:414-416
+        if self.stepper is not None:
+            raise RuntimeError("players must be added before initialize() (the device world is sized then)")
+        player.setAlive()
+        player.field = self
+        player.index = len(self.players)
+        self.players.append(player)
+
+    def _config(self):
+        ch, ex, g = obs_masks(self.parameters)
+        if not self.virusEnabled:
+            ch &= ~_abi.OBS_VIRUS
+        c = _abi.Config()
+        c.n_arenas, c.bots_per_arena = 1, len(self.players)
+        c.field_size = int(self.field_size)
+        c.virus_enabled = int(self.virusEnabled)
+        c.max_pellets, c.max_viruses = float(self.max_pellets), float(self.max_viruses)
+        c.grid_squares, c.obs_channels, c.obs_extras = g, ch, ex
+        c.rng_mode, c.device = _abi.RNG_PHILOX, self.device
+        c.flags = _abi.FLAG_EVENTS if self.record_events else 0
+        return c
+
+    def initialize(self):  # field.py:57-67
+        if not self.players:
+            raise RuntimeError("Field.initialize() needs at least one player")
+        if self.stepper is None:
+            self.stepper = Stepper(self._config())
+            self._cmd = np.zeros((len(self.players), 4))
+            self._cmd[:, :2] = -1
+        self.stepper.reset(self.seed)
+        self.size = int(self.stepper.get_state()["field_size"])
+        self._cache = {}
+
+    def reset(self):  # field.py:69-83
+        self._resets += 1
+        self.stepper.reset(self.seed + 7919 * self._resets)
+        self._cache = {}
+
+    def update(self):  # field.py:85-92
+        self.stepper.set_commands(self._cmd)
+        self.stepper.step(1)
+        self._cache = {}
+
+    # ---- batched fast path
+    def set_commands(self, cmd):
+        """cmd[B, 4] = (x, y, split, eject) for every player (numpy or device tensor)."""
+        self.stepper.set_commands(cmd)
+
+    def step(self, n=1):
+        self.stepper.step(n)
+        self._cache = {}
+
+    def observe_all(self, out=None, dtype=np.float64):
+        """Bot.getStateRepresentation() of every player, [B, L] (NaN rows for dead players)."""
+        return self.stepper.observe(out, dtype)
+
+    def events(self):
+        """Ordered (tick, code, a, b) rows of the last step (record_events=True)."""
+        return self.stepper.events()
+
+    # ---- snapshot-backed compatibility getters
+    def _snapshot(self):
+        if "state" not in self._cache:
+            self._cache["state"] = self.stepper.get_state()
+        return self._cache["state"]
+
+    def _player_stats(self):
+        if "stats" not in self._cache:
+            self._cache["stats"] = self.stepper.player_stats()
+        return self._cache["stats"]
+
+    def _views(self):
+        if "views" in self._cache:
+            return self._cache["views"]
+        st = self._snapshot()
+        per_player = [[] for _ in self.players]
+        cells = []
+        for f, i in zip(st["cells_f"], st["cells_i"]):
+            c = Cell("player", f[:8], i[2], i[1], self.players[int(i[0])], f[8])
+            per_player[int(i[0])].append(c)
+            cells.append(c)
+        pel = [Cell("pellet", f, s, 0) for f, s in zip(st["pellets_f"], st["pellets_seq"])]
+        blobs = [Cell("blob", f, i[1], i[0]) for f, i in zip(st["blobs_f"], st["blobs_i"])]
+        vir = [Cell("virus", f, i[1], i[0]) for f, i in zip(st["viruses_f"], st["viruses_i"])]
+        v = {"per_player": per_player, "cells": cells, "pellets": pel, "blobs": blobs, "viruses": vir,
+             "cell_hashed": np.asarray(st["cells_i"])[:, 3] != 0 if len(cells) else np.zeros(0, bool),
+             "virus_hashed": np.asarray(st["viruses_i"])[:, 2] != 0 if len(vir) else np.zeros(0, bool)}
+        self._cache["views"] = v
+        return v
+
+    def _player_cells(self, index):
+        return list(self._views()["per_player"][index])
+
+    def _query(self, objs, fov_pos, fov_size, member=None):
+        if not objs:
+            return []
+        x = np.array([o.x for o in objs])
+        y = np.array([o.y for o in objs])
+        r = np.array([o.radius for o in objs])
+        m = _in_area(x, y, r, self.size, fov_pos, fov_size)
+        if member is not None:
+            m &= member
+        sel = [objs[k] for k in np.nonzero(m)[0]]
+        sel.sort(key=lambda o: o.id)  # canonical order of the hash's set
+        return sel
+
+    # getters (field.py:418-487)
+    def getVirusEnabled(self): return self.virusEnabled
+    def getWidth(self): return self.size
+    def getHeight(self): return self.size
+    def getPlayers(self): return self.players
+    def getPellets(self): return self._views()["pellets"]
+    def getBlobs(self): return self._views()["blobs"]
+    def getViruses(self): return self._views()["viruses"]
+    def getPlayerCells(self): return list(self._views()["cells"])
+
+    def getDeadPlayers(self):
+        return [self.players[int(p)] for p in self._snapshot()["dead"]]
+
+    @staticmethod
+    def getPortionOfCellsInFov(cells, fovPos, fovSize):
+        return [c for c in cells if c.isInFov(fovPos, fovSize)]
+
+    def getPlayerCellsInFov(self, fovPos, fovSize):
+        v = self._views()
+        return self._query(v["cells"], fovPos, fovSize, v["cell_hashed"])
+
+    def getFoVPlayerCellsInFov(self, fovPlayer):
+        return [c for c in self.getPlayerCellsInFov(fovPlayer.getFovPos(), fovPlayer.getFovSize())
+                if c.getPlayer() is fovPlayer]
+
+    def getEnemyPlayerCellsInFov(self, fovPlayer):
+        return [c for c in self.getPlayerCellsInFov(fovPlayer.getFovPos(), fovPlayer.getFovSize())
+                if c.getPlayer() is not fovPlayer]
+
+    def getEnemyPlayerCellsInGivenFov(self, fovPlayer, fovPos, fovSize):
+        return [c for c in self.getPlayerCellsInFov(fovPos, fovSize) if c.getPlayer() is not fovPlayer]
+
+    def getPelletsInFov(self, fovPos, fovSize):
+        return self._query(self._views()["pellets"], fovPos, fovSize)
+
+    def getVirusesInFov(self, fovPos, fovSize):
+        v = self._views()
+        return self._query(v["viruses"], fovPos, fovSize, v["virus_hashed"])
+
+    def getBlobsInFov(self, fovPos, fovSize):
+        return self._query(self._views()["blobs"], fovPos, fovSize)
+
+    @staticmethod
+    def getReward(player):
+        return player.getTotalMass()
+
+    # observation for the bots: one device call per tick, rows served per bot
+    def _observation(self):
+        if "obs" not in self._cache:
+            self._cache["obs"] = self.stepper.observe()
+        return self._cache["obs"]
+
+    def _set_actions(self, bots):
+        cur = np.zeros((len(self.players), 4))
+        prev = np.zeros((len(self.players), 4))
+        for b in bots:
+            for arr, act in ((cur, b.currentAction), (prev, b.lastAction)):
+                if act is not None:
+                    a = list(act)[:4]
+                    arr[b.player.index, :len(a)] = a
+        self.stepper.set_actions(cur, prev)
+
+
+class Bot:
+    """bot.py:23-710, Random and NN bot types.  NN bots get their actions from
+    the caller (`currentAction` / `set_command_point`), as the reference's
+    learners supply them."""
+
+    def __init__(self, player, field, bot_type, learningAlg=None, parameters=None):
+        if bot_type not in ("Random", "NN"):
+            raise NotImplementedError("bot type %r: only Random and NN bots run on the device stepper so far"
+                                      % bot_type)
+        self.player, self.field, self.type = player, field, bot_type
+        self.learningAlg = learningAlg
+        self.parameters = parameters
+        self.time = 0
+        self.totalMasses = []
+        self.currentAction = [0, 0, 0, 0] if bot_type == "Random" else None
+        self.lastAction = None
+        self.currentlySkipping = False
+        self.reset()
+
+    def __repr__(self):
+        return "%s bot (%s)" % (self.type, self.player)
+
+    def reset(self):  # bot.py:125-164
+        if self.learningAlg is not None and hasattr(self.learningAlg, "reset"):
+            self.learningAlg.reset()
+        self.lastMass = None
+        self.cumulativeReward = 0
+        self.lastReward = 0
+        if self.type == "NN":
+            self.currentAction = None
+
+    def _param(self, name, default):
+        return getattr(self.parameters, name, default) if self.parameters is not None else default
+
+    def make_random_bot_move(self):  # bot.py:243-249
+        if self.time % self._param("FRAME_SKIP_RATE", 7) == 0:
+            self.currentAction[0] = np.random.random()
+            self.currentAction[1] = np.random.random()
+            self.currentAction[2] = np.random.random() if self._param("ENABLE_SPLIT", False) else False
+            self.currentAction[3] = np.random.random() if self._param("ENABLE_EJECT", False) else False
+        self.time += 1
+
+    def makeMove(self):  # bot.py:252-269
+        self.totalMasses.append(self.player.getTotalMass())
+        if not self.player.getIsAlive():
+            return
+        if self.type == "Random":
+            self.make_random_bot_move()
+        if self.currentAction is None:
+            return
+        action = list(self.currentAction)
+        if self.currentlySkipping:
+            action[2:] = [0, 0]
+        self.set_command_point(action)
+
+    def set_command_point(self, action):  # bot.py:550-577
+        mid = self.player.getFovPos()
+        size = self.player.getFovSize()
+        x, y = int(mid[0]), int(mid[1])
+        left, top = x - int(size / 2), y - int(size / 2)
+        size = int(size)
+        split = eject = False
+        if len(action) > 2:
+            if len(action) == 3:
+                if self._param("ENABLE_SPLIT", False):
+                    split = action[2] > 0.5
+                elif self._param("ENABLE_EJECT", False):
+                    # the reference evaluates `[3] > 0.5` here (bot.py:568): a TypeError in Python 3
+                    raise TypeError("'>' not supported between instances of 'list' and 'float'")
+            else:
+                split, eject = action[2] > 0.5, action[3] > 0.5
+        self.player.setCommands(left + action[0] * size, top + action[1] * size, split, eject)
+
+    def getStateRepresentation(self):  # bot.py:272-299 (grid view, MLP layout)
+        if not self.player.getIsAlive():
+            return None
+        row = self.field._observation()[self.player.index]
+        return row.reshape(1, -1).copy()
+
+    def getPlayer(self): return self.player
+    def getType(self): return self.type
+    def getLearningAlg(self): return self.learningAlg
+    def getCurrentAction(self): return self.currentAction
+    def getMassOverTime(self): return self.totalMasses
+
+
+class Model:
+    """model.py:48-200: the tick driver."""
+
+    def __init__(self, guiEnabled=False, viewEnabled=False, parameters=None, seed=0, device=0, **field_kw):
+        self.guiEnabled, self.viewEnabled = guiEnabled, viewEnabled
+        self.parameters = parameters
+        self.virusEnabled = bool(getattr(parameters, "VIRUS_SPAWN", False)) if parameters is not None else False
+        self.resetLimit = getattr(parameters, "RESET_LIMIT", 20000) if parameters is not None else 20000
+        self.players, self.bots, self.humans = [], [], []
+        self.field = Field(self.virusEnabled, parameters, seed=seed, device=device, **field_kw)
+        self.counter = 0
+
+    def createPlayer(self, name):  # model.py:149-152
+        p = Player(name)
+        self.addPlayer(p)
+        return p
+
+    def createBot(self, botType, learningAlg=None, parameters=None):  # model.py:154-162
+        name = botType + str(len(self.bots))
+        p = self.createPlayer(name)
+        bot = Bot(p, self.field, botType, learningAlg, parameters if parameters is not None else self.parameters)
+        self.addBot(bot)
+        return bot
+
+    def addPlayer(self, player):
+        self.players.append(player)
+        self.field.addPlayer(player)
+
+    def addBot(self, bot):
+        self.bots.append(bot)
+
+    def initialize(self):  # model.py:89-92
+        self.field.initialize()
+        self.resetBots()
+
+    def resetModel(self):  # model.py:94-96
+        self.field.reset()
+        self.counter = 0
+
+    def takeBotActions(self):
+        for bot in self.bots:
+            bot.makeMove()
+
+    def resetBots(self):
+        for bot in self.bots:
+            bot.reset()
+
+    def update(self):  # model.py:98-111
+        self.counter += 1
+        nn = [b for b in self.bots if b.type == "NN"]
+        if nn and self.parameters is not None and (getattr(self.parameters, "USE_LAST_ACTION", False) or
+                                                   getattr(self.parameters, "USE_SECOND_LAST_ACTION", False)):
+            self.field._set_actions(nn)
+        self.takeBotActions()
+        self.field.update()
+
+    # getters
+    def getField(self): return self.field
+    def getPlayers(self): return self.players
+    def getBots(self): return self.bots
+    def getHumans(self): return self.humans

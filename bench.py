@@ -60,6 +60,21 @@ def obs_bytes_per_bot(L, p_fov, c_fov, v_fov, n_cells=1.2):
     return n_cells * 33 + p_fov * 32 + c_fov * 36 + v_fov * 44 + 2 * 2 * 121 * 8 + L * 8
 
 
+def pmc_traffic(kernel_prefix, workload):
+    """HBM-side bytes per launch of the kernel from the newest committed PMC
+    summary (profiles/r*_pmc_<workload>.json, written by tools/pmc.sh +
+    tools/pmc_summary.py on the same bench command).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % workload)))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for k, v in data.items():
+        if kernel_prefix in k:
+            return float(v["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(name, budget_s=12.0, seed=1):
     """Single-thread C oracle (CPU port of the reference) on the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -183,8 +198,11 @@ def main():
     obs_avg_s = (obs_ms / max(1, obs_n)) / 1e3
     achieved = obs_bytes_launch / obs_avg_s / 1e9
     peak = 8000.0
+    traffic, traffic_src = pmc_traffic("k_observe", name)
     roofline = {"bound": "hbm", "kernel": "k_observe", "achieved": round(achieved, 2), "peak": peak,
-                "unit": "GB/s", "frac": achieved / peak, "traffic": None,
+                "unit": "GB/s", "frac": achieved / peak,
+                "traffic": None if traffic is None else int(traffic),
+                "traffic_source": traffic_src,
                 "bytes_per_launch": int(obs_bytes_launch), "avg_launch_ms": obs_avg_s * 1e3}
 
     out = {
