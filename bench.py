@@ -26,25 +26,27 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from aigar_amd import _abi  # noqa: E402
+from aigar_amd import _abi, replicas  # noqa: E402
 
 # C3 observation config: VIRUS_SPAWN + ENABLE_SPLIT (networkParameters.py:76-96)
 C3_CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
          | _abi.OBS_ENEMY_LF)
 C3_EX = _abi.EX_LAST_FOV | _abi.EX_FOV | _abi.EX_MASS | _abi.EX_LAST_ACT
 
+MULTI_CH = _abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY
 WORKLOADS = {
-    # name: (bots, field, pellets, virus, p_split, p_eject, channels, extras)
-    "c3": (4096, 4800, 100000.0, True, 2.5e-3, 1e-2, C3_CH, C3_EX),
-    "c2": (256, 1200, 10000.0, False, 0.0, 0.0, _abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY,
-           _abi.EX_FOV | _abi.EX_MASS),
+    # name: (bots per arena, field, pellets, virus, p_split, p_eject, channels, extras, arenas per GPU)
+    "c3": (4096, 4800, 100000.0, True, 2.5e-3, 1e-2, C3_CH, C3_EX, 1),
+    "c2": (256, 1200, 10000.0, False, 0.0, 0.0, MULTI_CH, _abi.EX_FOV | _abi.EX_MASS, 1),
+    # C5: 64 arenas x 512 bots over 8 GPUs = 8 arenas per GPU
+    "c5": (512, 1697, 43200.0, False, 0.0, 0.0, MULTI_CH, _abi.EX_FOV | _abi.EX_MASS, 8),
 }
 
 
 def make_cfg(name, device=0, flags=0):
-    bots, field, pellets, virus, _, _, ch, ex = WORKLOADS[name]
+    bots, field, pellets, virus, _, _, ch, ex, arenas = WORKLOADS[name]
     c = _abi.Config()
-    c.n_arenas, c.bots_per_arena, c.field_size = 1, bots, field
+    c.n_arenas, c.bots_per_arena, c.field_size = arenas, bots, field
     c.virus_enabled = int(virus)
     c.max_pellets, c.max_viruses = pellets, -1.0
     c.grid_squares, c.obs_channels, c.obs_extras = 11, ch, ex
@@ -79,7 +81,8 @@ def cpu_baseline(name, budget_s=12.0, seed=1):
     """Single-thread C oracle (CPU port of the reference) on the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle  # test infrastructure: the checker / CPU baseline only
-    bots, field, pellets, virus, ps, pe, ch, ex = WORKLOADS[name]
+    bots, field, pellets, virus, ps, pe, ch, ex, arenas = WORKLOADS[name]
+    bots *= arenas
     cfg = make_cfg(name, flags=0)
     o = Oracle(cfg)
     o.reset(seed)
@@ -129,25 +132,21 @@ def main():
     args = ap.parse_args()
 
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = replicas.world_from_env()
     dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(local)
+    if world > 1:  # one process per GPU, independent replicas (weak scaling)
+        dist = replicas.init("nccl")
     from aigar_amd import _lib  # raises if libaigar_hip.so is missing: no fallback
 
     name = args.workload
-    bots, field, pellets, virus, ps, pe, ch, ex = WORKLOADS[name]
+    bots, field, pellets, virus, ps, pe, ch, ex, arenas = WORKLOADS[name]
+    bots *= arenas  # players stepped per GPU
     stp = _lib.Stepper(make_cfg(name, device=local))
     stream = torch.cuda.current_stream()
     stp.set_stream(stream.cuda_stream)
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
-    stp.reset(args.seed + 7919 * rank)
+    stp.reset(replicas.rank_seed(args.seed, rank))
 
     def one_step():
         stp.policy_random(ps, pe, args.seed)
@@ -160,15 +159,13 @@ def main():
     stp.sync()
     stats = stp.player_stats()
     stp.profile(True)
-    if dist is not None:
-        dist.barrier()
+    replicas.barrier(dist)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    replicas.barrier(dist)
     t1 = time.perf_counter()
     elapsed = t1 - t0
     obs_ms, obs_n = stp.kernel_time("observe")
@@ -176,14 +173,10 @@ def main():
     pol_ms, pol_n = stp.kernel_time("policy")
     stp.profile(False)
     stp.sync()  # raises on any device-side capacity error
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = replicas.max_over_ranks(dist, elapsed, device="cuda")
     st = stp.get_state()
     work = stp.counters()
-    n_total = bots * args.steps * world
-    value = n_total / elapsed
+    value = replicas.job_throughput(bots * args.steps, world, elapsed)
 
     # roofline of the dominant kernel (k_observe): algorithmic bytes per launch / avg duration
     alive = int(np.sum(stats[:, 0] > 0))
@@ -210,9 +203,10 @@ def main():
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox bot population, random-action policy)",
-        "config": {"workload": "%s: %d bots, %d pellets, %s viruses, split p=%g, eject p=%g, field %d, "
-                               "obs %d floats/bot" % (name.upper(), bots, int(pellets),
-                                                      "1152" if virus else "no", ps, pe, field, stp.obs_len),
+        "config": {"workload": "%s: %s%d bots, %d pellets, %s viruses, split p=%g, eject p=%g, field %d, "
+                               "obs %d floats/bot" % (name.upper(), "%d arenas x " % arenas if arenas > 1 else "",
+                                                      bots // arenas, int(pellets), "1152" if virus else "no", ps,
+                                                      pe, field, stp.obs_len),
                    "parallelism": "replicas%d" % world if world > 1 else "single-gpu"},
         "roofline": roofline,
         "breakdown_ms_per_step": {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
