@@ -13,17 +13,35 @@ namespace aigar {
 // item ranges are loaded by one lane each and flattened with a prefix sum, so
 // 64 items are inspected per step whatever the row layout.  f(valid, item) is
 // called by every lane (it may ballot); valid is false on padding lanes.
+// Buckets of a centre-bucket grid covering footprint q grown by E fine
+// buckets.  Grids of the small entity sets (viruses, blobs) are coarsened by
+// 2^shift fine buckets per side (Dev::cshift); every consumer still applies
+// the exact reference membership test, so coarsening only adds candidates.
+struct Span {
+  int bx0, bx1, by0, by1, stride;
+};
+__device__ __forceinline__ Span grid_span(Rect q, int E, int cols, int shift) {
+  Span s;
+  s.bx0 = max(0, q.x0 - E) >> shift;
+  s.bx1 = min(cols - 1, q.x1 + E) >> shift;
+  s.by0 = max(0, q.y0 - E) >> shift;
+  s.by1 = min(cols - 1, q.y1 + E) >> shift;
+  s.stride = (cols + (1 << shift) - 1) >> shift;
+  return s;
+}
+
 template <class F>
-__device__ __forceinline__ void wave_grid_for(const int *st, const int *items, int cols, Rect q, int E, F f) {
+__device__ __forceinline__ void wave_grid_for(const int *st, const int *items, int cols, Rect q, int E, F f,
+                                              int shift = 0) {
   if (q.x1 < q.x0 || q.y1 < q.y0) return;
-  const int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
-  const int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
-  const int lane = threadIdx.x & 63, nrows = by1 - by0 + 1;
+  const Span g = grid_span(q, E, cols, shift);
+  const int bx0 = g.bx0, bx1 = g.bx1, by0 = g.by0, cols_ = g.stride;
+  const int lane = threadIdx.x & 63, nrows = g.by1 - by0 + 1;
   for (int r0 = 0; r0 < nrows; r0 += 64) {
     const int r = r0 + lane, nr = min(64, nrows - r0);
     int lo = 0, len = 0;
     if (r < nrows) {
-      int b = (by0 + r) * cols;
+      int b = (by0 + r) * cols_;
       lo = st[b + bx0];
       len = st[b + bx1 + 1] - lo;
     }

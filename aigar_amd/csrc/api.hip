@@ -173,6 +173,9 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.flags = cfg->flags;
   d.occ_words = (d.H + 63) / 64;
   d.scan_tiles = (d.H + 2047) / 2048;
+  d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (k_grid_small)
+  while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
+    d.cshift++;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return fail("hipStreamCreate failed");
@@ -582,17 +585,18 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
 
 // counting sort of items by centre bucket (host side, used by load_state)
 static void host_grid(int cols, const std::vector<double> &x, const std::vector<double> &y, std::vector<int> &start,
-                      std::vector<int> &order) {
-  int H = cols * cols;
+                      std::vector<int> &order, int shift = 0) {
+  const int cc = (cols + (1 << shift) - 1) >> shift;
+  int H = cc * cc;
   start.assign(H + 1, 0);
   std::vector<int> b(x.size());
   for (size_t i = 0; i < x.size(); i++) {
     auto cb = [&](double v) {
       int q = (int)(v / 20);
       if (v < 0) q = 0;
-      return q < cols ? q : cols - 1;
+      return (q < cols ? q : cols - 1) >> shift;
     };
-    b[i] = cb(y[i]) * cols + cb(x[i]);
+    b[i] = cb(y[i]) * cc + cb(x[i]);
     start[b[i] + 1]++;
   }
   for (int i = 0; i < H; i++) start[i + 1] += start[i];
@@ -728,8 +732,8 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
       h2d(h, d.b_flags + bo, bfl) || h2d(h, d.v_svc + vo, vsvc) || h2d(h, d.v_seq + vo, vseq) ||
       h2d(h, d.v_flags + vo, vfl))
     return -1;
-  host_grid(d.cols, vgx, vgy, start, order);
-  HIPCHK(hipMemcpyAsync(d.vstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
+  host_grid(d.cols, vgx, vgy, start, order, d.cshift);
+  HIPCHK(hipMemcpyAsync(d.vstart + arena * H1, start.data(), 4 * start.size(), hipMemcpyHostToDevice, h->stream));
   if (!order.empty()) HIPCHK(hipMemcpyAsync(d.vitems + vo, order.data(), 4 * order.size(), hipMemcpyHostToDevice, h->stream));
   // control block
   ArenaCtl c;

@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
           }
         }
         list_append(c, Lst, cap, n);
-      });
+      }, d.cshift);
       return n;
     };
     nv = collect(run, VL, OBS_VCAP, ObjList{Gpool.seq, Gpool.m, Gpool.r, Gpool.mask, nullptr, nullptr});

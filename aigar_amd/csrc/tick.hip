@@ -68,12 +68,12 @@ __device__ __forceinline__ void wave_atomic_max_pos(double *addr, double v) {
 // centre-bucket grid iteration: every entity whose centre bucket lies in the
 // query rectangle grown by E buckets (E covers the largest footprint).
 template <class F>
-__device__ __forceinline__ void grid_visit(const int *start, const int *items, int cols, Rect q, int E, F f) {
+__device__ __forceinline__ void grid_visit(const int *start, const int *items, int cols, Rect q, int E, F f,
+                                           int shift = 0) {
   if (q.x1 < q.x0 || q.y1 < q.y0) return;
-  int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
-  int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
-  for (int by = by0; by <= by1; by++) {
-    int lo = start[by * cols + bx0], hi = start[by * cols + bx1 + 1];
+  const Span g = grid_span(q, E, cols, shift);
+  for (int by = g.by0; by <= g.by1; by++) {
+    int lo = start[by * g.stride + g.bx0], hi = start[by * g.stride + g.bx1 + 1];
     for (int t = lo; t < hi; t++) f(items ? items[t] : t);
   }
 }
@@ -488,6 +488,52 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
 }
 
 
+// Grids of the small entity sets (blobs, viruses): one 1024-thread block per
+// arena runs the whole counting sort in LDS on a grid coarsened by
+// 2^cshift (<= SG_CAP cells, chosen at create): LDS-atomic ranks, block scan,
+// coalesced start[] store, scatter.  One launch instead of count/scan/scatter.
+constexpr int SG_CAP = 4096;
+template <int KIND>
+__global__ void __launch_bounds__(1024) k_grid_small(Dev d, int fix) {
+  __shared__ int cnt[SG_CAP + 1];
+  __shared__ int sh[1024];
+  const int a = blockIdx.x, tid = threadIdx.x, s = d.cshift;
+  const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
+  ArenaCtl &c = d.ctl[a];
+  const int per = KIND == 1 ? d.Ecap : d.Vcap;
+  const int n = KIND == 1 ? c.n_blob : c.n_vir;
+  if (fix && tid == 0) pgrid_finish(d, a, fix);  // (touches only pellet counters and the tick)
+  int *start = (KIND == 1 ? d.bstart : d.vstart) + (size_t)a * (d.H + 1);
+  int *items = (KIND == 1 ? d.bitems : d.vitems) + (size_t)a * per;
+  int *rank = (KIND == 1 ? d.b_rank : d.v_rank) + (size_t)a * per;
+  for (int i = tid; i <= Hc; i += 1024) cnt[i] = 0;
+  __syncthreads();
+  double rloc = 0;
+  for (int i = tid; i < n; i += 1024) {
+    size_t g = (size_t)a * per + i;
+    bool ok = (KIND == 1 ? d.b_flags[g] : d.v_flags[g]) & F_ALIVE;
+    int rk = -1;
+    if (ok) {
+      double x = KIND == 1 ? d.b_x[g] : d.v_x[g], y = KIND == 1 ? d.b_y[g] : d.v_y[g];
+      if (KIND == 2) rloc = fmax(rloc, d.v_r[g]);
+      int b = (center_bucket_coord(y, d.cols) >> s) * cc + (center_bucket_coord(x, d.cols) >> s);
+      rk = (b << 12) | atomicAdd(&cnt[b], 1);  // rank < 4096 per coarse cell (else ERR_SLOT)
+    }
+    rank[i] = rk;
+  }
+  if (KIND == 2) wave_atomic_max_pos(&c.rmax_virus, rloc);
+  __syncthreads();
+  block_scan_excl(cnt, cnt, Hc + 1, sh);  // in place: bucket starts
+  for (int i = tid; i <= Hc; i += 1024) start[i] = cnt[i];
+  for (int i = tid; i < n; i += 1024) {
+    int rk = rank[i];
+    if (rk < 0) continue;
+    int b = rk >> 12, r = rk & 4095;
+    if (r == 4095) set_err(d, a, ERR_SLOT);
+    items[cnt[b] + r] = i;
+  }
+}
+
 // Single-pass multi-block exclusive scan with decoupled look-back.  Grid
 // (tiles, arenas), 256 threads, LB_TILE counts per block.  Each tile publishes
 // one self-contained 64-bit word {status:2 | epoch:30 | value:32} with an
@@ -781,7 +827,7 @@ __global__ void k_vb_active(Dev d) {
     if (any || !(d.b_flags[g] & F_ALIVE)) return;
     if (!rect_hit(footprint(d.b_x[g], d.b_y[g], d.b_r[g], d.size), q)) return;
     if (overlap(vx, vy, vm, vr, d.b_x[g], d.b_y[g], d.b_m[g], d.b_r[g])) any = true;
-  });
+  }, d.cshift);
   if (any) {
     int w = atomicAdd(&d.ctl[a].n_pend, 1);
     if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = i;
@@ -825,7 +871,7 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
         cv[nc] = j;
         nc++;
       }
-    });
+    }, d.cshift);
     isort_kv(ck, cv, nc);
     for (int t = 0; t < nc; t++) {
       size_t g = (size_t)a * d.Ecap + cv[t];
@@ -877,16 +923,17 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
 // ------------------------------------------------------------ T12 cell <- virus
 // wave-wide "does any entity in the grid rows around q satisfy pred"
 template <class Pred>
-__device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items, int cols, Rect q, int E, Pred pred) {
+__device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items, int cols, Rect q, int E, Pred pred,
+                                                 int shift = 0) {
   if (q.x1 < q.x0 || q.y1 < q.y0) return false;
-  int bx0 = max(0, q.x0 - E), bx1 = min(cols - 1, q.x1 + E);
-  int by0 = max(0, q.y0 - E), by1 = min(cols - 1, q.y1 + E);
-  const int lane = threadIdx.x & 63, nrows = by1 - by0 + 1;
+  const Span g = grid_span(q, E, cols, shift);
+  const int bx0 = g.bx0, bx1 = g.bx1, by0 = g.by0;
+  const int lane = threadIdx.x & 63, nrows = g.by1 - by0 + 1;
   for (int r0 = 0; r0 < nrows; r0 += 64) {  // rows flattened as in wave_grid_for
     const int r = r0 + lane, nr = min(64, nrows - r0);
     int lo = 0, len = 0;
     if (r < nrows) {
-      int b = (by0 + r) * cols;
+      int b = (by0 + r) * g.stride;
       lo = st[b + bx0];
       len = st[b + bx1 + 1] - lo;
     }
@@ -929,7 +976,7 @@ __global__ void __launch_bounds__(256) k_pv_active(Dev d) {
       if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return false;
       if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return false;
       return overlap(x, y, m, r, d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) && m > 1.25 * d.v_m[g];
-    });
+    }, d.cshift);
     if (lane == 0) d.c_active[ci] = any;
     anyp |= any;
   }
@@ -976,7 +1023,7 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
           cv[nc] = j;
           nc++;
         }
-      });
+      }, d.cshift);
       isort_kv(ck, cv, nc);
       for (int t = 0; t < nc; t++) {
         size_t g = (size_t)a * d.Vcap + cv[t];
@@ -1066,6 +1113,7 @@ struct Food {
   __device__ uint64_t *owner(int j) const { return (KIND == 0 ? d.pel_owner : d.b_owner) + g(j); }
   __device__ const int *start() const { return (KIND == 0 ? d.pstart : d.bstart) + (size_t)a * (d.H + 1); }
   __device__ const int *items() const { return KIND == 0 ? nullptr : d.bitems + (size_t)a * d.Ecap; }
+  __device__ int shift() const { return KIND == 0 ? 0 : d.cshift; }  // blob grid is coarsened
 };
 // reservation key: higher round wins, within a round the lower priority wins.
 // Rounds are global per arena and only grow (ArenaCtl::food_round), so stale
@@ -1104,6 +1152,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
   const int gp = blockIdx.x * 4 + w;
   if (gp >= d.NP || !d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  if (KIND == 1 && d.ctl[a].n_blob == 0) return;  // no blobs: nothing to reserve (commit skips too)
   Food<KIND> F(d, a);
   const uint32_t base = d.ctl[a].food_round;
   const int cols = d.cols;
@@ -1140,7 +1189,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
         }
       }
       cnt += __popcll(bal);
-    });
+    }, F.shift());
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
     double sum = wave_sum(lsum);
@@ -1169,10 +1218,9 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
         d.f_cnt[ci] = kOverflow;
         d.f_done[ci] = 0;
       }
-      int bx0 = max(0, q.x0 - 1), bx1 = min(cols - 1, q.x1 + 1);
-      int by0 = max(0, q.y0 - 1), by1 = min(cols - 1, q.y1 + 1);
-      for (int by = by0; by <= by1; by++) {
-        int lo = st[by * cols + bx0], hi = st[by * cols + bx1 + 1];
+      const Span g = grid_span(q, 1, cols, F.shift());
+      for (int by = g.by0; by <= g.by1; by++) {
+        int lo = st[by * g.stride + g.bx0], hi = st[by * g.stride + g.bx1 + 1];
         for (int t = lo + lane; t < hi; t += 64) {
           int j = items ? items[t] : t;
           if (F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q))
@@ -1227,6 +1275,7 @@ __global__ void k_food_commit(Dev d, int round, int last) {
   int gp = GTID;
   if (gp >= d.NP || !d.p_alive[gp]) return;
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  if (KIND == 1 && d.ctl[a].n_blob == 0) return;
   Food<KIND> F(d, a);
   int n = d.p_ncells[gp];
   for (int k = 0; k < n; k++) {
@@ -1298,7 +1347,7 @@ __global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
       } else {
         set_err(d, a, ERR_CAND_CAP);
       }
-    });
+    }, F.shift());
     isort_kv(ck, cv, nc);
     food_eat_loop<KIND>(d, F, a, ci, (uint32_t)prios[wi], cv, nc);
     d.f_done[ci] = 1;
@@ -1820,8 +1869,8 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
   launch_pellet_rebuild(d, s, 0, 0, 0);  // P0 U conversions -> P1 (eat-phase buffer)
-  launch_grid<1>(d, s, d.bcnt, d.bstart, 1);
-  if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart);
+  hipLaunchKernelGGL(k_grid_small<1>, dim3(d.A), dim3(1024), 0, s, d, 1);
+  if (d.virus_enabled) hipLaunchKernelGGL(k_grid_small<2>, dim3(d.A), dim3(1024), 0, s, d, 0);
   hipLaunchKernelGGL(k_merge, dim3(gP), dim3(256), 0, s, d);
   if (d.virus_enabled) {
     hipLaunchKernelGGL(k_vb_active, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
@@ -1842,7 +1891,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   launch_pellet_rebuild(d, s, 1, 1, 1);  // P1 survivors U spawns -> P0 (+ FOV cache)
   // the virus list was compacted by k_spawn_plan: re-index the virus grid for the
   // observations (membership stays the F_INHASH flag: spawned viruses are not hashed)
-  if (d.virus_enabled) launch_grid<2>(d, s, d.vcnt, d.vstart, 2);
+  if (d.virus_enabled) hipLaunchKernelGGL(k_grid_small<2>, dim3(d.A), dim3(1024), 0, s, d, 2);
   else hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, 2);
 }
 
