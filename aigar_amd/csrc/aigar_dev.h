@@ -63,6 +63,7 @@ enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4
 
 struct Dev {
   int A, B, NP, size, cols, H;
+  int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)
   int Pcap, Ecap, Vcap, Wcap, EVcap;
   int virus_enabled;

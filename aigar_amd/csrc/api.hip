@@ -222,6 +222,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(o_act_prev, double, NP * 4);
   d.OBcap = (int)std::min<size_t>(std::max<size_t>(1u << 20, 64 * NP), (size_t)1 << 24);
   AL(scan_state, unsigned long long, A * d.scan_tiles);
+  AL(ticket, int, 4);
   AL(ob_used, unsigned long long, 1);
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);

@@ -80,9 +80,7 @@ __device__ __forceinline__ void grid_visit(const int *start, const int *items, i
 __device__ __forceinline__ int expand_for(double rmax) { return (int)ceil((rmax + 1.0) / kBucket) + 1; }
 
 // ------------------------------------------------------------ T1 viruses
-__global__ void k_update_viruses(Dev d) {
-  int gi = GTID;
-  if (gi >= d.A * d.Vcap) return;
+__device__ __forceinline__ void update_virus(const Dev &d, int gi) {
   int a = gi / d.Vcap, i = gi - a * d.Vcap;
   if (i >= d.ctl[a].n_vir || !(d.v_flags[gi] & F_ALIVE)) return;
   int svc = d.v_svc[gi];
@@ -98,9 +96,7 @@ __global__ void k_update_viruses(Dev d) {
 }
 
 // ------------------------------------------------------------ T2 blobs
-__global__ void k_update_blobs(Dev d) {
-  int gi = GTID;
-  if (gi >= d.A * d.Ecap) return;
+__device__ __forceinline__ void update_blob(const Dev &d, int gi) {
   int a = gi / d.Ecap, i = gi - a * d.Ecap;
   if (i >= d.ctl[a].n_blob || !(d.b_flags[gi] & F_ALIVE)) return;
   if (d.b_svc[gi] == 0) {  // stopped blob becomes a pellet (addPellet)
@@ -129,12 +125,14 @@ __global__ void k_update_blobs(Dev d) {
 }
 
 // ------------------------------------------------------------ T4 players
-__global__ void __launch_bounds__(256) k_update_players(Dev d) {
-  int gp = GTID;
-  // clear the player-hash occupancy bitmap for this tick's spawns (k_occupancy refills it)
-  for (size_t w = (size_t)gp; w < (size_t)d.A * d.occ_words; w += (size_t)gridDim.x * blockDim.x) d.occ[w] = 0;
-  if (gp >= d.NP) return;
+__device__ __forceinline__ void update_player(const Dev &d, int gp) {
   const int NP = d.NP;
+  // the cell arrays never alias: let the compiler keep values in registers across stores
+  double *__restrict__ cx = d.c_x, *__restrict__ cy = d.c_y, *__restrict__ cm = d.c_m, *__restrict__ cr = d.c_r;
+  double *__restrict__ cvx = d.c_vx, *__restrict__ cvy = d.c_vy, *__restrict__ csvx = d.c_svx;
+  double *__restrict__ csvy = d.c_svy, *__restrict__ cmt = d.c_mt;
+  int *__restrict__ csvc = d.c_svc;
+  uint32_t *__restrict__ cfl = d.c_flags;
   d.p_newc[gp] = 0;
   d.p_newb[gp] = 0;
   if (!d.p_alive[gp]) {  // updateRespawnTime (player.py:74-75)
@@ -149,36 +147,36 @@ __global__ void __launch_bounds__(256) k_update_players(Dev d) {
   // Player.decayMass -> Cell.decayMass (cell.py:123-126)
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)lst[k] * NP + gp;
-    double m = d.c_m[ci];
+    double m = cm[ci];
     if (m >= 4) {
       m = m * kDecay;
-      d.c_m[ci] = m;
-      d.c_r[ci] = radius_of(m);
+      cm[ci] = m;
+      cr[ci] = radius_of(m);
     }
   }
   // updateCellProperties: momentum, merge timer, direction (player.py:39-44)
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)lst[k] * NP + gp;
-    int svc = d.c_svc[ci];
-    double svx = d.c_svx[ci], svy = d.c_svy[ci];
+    int svc = csvc[ci];
+    double svx = csvx[ci], svy = csvy[ci];
     update_momentum(svc, svx, svy);
-    d.c_svc[ci] = svc;
-    d.c_svx[ci] = svx;
-    d.c_svy[ci] = svy;
-    double mt = d.c_mt[ci];
-    if (mt > 0) d.c_mt[ci] = mt - 1;
+    csvc[ci] = svc;
+    csvx[ci] = svx;
+    csvy[ci] = svy;
+    double mt = cmt[ci];
+    if (mt > 0) cmt[ci] = mt - 1;
     double vx, vy;
-    set_move_direction(d.c_x[ci], d.c_y[ci], d.c_m[ci], d.c_r[ci], cpx, cpy, vx, vy);
-    d.c_vx[ci] = vx;
-    d.c_vy[ci] = vy;
+    set_move_direction(cx[ci], cy[ci], cm[ci], cr[ci], cpx, cpy, vx, vy);
+    cvx[ci] = vx;
+    cvy[ci] = vy;
   }
   int n_new = 0;
   if (d.p_split[gp]) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
     for (int i = 1; i < n; i++) {
       uint8_t key = lst[i];
-      double km = d.c_m[(size_t)key * NP + gp];
+      double km = cm[(size_t)key * NP + gp];
       int j = i - 1;
-      while (j >= 0 && km > d.c_m[(size_t)lst[j] * NP + gp]) {
+      while (j >= 0 && km > cm[(size_t)lst[j] * NP + gp]) {
         lst[j + 1] = lst[j];
         j--;
       }
@@ -191,34 +189,34 @@ __global__ void __launch_bounds__(256) k_update_players(Dev d) {
     for (int k = 0; k < n0; k++) snap[k] = lst[k];
     for (int k = 0; k < n0; k++) {
       size_t ci = (size_t)snap[k] * NP + gp;
-      if (!(d.c_m[ci] > 36 && n < kMaxCells)) continue;
+      if (!(cm[ci] > 36 && n < kMaxCells)) continue;
       int slot = __ffs(~used) - 1;
       used |= 1u << slot;
       size_t ni = (size_t)slot * NP + gp;
       // Cell.split (cell.py:72-85)
-      double x = d.c_x[ci], y = d.c_y[ci];
-      double nm = d.c_m[ci] / 2, nr = radius_of(nm);
+      double x = cx[ci], y = cy[ci];
+      double nm = cm[ci] / 2, nr = radius_of(nm);
       double ang = atan2(cpy - y, cpx - x);
       double ca = cos(ang);
       double sa = sin(ang);
       double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
       double svx, svy;
       int svc;
-      add_momentum(x, y, xp, yp, W, W, d.c_r[ci], svx, svy, svc);
-      d.c_x[ni] = x;
-      d.c_y[ni] = y;
-      d.c_m[ni] = nm;
-      d.c_r[ni] = nr;
-      d.c_vx[ni] = 0;
-      d.c_vy[ni] = 0;
-      d.c_svx[ni] = svx;
-      d.c_svy[ni] = svy;
-      d.c_svc[ni] = svc;
-      d.c_mt[ni] = merge_time_for(1, nm);
-      d.c_flags[ni] = F_ALIVE | F_NEW;
-      double pm = d.c_m[ci] / 2;
-      d.c_m[ci] = pm;
-      d.c_r[ci] = radius_of(pm);
+      add_momentum(x, y, xp, yp, W, W, cr[ci], svx, svy, svc);
+      cx[ni] = x;
+      cy[ni] = y;
+      cm[ni] = nm;
+      cr[ni] = nr;
+      cvx[ni] = 0;
+      cvy[ni] = 0;
+      csvx[ni] = svx;
+      csvy[ni] = svy;
+      csvc[ni] = svc;
+      cmt[ni] = merge_time_for(1, nm);
+      cfl[ni] = F_ALIVE | F_NEW;
+      double pm = cm[ci] / 2;
+      cm[ci] = pm;
+      cr[ci] = radius_of(pm);
       lst[n++] = (uint8_t)slot;
       n_new++;
     }
@@ -226,26 +224,26 @@ __global__ void __launch_bounds__(256) k_update_players(Dev d) {
   if (d.p_eject[gp])  // Player.eject (player.py:54-58)
     for (int k = 0; k < n; k++) {
       size_t ci = (size_t)lst[k] * NP + gp;
-      if (d.c_m[ci] >= 35) d.c_flags[ci] |= F_EJECT;
+      if (cm[ci] >= 35) cfl[ci] |= F_EJECT;
     }
   for (int k = 0; k < n; k++) {  // updateCellsMovement
     size_t ci = (size_t)lst[k] * NP + gp;
-    double x = d.c_x[ci], y = d.c_y[ci], svx = d.c_svx[ci], svy = d.c_svy[ci];
-    update_pos(x, y, d.c_vx[ci], d.c_vy[ci], svx, svy, d.c_svc[ci], W, W);
-    d.c_x[ci] = x;
-    d.c_y[ci] = y;
-    d.c_svx[ci] = svx;
-    d.c_svy[ci] = svy;
+    double x = cx[ci], y = cy[ci], svx = csvx[ci], svy = csvy[ci];
+    update_pos(x, y, cvx[ci], cvy[ci], svx, svy, csvc[ci], W, W);
+    cx[ci] = x;
+    cy[ci] = y;
+    csvx[ci] = svx;
+    csvy[ci] = svy;
   }
   int nb = 0;
   for (int k = 0; k < n; k++) {  // performEjections (field.py:134-146)
     size_t ci = (size_t)lst[k] * NP + gp;
-    if (!(d.c_flags[ci] & F_EJECT)) continue;
-    d.c_m[ci] = d.c_m[ci] - kEjectMass;  // Cell.eject: radius stays stale (cell.py:90-94)
-    d.c_flags[ci] &= ~F_EJECT;
-    double bx = d.c_x[ci], by = d.c_y[ci], svx, svy;
+    if (!(cfl[ci] & F_EJECT)) continue;
+    cm[ci] = cm[ci] - kEjectMass;  // Cell.eject: radius stays stale (cell.py:90-94)
+    cfl[ci] &= ~F_EJECT;
+    double bx = cx[ci], by = cy[ci], svx, svy;
     int svc;
-    add_momentum(bx, by, cpx, cpy, W, W, d.c_r[ci], svx, svy, svc);
+    add_momentum(bx, by, cpx, cpy, W, W, cr[ci], svx, svy, svc);
     size_t si = (size_t)nb * NP + gp;
     d.sb_x[si] = bx;
     d.sb_y[si] = by;
@@ -256,25 +254,25 @@ __global__ void __launch_bounds__(256) k_update_players(Dev d) {
   }
   for (int i = 0; i < n; i++) {  // handlePlayerCollisions (field.py:149-159)
     size_t ci = (size_t)lst[i] * NP + gp;
-    if (d.c_svc[ci] > 0) continue;
+    if (csvc[ci] > 0) continue;
     for (int j = 0; j < n; j++) {
       size_t cj = (size_t)lst[j] * NP + gp;
-      if (i == j || d.c_svc[cj] > 0 || (d.c_mt[ci] <= 0 && d.c_mt[cj] <= 0)) continue;
-      double x1 = d.c_x[ci], y1 = d.c_y[ci], x2 = d.c_x[cj], y2 = d.c_y[cj];
+      if (i == j || csvc[cj] > 0 || (cmt[ci] <= 0 && cmt[cj] <= 0)) continue;
+      double x1 = cx[ci], y1 = cy[ci], x2 = cx[cj], y2 = cy[cj];
       double dist = sqrt((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2));
-      double sr = d.c_r[ci] + d.c_r[cj];
+      double sr = cr[ci] + cr[cj];
       if (dist < sr && dist != 0) {  // adjustCellPositions (field.py:161-181)
-        bool one_big = d.c_m[ci] > d.c_m[cj];
+        bool one_big = cm[ci] > cm[cj];
         size_t bi = one_big ? ci : cj, si = one_big ? cj : ci;
-        double bx = d.c_x[bi], by = d.c_y[bi], sx = d.c_x[si], sy = d.c_y[si];
-        double ds = (sr - dist) / dist, mds = d.c_m[si] / d.c_m[bi];
+        double bx = cx[bi], by = cy[bi], sx = cx[si], sy = cy[si];
+        double ds = (sr - dist) / dist, mds = cm[si] / cm[bi];
         double xd = (bx - sx) * ds, yd = (by - sy) * ds;
         double nbx = bx + xd * mds, nby = by + yd * mds;
         double nsx = sx - xd * (1 - mds), nsy = sy - yd * (1 - mds);
-        d.c_x[bi] = py_min(W, py_max(0.0, nbx));
-        d.c_y[bi] = py_min(W, py_max(0.0, nby));
-        d.c_x[si] = py_min(W, py_max(0.0, nsx));
-        d.c_y[si] = py_min(W, py_max(0.0, nsy));
+        cx[bi] = py_min(W, py_max(0.0, nbx));
+        cy[bi] = py_min(W, py_max(0.0, nby));
+        cx[si] = py_min(W, py_max(0.0, nsx));
+        cy[si] = py_min(W, py_max(0.0, nsy));
       }
     }
   }
@@ -284,22 +282,76 @@ __global__ void __launch_bounds__(256) k_update_players(Dev d) {
   d.p_newb[gp] = nb;
 }
 
-// block-wide exclusive scan of a[0..n) into out (1024 threads); returns total
+// updateViruses + updateBlobs + updatePlayers in one launch: thread ranges
+// [players | viruses | blobs] (independent entity sets, field.py:94-119)
+__global__ void __launch_bounds__(256) k_tick_begin(Dev d) {
+  int gi = GTID;
+  // clear the player-hash occupancy bitmap for this tick's spawns (k_occupancy refills it)
+  for (size_t w = (size_t)gi; w < (size_t)d.A * d.occ_words; w += (size_t)gridDim.x * blockDim.x) d.occ[w] = 0;
+  if (gi < d.NP) {
+    update_player(d, gi);
+    return;
+  }
+  gi -= d.NP;
+  if (d.virus_enabled) {
+    if (gi < d.A * d.Vcap) {
+      update_virus(d, gi);
+      return;
+    }
+    gi -= d.A * d.Vcap;
+  }
+  if (gi < d.A * d.Ecap) update_blob(d, gi);
+}
+
+// rank of this thread among the flagged threads of the block (thread order);
+// *total = number flagged.  Ballot per wave + one pass over <= 16 wave counts.
+__device__ int block_rank(bool flag, int *sh, int *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned long long b = __ballot(flag);
+  int before = __popcll(b & ((1ull << lane) - 1));
+  if (lane == 0) sh[w] = __popcll(b);
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < nw; k++) {
+    int v = sh[k];
+    off += k < w ? v : 0;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + before;
+}
+
+// block-wide exclusive scan of in[0..n) into out (may alias; any multiple of 64
+// threads up to 1024; sh >= 17 ints); each thread scans a consecutive chunk,
+// per-thread sums go through a shuffle scan per wave and one across waves.
+// Returns the total.
 __device__ int block_scan_excl(const int *in, int *out, int n, int *sh) {
-  const int T = blockDim.x, tid = threadIdx.x;
+  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = T >> 6;
   int per = (n + T - 1) / T, lo = min(n, tid * per), hi = min(n, lo + per);
   int s = 0;
   for (int i = lo; i < hi; i++) s += in[i];
-  sh[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < T; off <<= 1) {  // Hillis-Steele over per-thread sums
-    int v = (tid >= off) ? sh[tid - off] : 0;
-    __syncthreads();
-    sh[tid] += v;
-    __syncthreads();
+  int inc = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
   }
-  int run = sh[tid] - s;
-  int total = sh[T - 1];
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    int v = lane < nw ? sh[lane] : 0, vi = v;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      int y = __shfl_up(vi, off);
+      if (lane >= off) vi += y;
+    }
+    if (lane < nw) sh[lane] = vi - v;
+    if (lane == nw - 1) sh[16] = vi;
+  }
+  __syncthreads();
+  int run = sh[w] + inc - s;
+  const int total = sh[16];
   for (int i = lo; i < hi; i++) {
     int v = in[i];
     out[i] = run;
@@ -494,15 +546,13 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
 // coalesced start[] store, scatter.  One launch instead of count/scan/scatter.
 constexpr int SG_CAP = 4096;
 template <int KIND>
-__global__ void __launch_bounds__(1024) k_grid_small(Dev d, int fix) {
-  __shared__ int cnt[SG_CAP + 1];
-  __shared__ int sh[1024];
-  const int a = blockIdx.x, tid = threadIdx.x, s = d.cshift;
+__device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
+  const int tid = threadIdx.x, s = d.cshift;
   const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
   ArenaCtl &c = d.ctl[a];
   const int per = KIND == 1 ? d.Ecap : d.Vcap;
   const int n = KIND == 1 ? c.n_blob : c.n_vir;
-  if (fix && tid == 0) pgrid_finish(d, a, fix);  // (touches only pellet counters and the tick)
+  __syncthreads();
   int *start = (KIND == 1 ? d.bstart : d.vstart) + (size_t)a * (d.H + 1);
   int *items = (KIND == 1 ? d.bitems : d.vitems) + (size_t)a * per;
   int *rank = (KIND == 1 ? d.b_rank : d.v_rank) + (size_t)a * per;
@@ -532,6 +582,14 @@ __global__ void __launch_bounds__(1024) k_grid_small(Dev d, int fix) {
     if (r == 4095) set_err(d, a, ERR_SLOT);
     items[cnt[b] + r] = i;
   }
+  __syncthreads();
+}
+// blocks [0, A): blob grids; [A, 2A): virus grids (when enabled)
+__global__ void __launch_bounds__(1024) k_grid_small(Dev d) {
+  __shared__ int cnt[SG_CAP + 1];
+  __shared__ int sh[32];
+  if ((int)blockIdx.x < d.A) grid_small_build<1>(d, blockIdx.x, cnt, sh);
+  else grid_small_build<2>(d, blockIdx.x - d.A, cnt, sh);
 }
 
 // Single-pass multi-block exclusive scan with decoupled look-back.  Grid
@@ -659,32 +717,37 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
 // records (blob conversions, spawns) take atomic ranks in pncnt and fill their
 // bucket from the end.  Order inside a bucket carries no meaning: every
 // consumer ranks candidates by creation sequence.
-__global__ void k_pgrid_count(Dev d, int src, int use_dead, int fov) {
-  const int gi = GTID;
-  if (fov && gi < d.NP) store_player_fov(d, gi);  // player state is final here (end of tick / reset)
-  const int per = d.H + d.Pcap;
-  if (gi >= d.A * per) return;
-  const int a = gi / per, i = gi - a * per;
+// survivors of source bucket i: ranks and count (no atomics)
+__device__ __forceinline__ void pgrid_count_bucket(const Dev &d, int a, int i, int use_dead) {
   const ArenaCtl &c = d.ctl[a];
   const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
-  if (i < d.H) {  // bucket i of the source layout
-    const int lo = min(d.pstart[H1 + i], c.n_pel), hi = min(d.pstart[H1 + i + 1], c.n_pel);  // (empty source at reset)
-    int k = 0;
-    for (int t = lo; t < hi; t++) {
-      if (use_dead && d.pel_dead[(size_t)a * d.Pcap + t]) continue;
-      d.pel_rank[R0 + t] = k++;
-    }
-    d.pcnt[H1 + i] = k;
-    return;
+  const int lo = min(d.pstart[H1 + i], c.n_pel), hi = min(d.pstart[H1 + i + 1], c.n_pel);  // (empty source at reset)
+  int k = 0;
+  for (int t = lo; t < hi; t++) {
+    if (use_dead && d.pel_dead[(size_t)a * d.Pcap + t]) continue;
+    d.pel_rank[R0 + t] = k++;
   }
-  const int j = i - d.H;  // staged record j
-  if (j >= c.n_pnew) return;
-  const size_t g = (size_t)a * d.Pcap + j;
+  d.pcnt[H1 + i] = k;
+}
+// staged record j (index into the staging list): atomic rank in its bucket
+__device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
+  const size_t g = (size_t)a * d.Pcap + j, H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
   const int b = center_bucket_coord(d.pn_y[g], d.cols) * d.cols + center_bucket_coord(d.pn_x[g], d.cols);
   d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + b], 1);
 }
-__global__ void k_pgrid_scatter(Dev d, int src, int use_dead) {
+__global__ void k_pgrid_count(Dev d, int src, int use_dead) {
   const int gi = GTID;
+  const int per = d.H + d.Pcap;
+  if (gi >= d.A * per) return;
+  const int a = gi / per, i = gi - a * per;
+  if (i < d.H) {  // bucket i of the source layout
+    pgrid_count_bucket(d, a, i, use_dead);
+    return;
+  }
+  const int j = i - d.H;
+  if (j < d.ctl[a].n_pnew) pgrid_rank_staged(d, a, j);
+}
+__device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src, int use_dead, int extra) {
   const int per = 2 * d.Pcap;
   if (gi >= d.A * per) return;
   const int a = gi / per, i = gi - a * per;
@@ -705,7 +768,7 @@ __global__ void k_pgrid_scatter(Dev d, int src, int use_dead) {
     pos = d.pstart[H1 + b] + d.pel_rank[R0 + i];
   } else {
     int j = i - d.Pcap;
-    if (j >= c.n_pnew) return;
+    if (j >= c.n_pnew + (extra ? c.n_spawn_p : 0)) return;  // (this tick's spawns are staged, not committed)
     size_t g = (size_t)a * d.Pcap + j;
     x = d.pn_x[g];
     y = d.pn_y[g];
@@ -726,6 +789,20 @@ __global__ void k_pgrid_scatter(Dev d, int src, int use_dead) {
   d.pel_seq[dst][o] = s;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
+// fov: refresh the FOV cache (player state is final); fix: the last block runs
+// the rebuild epilogue for every arena (1; 2 also closes the tick) -- every
+// block has read the staging counters before it takes its ticket
+__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int src, int use_dead, int extra, int fov, int fix) {
+  const int gi = GTID;
+  if (fov && gi < d.NP) store_player_fov(d, gi);
+  pgrid_scatter_one(d, gi, src, use_dead, extra);
+  if (!fix) return;
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(&d.ticket[0], 1) == (int)gridDim.x - 1) {
+    d.ticket[0] = 0;
+    for (int a = 0; a < d.A; a++) pgrid_finish(d, a, fix);
+  }
+}
 // pellet-rebuild epilogue (also folded into the next grid-count kernel: fix 1;
 // fix 2 additionally closes the tick)
 __device__ void pgrid_finish(const Dev &d, int a, int fix) {
@@ -742,8 +819,7 @@ __global__ void k_pgrid_finish(Dev d, int fix) {
 }
 
 // ------------------------------------------------------------ T10 merge
-__global__ void k_merge(Dev d) {
-  int gp = GTID;
+__device__ __forceinline__ void merge_player(const Dev &d, int gp) {
   if (gp >= d.NP || !d.p_alive[gp]) return;
   const int NP = d.NP, a = gp / d.B;
   int n = d.p_ncells[gp];
@@ -811,8 +887,7 @@ __device__ void isort_kv(int64_t *key, int *val, int n) {
 }
 
 // ------------------------------------------------------------ T11 virus <- blob
-__global__ void k_vb_active(Dev d) {
-  int gi = GTID;
+__device__ __forceinline__ void vb_active(const Dev &d, int gi) {
   if (gi >= d.A * d.Vcap) return;
   int a = gi / d.Vcap, i = gi - a * d.Vcap;
   if (i == 0) d.ctl[a].n_vir_start = d.ctl[a].n_vir;
@@ -918,6 +993,14 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
       }
     }
   }
+}
+
+// mergePlayerCells (per player) and the virus<-blob activity test (per virus)
+// in one launch: merging touches only player cells, the test only viruses/blobs
+__global__ void __launch_bounds__(256) k_merge_vb(Dev d) {
+  int gi = GTID;
+  if (gi < d.NP) return merge_player(d, gi);
+  if (d.virus_enabled) vb_active(d, gi - d.NP);
 }
 
 // ------------------------------------------------------------ T12 cell <- virus
@@ -1600,6 +1683,7 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
 
 __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
   __shared__ int sflag[1024];
+  __shared__ int gcnt[SG_CAP + 1];
   int a = blockIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
@@ -1625,18 +1709,8 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
           f6 = d.b_svx[g]; f7 = d.b_svy[g]; svc = d.b_svc[g]; s = d.b_seq[g]; e = d.b_ej[g]; fl = d.b_flags[g];
         }
       }
-      sflag[tid] = alive;
-      __syncthreads();
-      // Hillis-Steele inclusive prefix of the alive flags
-      for (int off = 1; off < T; off <<= 1) {
-        int v = (tid >= off) ? sflag[tid - off] : 0;
-        __syncthreads();
-        sflag[tid] += v;
-        __syncthreads();
-      }
-      int pos = out + sflag[tid] - (alive ? 1 : 0);
-      int chunk = sflag[T - 1];
-      __syncthreads();
+      int chunk;
+      const int pos = out + block_rank(alive, sflag, &chunk);  // (all loads of this chunk are done)
       if (alive) {
         size_t o = (size_t)a * cap + pos;
         if (kind == 0) {
@@ -1663,6 +1737,9 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
     }
     __syncthreads();
   }
+  // the virus list is compacted: re-index the virus grid for the observations
+  // (membership stays the F_INHASH flag; the viruses spawned below are not hashed)
+  if (d.virus_enabled) grid_small_build<2>(d, a, gcnt, sflag);
   if (tid != 0) return;
   // spawnPellets: while len(pellets) < maxCollectibleCount
   int alive_p = c.n_pel - c.n_pel_eaten + c.n_pnew;
@@ -1714,8 +1791,7 @@ __global__ void k_pnew_commit(Dev d) {
   d.ctl[a].n_pnew += d.ctl[a].n_spawn_p;
 }
 
-__global__ void k_spawn_pellets(Dev d) {
-  int gi = GTID;
+__device__ __forceinline__ void spawn_pellet(const Dev &d, int gi, bool rank_staged) {
   if (gi >= d.A * d.Pcap) return;
   int a = gi / d.Pcap, j = gi - a * d.Pcap;
   ArenaCtl &c = d.ctl[a];
@@ -1730,9 +1806,10 @@ __global__ void k_spawn_pellets(Dev d) {
   d.pn_y[o] = (double)y;
   d.pn_m[o] = m;
   d.pn_seq[o] = c.seq_base_spawn + j;
+  if (rank_staged) pgrid_rank_staged(d, a, c.n_pnew + j);  // rebuild ranks taken at spawn time
 }
-__global__ void k_spawn_viruses(Dev d) {
-  int gi = GTID;
+__global__ void k_spawn_pellets(Dev d) { spawn_pellet(d, GTID, false); }
+__device__ __forceinline__ void spawn_virus(const Dev &d, int gi) {
   if (gi >= d.A * d.Vcap) return;
   int a = gi / d.Vcap, j = gi - a * d.Vcap;
   ArenaCtl &c = d.ctl[a];
@@ -1759,14 +1836,12 @@ __global__ void k_spawn_viruses(Dev d) {
   d.v_seq[o] = c.seq_base_spawn + c.n_spawn_p + j;
   d.v_flags[o] = F_ALIVE;  // addVirus: not hashed until the next rebuild
 }
-__global__ void k_spawn_players(Dev d, int init) {
-  int gi = GTID;
+__global__ void k_spawn_viruses(Dev d) { spawn_virus(d, GTID); }
+__device__ __forceinline__ void spawn_player(const Dev &d, int gi, int init) {
   if (gi >= d.NP) return;
   int a = gi / d.B, j = gi - a * d.B;
   ArenaCtl &c = d.ctl[a];
-  const int nsp = c.n_spawn_pl;
-  if (!init && j == 0) c.n_pnew += c.n_spawn_p;  // this tick's pellet spawns join the staging list
-  if (j >= nsp) return;
+  if (j >= c.n_spawn_pl) return;
   int p = d.respawn_list[(size_t)a * d.B + j];
   int gp = a * d.B + p;
   const int NP = d.NP;
@@ -1797,6 +1872,24 @@ __global__ void k_spawn_players(Dev d, int init) {
   d.p_alive[gp] = 1;
   d.p_respawn[gp] = 0;
   if (!init) ev_push(d, a, PH_SPAWN, (uint64_t)j, 10, p, seq);
+}
+__global__ void k_spawn_players(Dev d, int init) { spawn_player(d, GTID, init); }
+
+// spawnStuff (field.py:256-313) in one launch, thread ranges [players | pellets
+// | viruses | pellet buckets]: the three spawn lists are independent (their
+// counts and sequence bases come from k_spawn_plan), and the survivor counts of
+// the closing pellet rebuild only read the eat-phase buffer.
+__global__ void __launch_bounds__(256) k_spawn_all(Dev d) {
+  int gi = GTID;
+  if (gi < d.NP) return spawn_player(d, gi, 0);
+  gi -= d.NP;
+  if (gi < d.A * d.Pcap) return spawn_pellet(d, gi, true);
+  gi -= d.A * d.Pcap;
+  if (d.virus_enabled) {
+    if (gi < d.A * d.Vcap) return spawn_virus(d, gi);
+    gi -= d.A * d.Vcap;
+  }
+  if (gi < d.A * d.H) pgrid_count_bucket(d, gi / d.H, gi % d.H, 1);
 }
 
 
@@ -1833,12 +1926,13 @@ struct Scratch {
   int *v;
 };
 
-void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead, int fov) {
-  long nc = std::max((long)d.A * (d.H + d.Pcap), (long)d.NP), ns = (long)d.A * 2 * d.Pcap;
-  hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, src, use_dead, fov);
+// counts (unless already taken by k_spawn_all) -> scan -> scatter (+ epilogue)
+void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead, int fov, int fix, bool counted) {
+  long nc = (long)d.A * (d.H + d.Pcap), ns = std::max((long)d.A * 2 * d.Pcap, (long)d.NP);
+  if (!counted) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, src, use_dead);
   hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt);
-  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, src, use_dead);
-  // epilogue (pgrid_finish) is run by the caller's next kernel
+  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, src, use_dead, counted ? 1 : 0, fov,
+                     fix);
 }
 
 template <int KIND>
@@ -1863,17 +1957,15 @@ static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v) {
   Scratch scr{scr_k, scr_v};
   const int gP = nblk(d.NP, 256);
-  if (d.virus_enabled) hipLaunchKernelGGL(k_update_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_update_blobs, dim3(nblk((long)d.A * d.Ecap, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_update_players, dim3(gP), dim3(256), 0, s, d);
+  const long n_begin = (long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
+  hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
-  launch_pellet_rebuild(d, s, 0, 0, 0);  // P0 U conversions -> P1 (eat-phase buffer)
-  hipLaunchKernelGGL(k_grid_small<1>, dim3(d.A), dim3(1024), 0, s, d, 1);
-  if (d.virus_enabled) hipLaunchKernelGGL(k_grid_small<2>, dim3(d.A), dim3(1024), 0, s, d, 0);
-  hipLaunchKernelGGL(k_merge, dim3(gP), dim3(256), 0, s, d);
+  launch_pellet_rebuild(d, s, 0, 0, 0, 1, false);  // P0 U conversions -> P1 (eat-phase buffer)
+  hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
+  hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
+                     dim3(256), 0, s, d);
   if (d.virus_enabled) {
-    hipLaunchKernelGGL(k_vb_active, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_vb_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
     hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
@@ -1884,15 +1976,12 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
   hipLaunchKernelGGL(k_occupancy, dim3(nblk((long)d.A * kMaxCells * d.B, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);
-  hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
-  if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_spawn_players, dim3(gP), dim3(256), 0, s, d, 0);  // + n_pnew commit
-  launch_pellet_rebuild(d, s, 1, 1, 1);  // P1 survivors U spawns -> P0 (+ FOV cache)
-  // the virus list was compacted by k_spawn_plan: re-index the virus grid for the
-  // observations (membership stays the F_INHASH flag: spawned viruses are not hashed)
-  if (d.virus_enabled) hipLaunchKernelGGL(k_grid_small<2>, dim3(d.A), dim3(1024), 0, s, d, 2);
-  else hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, 2);
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);  // + end-of-tick virus grid
+  const long n_spawn = (long)d.NP + (long)d.A * d.Pcap + (d.virus_enabled ? (long)d.A * d.Vcap : 0) +
+                       (long)d.A * d.H;
+  hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d);
+  // P1 survivors U spawns -> P0, FOV cache, epilogue closes the tick
+  launch_pellet_rebuild(d, s, 1, 1, 1, 2, true);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty
@@ -1913,8 +2002,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
-  launch_pellet_rebuild(d, s, 1, 0, 1);  // staging -> P0 (+ FOV cache)
-  hipLaunchKernelGGL(k_pgrid_finish, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, 0);
+  launch_pellet_rebuild(d, s, 1, 0, 1, 1, false);  // staging -> P0 (+ FOV cache)
 }
 
 }  // namespace aigar
