@@ -44,8 +44,9 @@ struct ArenaCtl {
   double rmax_cell, rmax_virus;
   uint64_t ev_order;     // serial-phase event counter
   uint32_t food_round;   // reservation epoch (grows every eat phase)
-  uint32_t scan_epoch;   // decoupled look-back epoch (grows every scan launch)
-  int scan_ticket;
+  uint32_t scan_epoch[2];  // decoupled look-back epoch per scan slot (grows every launch)
+  int scan_ticket[2];      // slot 0: pellet rebuilds, slot 1: cell grid (may run concurrently)
+  int src_n_pel, src_n_stage;  // pellet rebuild: source counts snapshotted by the scan epilogue
   int pad1;
   // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
   // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
@@ -64,6 +65,7 @@ enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4
 struct Dev {
   int A, B, NP, size, cols, H;
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
+  double pow_n032[17];  // pow_cr(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)
   int Pcap, Ecap, Vcap, Wcap, EVcap;
   int virus_enabled;
@@ -132,7 +134,7 @@ struct Dev {
   double *o_self_lf, *o_self_slf, *o_en_lf, *o_en_slf;  // [NP][G*G]
   double *o_act_cur, *o_act_prev;                // [NP][4]
   // decoupled look-back tile states [A][scan_tiles]
-  unsigned long long *scan_state;
+  unsigned long long *scan_state;  // [2 slots][A][scan_tiles]
   int scan_tiles;
   // observation overflow pool (bots that see more objects than their LDS lists hold)
   int OBcap;

@@ -19,6 +19,7 @@
 #include <cmath>
 #define AIGAR_HD static inline
 #endif
+#include "aigar_pow_tables.h"
 
 namespace aigar_math {
 
@@ -116,14 +117,123 @@ AIGAR_HD dd exp_dd(dd p) {
   return acc;
 }
 
+// ---------------------------------------------------------------- fast path
+// Table-driven x^y with ~2^-70 relative error as a double-double, plus Ziv's
+// rounding test: when the error interval rounds to one double, that double is
+// the correctly rounded result; otherwise (about 1 call in 2^16) the slow
+// series above decides.  log: x = 2^E m, m in [1,2), t = m r_i - 1 exact
+// (r_i has 8 significant bits, |t| < 2^-7), log1p(t) = t - t^2/2 + t^3 P(t).
+// exp: p = (128 kk + j) ln2/128 + r, |r| < 2^-8, 2^(j/128) from a table.
+struct PowLogEnt {
+  double r, lh, ll;
+};
+struct PowExpEnt {
+  double h, l;
+};
+#ifdef __HIPCC__
+static __constant__ PowLogEnt kPowLogDev[128] = AIGAR_POW_LOG_TABLE;
+static __constant__ PowExpEnt kPowExpDev[128] = AIGAR_POW_EXP_TABLE;
+#endif
+static const PowLogEnt kPowLogHost[128] = AIGAR_POW_LOG_TABLE;
+static const PowExpEnt kPowExpHost[128] = AIGAR_POW_EXP_TABLE;
+AIGAR_HD PowLogEnt pow_log_ent(int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return kPowLogDev[i];
+#else
+  return kPowLogHost[i];
+#endif
+}
+AIGAR_HD PowExpEnt pow_exp_ent(int j) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return kPowExpDev[j];
+#else
+  return kPowExpHost[j];
+#endif
+}
+AIGAR_HD dd dd_add_d(dd a, double b) {
+  dd s = two_sum(a.hi, b);
+  s.lo += a.lo;
+  return fast_two_sum(s.hi, s.lo);
+}
+// relative error bound of the fast double-double result (measured max 2^-75.7 over
+// 3M samples of the path's domain, tools/gen/check_pow.cpp; 2^5.7 margin)
+#define AIGAR_POW_FAST_ERR 0x1p-70
+AIGAR_HD bool pow_fast(double x, double y, double &res, dd *raw = nullptr) {
+  uint64_t bits;
+  __builtin_memcpy(&bits, &x, 8);
+  int E = (int)((bits >> 52) & 0x7ff);
+  if (E == 0 || E == 0x7ff || (bits >> 63)) return false;  // zero/subnormal/inf/nan/negative
+  E -= 1023;
+  const int i = (int)((bits >> 45) & 127);
+  const uint64_t mb = (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+  double m;
+  __builtin_memcpy(&m, &mb, 8);
+  const PowLogEnt L = pow_log_ent(i);
+  const double t = fma(m, L.r, -1.0);  // exact
+  const dd t2 = two_prod(t, t);
+  double P = -0x1.999999999999ap-4;  // -1/10
+  P = fma(P, t, 0x1.c71c71c71c71cp-4);   // 1/9
+  P = fma(P, t, -0x1.0000000000000p-3);  // -1/8
+  P = fma(P, t, 0x1.2492492492492p-3);   // 1/7
+  P = fma(P, t, -0x1.5555555555555p-3);  // -1/6
+  P = fma(P, t, 0x1.999999999999ap-3);   // 1/5
+  P = fma(P, t, -0x1.0000000000000p-2);  // -1/4
+  P = fma(P, t, 0x1.5555555555555p-2);   // 1/3
+  const double ln2[3] = AIGAR_POW_LN2;
+  const double Ed = (double)E;
+  // small terms first (all << 2^-20 in magnitude)
+  const double small = Ed * ln2[1] + Ed * ln2[2] + L.ll - 0.5 * t2.lo + t * t2.hi * P;
+  dd lg = two_sum(Ed * ln2[0], L.lh);  // E ln2_hi is exact
+  lg = dd_add_d(lg, t);
+  lg = dd_add_d(lg, -0.5 * t2.hi);
+  lg = dd_add_d(lg, small);
+  // p = y log x
+  dd p = two_prod(y, lg.hi);
+  p.lo += y * lg.lo;
+  p = fast_two_sum(p.hi, p.lo);
+  if (!(p.hi > -700.0 && p.hi < 700.0)) return false;
+  const double l128[3] = AIGAR_POW_LN2_128;
+  const double kd = rint(p.hi * AIGAR_POW_INV_LN2_128);
+  const int k = (int)kd;
+  dd r = two_sum(p.hi, -kd * l128[0]);  // kd * ln2/128_hi is exact
+  double rl = r.lo + p.lo - kd * l128[1] - kd * l128[2];
+  r = two_sum(r.hi, rl);
+  const double rh = r.hi;
+  rl = r.lo;
+  const dd r2 = two_prod(rh, rh);
+  double Q = 0x1.a01a01a01a01ap-16;  // 1/40320
+  Q = fma(Q, rh, 0x1.a01a01a01a01ap-13);  // 1/5040
+  Q = fma(Q, rh, 0x1.6c16c16c16c17p-10);  // 1/720
+  Q = fma(Q, rh, 0x1.1111111111111p-7);   // 1/120
+  Q = fma(Q, rh, 0x1.5555555555555p-5);   // 1/24
+  Q = fma(Q, rh, 0x1.5555555555555p-3);   // 1/6
+  const double tail = rl + 0.5 * r2.lo + rh * rl + rh * r2.hi * Q;
+  dd e = fast_two_sum(1.0, rh);
+  e = dd_add_d(e, 0.5 * r2.hi);
+  e = dd_add_d(e, tail);
+  const PowExpEnt T = pow_exp_ent(k & 127);
+  e = dd_mul(e, dd{T.h, T.l});
+  if (raw) *raw = dd{ldexp(e.hi, k >> 7), ldexp(e.lo, k >> 7)};  // (diagnostics: tools/gen/check_pow.cpp)
+  const double err = fabs(e.hi) * AIGAR_POW_FAST_ERR;
+  const double u1 = e.hi + (e.lo - err), u2 = e.hi + (e.lo + err);
+  if (u1 != u2) return false;
+  res = ldexp(u1, k >> 7);  // (arithmetic shift: k = 128 (k >> 7) + (k & 127))
+  return true;
+}
+
 // correctly rounded x^y (x > 0)
-AIGAR_HD double pow_cr(double x, double y) {
-  if (y == 0.0 || x == 1.0) return 1.0;
-  if (x == 0.0) return y > 0 ? 0.0 : __builtin_inf();
+AIGAR_HD double pow_cr_slow(double x, double y) {
   dd l = log_dd(x);
   dd p = dd_add(two_prod(l.hi, y), dd{l.lo * y, 0.0});
   dd e = exp_dd(p);
   return e.hi + e.lo;
+}
+AIGAR_HD double pow_cr(double x, double y) {
+  if (y == 0.0 || x == 1.0) return 1.0;
+  if (x == 0.0) return y > 0 ? 0.0 : __builtin_inf();
+  double r;
+  if (pow_fast(x, y, r)) return r;
+  return pow_cr_slow(x, y);
 }
 
 }  // namespace aigar_math

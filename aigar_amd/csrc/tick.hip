@@ -125,6 +125,38 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
 }
 
 // ------------------------------------------------------------ T4 players
+// Player.decayMass + updateCellProperties for one cell (player.py:39-44,
+// cell.py:105-130,47-57): independent per cell, so one thread per pool slot --
+// the correctly rounded pow of the move speed no longer chains per player
+__device__ __forceinline__ void update_cell(const Dev &d, int gi) {
+  const int NP = d.NP;
+  if (gi >= kMaxCells * NP) return;
+  const int gp = gi % NP;
+  const size_t ci = (size_t)gi;
+  if (!(d.c_flags[ci] & F_ALIVE) || !d.p_alive[gp]) return;
+  double m = d.c_m[ci], r = d.c_r[ci];
+  if (m >= 4) {  // Cell.decayMass (cell.py:123-126)
+    m = m * kDecay;
+    r = radius_of(m);
+    d.c_m[ci] = m;
+    d.c_r[ci] = r;
+  }
+  int svc = d.c_svc[ci];
+  double svx = d.c_svx[ci], svy = d.c_svy[ci];
+  update_momentum(svc, svx, svy);
+  d.c_svc[ci] = svc;
+  d.c_svx[ci] = svx;
+  d.c_svy[ci] = svy;
+  double mt = d.c_mt[ci];
+  if (mt > 0) d.c_mt[ci] = mt - 1;
+  double vx, vy;
+  set_move_direction(d.c_x[ci], d.c_y[ci], m, r, d.p_cmdx[gp], d.p_cmdy[gp], vx, vy);
+  d.c_vx[ci] = vx;
+  d.c_vy[ci] = vy;
+}
+
+// the rest of Player.update (split, eject, move) + performEjections +
+// handlePlayerCollisions, one thread per player (list order matters)
 __device__ __forceinline__ void update_player(const Dev &d, int gp) {
   const int NP = d.NP;
   // the cell arrays never alias: let the compiler keep values in registers across stores
@@ -144,32 +176,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
   int n = d.p_ncells[gp];
   uint8_t lst[kMaxCells];
   for (int k = 0; k < n; k++) lst[k] = d.p_list[k * NP + gp];
-  // Player.decayMass -> Cell.decayMass (cell.py:123-126)
-  for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)lst[k] * NP + gp;
-    double m = cm[ci];
-    if (m >= 4) {
-      m = m * kDecay;
-      cm[ci] = m;
-      cr[ci] = radius_of(m);
-    }
-  }
-  // updateCellProperties: momentum, merge timer, direction (player.py:39-44)
-  for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)lst[k] * NP + gp;
-    int svc = csvc[ci];
-    double svx = csvx[ci], svy = csvy[ci];
-    update_momentum(svc, svx, svy);
-    csvc[ci] = svc;
-    csvx[ci] = svx;
-    csvy[ci] = svy;
-    double mt = cmt[ci];
-    if (mt > 0) cmt[ci] = mt - 1;
-    double vx, vy;
-    set_move_direction(cx[ci], cy[ci], cm[ci], cr[ci], cpx, cpy, vx, vy);
-    cvx[ci] = vx;
-    cvy[ci] = vy;
-  }
+  // (decay, momentum, merge timer and direction already ran per cell: update_cell)
   int n_new = 0;
   if (d.p_split[gp]) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
     for (int i = 1; i < n; i++) {
@@ -282,17 +289,21 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
   d.p_newb[gp] = nb;
 }
 
-// updateViruses + updateBlobs + updatePlayers in one launch: thread ranges
-// [players | viruses | blobs] (independent entity sets, field.py:94-119)
+// updateViruses + updateBlobs + the per-cell part of updatePlayers in one
+// launch: thread ranges [cell slots | viruses | blobs] (independent, field.py:94-119)
+__global__ void __launch_bounds__(256) k_update_players(Dev d) {
+  int gp = GTID;
+  if (gp < d.NP) update_player(d, gp);
+}
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d) {
   int gi = GTID;
   // clear the player-hash occupancy bitmap for this tick's spawns (k_occupancy refills it)
   for (size_t w = (size_t)gi; w < (size_t)d.A * d.occ_words; w += (size_t)gridDim.x * blockDim.x) d.occ[w] = 0;
-  if (gi < d.NP) {
-    update_player(d, gi);
+  if (gi < kMaxCells * d.NP) {
+    update_cell(d, gi);
     return;
   }
-  gi -= d.NP;
+  gi -= kMaxCells * d.NP;
   if (d.virus_enabled) {
     if (gi < d.A * d.Vcap) {
       update_virus(d, gi);
@@ -422,7 +433,6 @@ __global__ void k_finalize_players(Dev d) {
 }
 
 // ------------------------------------------------------------ grids
-__device__ void pgrid_finish(const Dev &d, int a, int fix);
 
 // generic counting sort by centre bucket. kind: 0 cells (pool), 1 blobs, 2 viruses
 template <int KIND>
@@ -431,7 +441,6 @@ __global__ void k_grid_count(Dev d, int fix) {
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
   bool in = gi < d.A * per;
   int a = in ? gi / per : 0, i = in ? gi - a * per : 0;
-  if (fix && in && i == 0) pgrid_finish(d, a, fix);
   double x = 0, y = 0, r = 0;
   bool ok = false;
   int *rank, *cnt;
@@ -604,7 +613,12 @@ constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
 __device__ __forceinline__ unsigned long long lb_word(unsigned long long st, uint32_t ep, uint32_t v) {
   return st | ((unsigned long long)(ep & 0x3FFFFFFFu) << 32) | v;
 }
-__global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, int *cnt2) {
+// pfix (pellet rebuilds): the block of the last tile, which knows the total,
+// closes the rebuild -- snapshot the source counts for the scatter, set the
+// new pellet count, empty the staging list; pfix 2 also closes the tick.
+// extra: this tick's spawns sit in the staging list uncommitted.
+__global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, int *cnt2, int pfix, int extra,
+                                                 int slot) {
   __shared__ int wsum[4];
   __shared__ int s_total, s_prefix;
   __shared__ uint32_t s_epoch;
@@ -613,9 +627,9 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
   int *c = cnt + (size_t)a * (d.H + 1);
   int *c2 = cnt2 ? cnt2 + (size_t)a * (d.H + 1) : nullptr;  // optional second count array (summed, re-zeroed)
   int *o = start + (size_t)a * (d.H + 1);
-  unsigned long long *st = d.scan_state + (size_t)a * d.scan_tiles;
+  unsigned long long *st = d.scan_state + ((size_t)slot * d.A + a) * d.scan_tiles;
   ArenaCtl &ctl = d.ctl[a];
-  if (tid == 0) s_epoch = __hip_atomic_load(&ctl.scan_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) s_epoch = __hip_atomic_load(&ctl.scan_epoch[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int base = tile * LB_TILE + tid * LB_PER;
   int v[LB_PER], sum = 0;
 #pragma unroll
@@ -699,12 +713,22 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
     if (i < n) o[i] = run;
     run += v[j];
   }
-  if (tile == ntiles - 1 && tid == 0) o[n] = s_prefix + total;
+  if (tile == ntiles - 1 && tid == 0) {
+    o[n] = s_prefix + total;
+    if (pfix) {
+      ctl.src_n_pel = ctl.n_pel;
+      ctl.src_n_stage = ctl.n_pnew + (extra ? ctl.n_spawn_p : 0);
+      ctl.n_pel = min(s_prefix + total, d.Pcap);
+      ctl.n_pnew = 0;
+      ctl.n_pel_eaten = 0;
+      if (pfix == 2) ctl.tick += 1;
+    }
+  }
   if (tid == 0) {  // last block of this launch bumps the epoch
-    int tk = atomicAdd(&ctl.scan_ticket, 1);
+    int tk = atomicAdd(&ctl.scan_ticket[slot], 1);
     if (tk == ntiles - 1) {
-      ctl.scan_ticket = 0;
-      __hip_atomic_fetch_add(&ctl.scan_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ctl.scan_ticket[slot] = 0;
+      __hip_atomic_fetch_add(&ctl.scan_epoch[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -747,7 +771,8 @@ __global__ void k_pgrid_count(Dev d, int src, int use_dead) {
   const int j = i - d.H;
   if (j < d.ctl[a].n_pnew) pgrid_rank_staged(d, a, j);
 }
-__device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src, int use_dead, int extra) {
+// the source counts were snapshotted by the scan's epilogue (src_n_pel, src_n_stage)
+__device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src, int use_dead) {
   const int per = 2 * d.Pcap;
   if (gi >= d.A * per) return;
   const int a = gi / per, i = gi - a * per;
@@ -757,7 +782,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src,
   int64_t s;
   int pos;
   if (i < d.Pcap) {
-    if (i >= c.n_pel) return;
+    if (i >= c.src_n_pel) return;
     size_t g = (size_t)a * d.Pcap + i;
     if (use_dead && d.pel_dead[g]) return;
     x = d.pel_x[src][g];
@@ -768,7 +793,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src,
     pos = d.pstart[H1 + b] + d.pel_rank[R0 + i];
   } else {
     int j = i - d.Pcap;
-    if (j >= c.n_pnew + (extra ? c.n_spawn_p : 0)) return;  // (this tick's spawns are staged, not committed)
+    if (j >= c.src_n_stage) return;
     size_t g = (size_t)a * d.Pcap + j;
     x = d.pn_x[g];
     y = d.pn_y[g];
@@ -789,35 +814,9 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src,
   d.pel_seq[dst][o] = s;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
-// fov: refresh the FOV cache (player state is final); fix: the last block runs
-// the rebuild epilogue for every arena (1; 2 also closes the tick) -- every
-// block has read the staging counters before it takes its ticket
-__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int src, int use_dead, int extra, int fov, int fix) {
-  const int gi = GTID;
-  if (fov && gi < d.NP) store_player_fov(d, gi);
-  pgrid_scatter_one(d, gi, src, use_dead, extra);
-  if (!fix) return;
-  __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(&d.ticket[0], 1) == (int)gridDim.x - 1) {
-    d.ticket[0] = 0;
-    for (int a = 0; a < d.A; a++) pgrid_finish(d, a, fix);
-  }
+__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int src, int use_dead) {
+  pgrid_scatter_one(d, GTID, src, use_dead);
 }
-// pellet-rebuild epilogue (also folded into the next grid-count kernel: fix 1;
-// fix 2 additionally closes the tick)
-__device__ void pgrid_finish(const Dev &d, int a, int fix) {
-  ArenaCtl &c = d.ctl[a];
-  if (fix == 2) c.tick += 1;
-  c.n_pel = d.pstart[(size_t)a * (d.H + 1) + d.H];
-  if (c.n_pel > d.Pcap) c.n_pel = d.Pcap;
-  c.n_pnew = 0;
-  c.n_pel_eaten = 0;
-}
-__global__ void k_pgrid_finish(Dev d, int fix) {
-  int a = GTID;
-  if (a < d.A) pgrid_finish(d, a, fix);
-}
-
 // ------------------------------------------------------------ T10 merge
 __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
   if (gp >= d.NP || !d.p_alive[gp]) return;
@@ -1913,8 +1912,8 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.rmax_cell = radius_of(kStartMass);
   c.rmax_virus = radius_of(kVirusBase);
   c.food_round = 1;
-  c.scan_epoch = 0;
-  c.scan_ticket = 0;
+  c.scan_epoch[0] = c.scan_epoch[1] = 0;
+  c.scan_ticket[0] = c.scan_ticket[1] = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
 }
 
@@ -1927,12 +1926,12 @@ struct Scratch {
 };
 
 // counts (unless already taken by k_spawn_all) -> scan -> scatter (+ epilogue)
-void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead, int fov, int fix, bool counted) {
+void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead, int fix, bool counted) {
   long nc = (long)d.A * (d.H + d.Pcap), ns = std::max((long)d.A * 2 * d.Pcap, (long)d.NP);
   if (!counted) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, src, use_dead);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt);
-  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, src, use_dead, counted ? 1 : 0, fov,
-                     fix);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt, fix,
+                     counted ? 1 : 0, 0);
+  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, src, use_dead);
 }
 
 template <int KIND>
@@ -1940,7 +1939,7 @@ static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start, int f
   int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
   long n = (long)d.A * per;
   hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d, fix);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, cnt, start, nullptr);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, cnt, start, nullptr, 0, 0, 1);
   hipLaunchKernelGGL(k_grid_scatter<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
 }
 
@@ -1954,14 +1953,20 @@ static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
   hipLaunchKernelGGL(k_food_serial<KIND>, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
 }
 
+void launch_player_fov(const Dev &d, hipStream_t s);
+// One Field.update(): a single stream of dependent launches (captured once into a
+// hipGraph by api.hip).  Forking independent phases onto a second stream was
+// measured slower on MI355X (cross-queue dependencies cost more than the
+// overlap gains at this kernel size), so the graph stays linear.
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v) {
   Scratch scr{scr_k, scr_v};
   const int gP = nblk(d.NP, 256);
-  const long n_begin = (long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
+  const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_update_players, dim3(gP), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
-  launch_pellet_rebuild(d, s, 0, 0, 0, 1, false);  // P0 U conversions -> P1 (eat-phase buffer)
+  launch_pellet_rebuild(d, s, 0, 0, 1, false);  // P0 U conversions -> P1 (eat-phase buffer)
   hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
                      dim3(256), 0, s, d);
@@ -1981,7 +1986,10 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
                        (long)d.A * d.H;
   hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d);
   // P1 survivors U spawns -> P0, FOV cache, epilogue closes the tick
-  launch_pellet_rebuild(d, s, 1, 1, 1, 2, true);
+  // closing pellet rebuild, then the FOV cache (player state is final).  The FOV
+  // is its own launch: fused into the scatter it stretched that kernel ~5x.
+  launch_pellet_rebuild(d, s, 1, 1, 2, true);
+  launch_player_fov(d, s);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty
@@ -1994,7 +2002,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.p_eject, 0, sizeof(int) * d.NP, s);
   (void)hipMemsetAsync(d.pel_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Pcap, s);
   (void)hipMemsetAsync(d.b_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Ecap, s);
-  (void)hipMemsetAsync(d.scan_state, 0, sizeof(unsigned long long) * (size_t)d.A * d.scan_tiles, s);
+  (void)hipMemsetAsync(d.scan_state, 0, sizeof(unsigned long long) * 2 * (size_t)d.A * d.scan_tiles, s);
   hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
   (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1);
@@ -2002,7 +2010,8 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
-  launch_pellet_rebuild(d, s, 1, 0, 1, 1, false);  // staging -> P0 (+ FOV cache)
+  launch_pellet_rebuild(d, s, 1, 0, 1, false);  // staging -> P0
+  launch_player_fov(d, s);
 }
 
 }  // namespace aigar

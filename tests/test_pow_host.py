@@ -1,0 +1,18 @@
+"""The fast table-driven pow of aigar_math.h must return exactly the correctly
+rounded value the slow double-double series gives (Ziv test; host build)."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_fast_pow_matches_slow_series(tmp_path):
+    exe = str(tmp_path / "check_pow")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I",
+                           os.path.join(ROOT, "aigar_amd", "csrc"), os.path.join(ROOT, "tools", "gen", "check_pow.cpp"),
+                           "-o", exe])
+    out = subprocess.run([exe, "400000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout, out.stdout
+    err = float(out.stdout.split("(2^")[1].split(")")[0])
+    assert err < -72.0, out.stdout  # bound used by the rounding test is 2^-70
