@@ -46,7 +46,9 @@ struct ArenaCtl {
   uint32_t food_round;   // reservation epoch (grows every eat phase)
   uint32_t scan_epoch[2];  // decoupled look-back epoch per scan slot (grows every launch)
   int scan_ticket[2];      // slot 0: pellet rebuilds, slot 1: cell grid (may run concurrently)
-  int src_n_pel, src_n_stage;  // pellet rebuild: source counts snapshotted by the scan epilogue
+  int src_n_pel, src_n_stage;
+  uint32_t pl_epoch;  // k_players look-back epoch / finished-tile ticket
+  int pl_ticket;  // pellet rebuild: source counts snapshotted by the scan epilogue
   int pad1;
   // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
   // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
@@ -135,6 +137,8 @@ struct Dev {
   double *o_act_cur, *o_act_prev;                // [NP][4]
   // decoupled look-back tile states [A][scan_tiles]
   unsigned long long *scan_state;  // [2 slots][A][scan_tiles]
+  unsigned long long *pl_state;    // [A][pl_tiles] (k_players)
+  int pl_tiles;
   int scan_tiles;
   // observation overflow pool (bots that see more objects than their LDS lists hold)
   int OBcap;

@@ -173,6 +173,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.flags = cfg->flags;
   d.occ_words = (d.H + 63) / 64;
   d.scan_tiles = (d.H + 2047) / 2048;
+  d.pl_tiles = (d.B + 255) / 256;
   for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_cr((double)k, 0.32);
   d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (k_grid_small)
   while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
@@ -223,6 +224,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(o_act_prev, double, NP * 4);
   d.OBcap = (int)std::min<size_t>(std::max<size_t>(1u << 20, 64 * NP), (size_t)1 << 24);
   AL(scan_state, unsigned long long, 2 * A * d.scan_tiles);
+  AL(pl_state, unsigned long long, A * d.pl_tiles);
   AL(ticket, int, 4);
   AL(ob_used, unsigned long long, 1);
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
@@ -756,6 +758,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   HIPCHK(hipMemsetAsync(d.pel_owner + (size_t)arena * d.Pcap, 0, 8 * (size_t)d.Pcap, h->stream));
   HIPCHK(hipMemsetAsync(d.b_owner + (size_t)arena * d.Ecap, 0, 8 * (size_t)d.Ecap, h->stream));
   // look-back epochs restart too: clear this arena's tile states
+  HIPCHK(hipMemsetAsync(d.pl_state + (size_t)arena * d.pl_tiles, 0, 8 * (size_t)d.pl_tiles, h->stream));
   for (int sl = 0; sl < 2; sl++)
     HIPCHK(hipMemsetAsync(d.scan_state + ((size_t)sl * d.A + arena) * d.scan_tiles, 0, 8 * (size_t)d.scan_tiles,
                           h->stream));

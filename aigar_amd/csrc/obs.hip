@@ -109,115 +109,141 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
   const ArenaCtl &ctl = d.ctl[a];
 
-  // collect(run, L, cap): run the scan into the LDS list; on overflow claim a
-  // slice of the global pool and rerun the scan into it.  Returns the count.
-  auto collect = [&](auto run, ObjList &Lst, int cap, ObjList Gp) -> int {
-    int n = run(Lst, cap);
-    if (n <= cap) return n;
-    int b = 0;
-    if (lane == 0) b = obs_claim(d, epoch, n);
-    b = __shfl(b, 0);
-    if (b + n > d.OBcap) {
-      if (lane == 0) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
-      return 0;
-    }
-    if (Gp.seq) Gp.seq += b;
-    if (Gp.m) Gp.m += b;
-    if (Gp.r) Gp.r += b;
-    Gp.mask += b;
-    if (Gp.own) Gp.own += b;
-    if (Gp.perm) Gp.perm += b;
-    run(Gp, n);
-    Lst = Gp;
-    return n;
-  };
-  const ObjList Gpool{d.ob_seq, d.ob_m, d.ob_r, d.ob_mask, d.ob_own, d.ob_perm};
+  // ---- getPelletsInFov / getEnemyPlayerCellsInFov / getVirusesInFov
+  // (field.py:434-456) as ONE walk: every grid row the FOV touches (pellet,
+  // cell and virus grids) gets a lane that fetches its item range, the ranges
+  // are flattened with a prefix sum, and each step inspects 64 candidates of any
+  // kind with a single round of loads (per-lane base pointers), so the three
+  // queries share their memory latency instead of chaining it.
+  const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
+  const int Ec = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
+  const int Ev = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
+  const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, 0), sv = grid_span(Q, Ev, d.cols, d.cshift);
+  const int np_rows = (qok && (d.obs_ch & AIGAR_OBS_PELLET)) ? sp.by1 - sp.by0 + 1 : 0;
+  const int nc_rows = qok ? sc.by1 - sc.by0 + 1 : 0;
+  const int nv_rows = (qok && d.virus_enabled) ? sv.by1 - sv.by0 + 1 : 0;
+  const int nrows = np_rows + nc_rows + nv_rows;
+  const size_t H1 = (size_t)a * (d.H + 1);
+  const int *pst = d.pstart + H1, *cst = d.cstart + H1, *vst = d.vstart + H1;
+  const int *cit = d.citems + (size_t)a * kMaxCells * d.B, *vit = d.vitems + (size_t)a * d.Vcap;
+  const unsigned long long lt = (1ull << lane) - 1;
 
-  // ---- pellets: getPelletsInFov (field.py:442-444) -> float hash
-  ObjList PL{p_seq, p_m, nullptr, p_mask, nullptr, p_perm};
-  int np = 0;
-  if (d.obs_ch & AIGAR_OBS_PELLET) {
-    const int *st = d.pstart + (size_t)a * (d.H + 1);
-    auto run = [&](ObjList &Lst, int cap) -> int {
-      int n = 0;
-      wave_grid_for(st, nullptr, d.cols, Q, 1, [&](bool valid, int t) {
-        Cand c{false, 0, 0, 0, 0, 0};
-        if (valid) {
-          size_t g = (size_t)a * d.Pcap + t;
-          double px = d.pel_x[0][g], py = d.pel_y[0][g], pm = d.pel_m[0][g];
-          double pr = radius_of(pm);
-          if (rect_hit(footprint(px, py, pr, d.size), Q) && in_fov(px, py, pr, fx, fy, fs)) {
-            uint32_t ix = axis_mask(px - left, pr, gs, lim), iy = axis_mask(py - top, pr, gs, lim);
-            if (ix && iy) c = Cand{true, d.pel_seq[0][g], pm, pr, ix | (iy << 16), 0};
-          }
-        }
-        list_append(c, Lst, cap, n);
-      });
-      return n;
-    };
-    np = collect(run, PL, OBS_PCAP, ObjList{Gpool.seq, Gpool.m, nullptr, Gpool.mask, nullptr, Gpool.perm});
-  }
-  // ---- cells: own (getPortionOfCellsInFov(player.getCells())) then enemies in the
-  // player hash (getEnemyPlayerCellsInFov, field.py:434-436)
-  ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
-  int nc;
-  {
-    const int *st = d.cstart + (size_t)a * (d.H + 1);
-    const int *it = d.citems + (size_t)a * kMaxCells * d.B;
-    int E = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
-    auto run = [&](ObjList &Lst, int cap) -> int {
-      int n = 0;
+  auto walk = [&](ObjList &PLx, int capP, ObjList &CLx, int capC, ObjList &VLx, int capV, int &np, int &nc,
+                  int &nv) {
+    np = nc = nv = 0;
+    {  // own cells first: getPortionOfCellsInFov(player.getCells())
       Cand c{false, 0, 0, 0, 0, 1};
       if (lane < ncell) {
         size_t ci = (size_t)d.p_list[lane * NP + gp] * NP + gp;
-        double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci];
+        double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci], m = d.c_m[ci];
         if (in_fov(x, y, r, fx, fy, fs)) {
           uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
-          if (ix && iy) c = Cand{true, 0, d.c_m[ci], r, ix | (iy << 16), 1};
+          if (ix && iy) c = Cand{true, 0, m, r, ix | (iy << 16), 1};
         }
       }
-      list_append(c, Lst, cap, n);
-      wave_grid_for(st, it, d.cols, Q, E, [&](bool valid, int e) {
-        Cand q{false, 0, 0, 0, 0, 0};
-        if (valid && (d.c_flags[e] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && (e % NP) != gp) {
-          double x = d.c_x[e], y = d.c_y[e], r = d.c_r[e];
-          if (rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs)) {
-            uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
-            if (ix && iy) q = Cand{true, 0, d.c_m[e], r, ix | (iy << 16), 0};
-          }
+      list_append(c, CLx, capC, nc);
+    }
+    for (int r0 = 0; r0 < nrows; r0 += 64) {
+      const int R = r0 + lane, nr = min(64, nrows - r0);
+      int lo = 0, len = 0, kind = 0;
+      if (R < nrows) {
+        const int *st;
+        int row, bx0, bx1, stride;
+        if (R < np_rows) {
+          st = pst; row = sp.by0 + R; bx0 = sp.bx0; bx1 = sp.bx1; stride = sp.stride;
+        } else if (R < np_rows + nc_rows) {
+          kind = 1; st = cst; row = sc.by0 + (R - np_rows); bx0 = sc.bx0; bx1 = sc.bx1; stride = sc.stride;
+        } else {
+          kind = 2; st = vst; row = sv.by0 + (R - np_rows - nc_rows); bx0 = sv.bx0; bx1 = sv.bx1; stride = sv.stride;
         }
-        list_append(q, Lst, cap, n);
-      });
-      return n;
-    };
-    nc = collect(run, CL, OBS_CCAP, ObjList{nullptr, Gpool.m, nullptr, Gpool.mask, Gpool.own, nullptr});
-  }
-  // ---- viruses: getVirusesInFov (virus hash members only)
-  ObjList VL{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
-  int nv = 0;
-  if (d.virus_enabled) {
-    const int *st = d.vstart + (size_t)a * (d.H + 1);
-    const int *it = d.vitems + (size_t)a * d.Vcap;
-    int E = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
-    auto run = [&](ObjList &Lst, int cap) -> int {
-      int n = 0;
-      wave_grid_for(st, it, d.cols, Q, E, [&](bool valid, int j) {
-        Cand c{false, 0, 0, 0, 0, 0};
+        lo = st[row * stride + bx0];
+        len = st[row * stride + bx1 + 1] - lo;
+      }
+      int inc = len;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        int y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+      }
+      const int excl = inc - len, total = __shfl(inc, 63);
+      for (int t0 = 0; t0 < total; t0 += 64) {
+        const int t = t0 + lane;
+        int rw = 0;
+        for (int k = 1; k < nr; k++) rw = (__shfl(excl, k) <= t) ? k : rw;
+        const int idx = __shfl(lo, rw) + (t - __shfl(excl, rw));
+        const int kd = __shfl(kind, rw);
+        const bool valid = t < total;
+        size_t g = 0;
+        if (valid) g = kd == 0 ? (size_t)a * d.Pcap + idx : (kd == 1 ? (size_t)cit[idx] : (size_t)a * d.Vcap + vit[idx]);
+        const double *X = kd == 0 ? d.pel_x[0] : (kd == 1 ? d.c_x : d.v_x);
+        const double *Y = kd == 0 ? d.pel_y[0] : (kd == 1 ? d.c_y : d.v_y);
+        const double *M = kd == 0 ? d.pel_m[0] : (kd == 1 ? d.c_m : d.v_m);
+        const double *RR = kd == 1 ? d.c_r : d.v_r;
+        const int64_t *S = kd == 0 ? d.pel_seq[0] : d.v_seq;
+        const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
+        bool ok = false;
+        double x = 0, y = 0, m = 0, r = 0;
+        int64_t sq = 0;
         if (valid) {
-          size_t g = (size_t)a * d.Vcap + j;
-          if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH)) {
-            double x = d.v_x[g], y = d.v_y[g], vr = d.v_r[g];
-            if (rect_hit(footprint(x, y, vr, d.size), Q) && in_fov(x, y, vr, fx, fy, fs)) {
-              uint32_t ix = axis_mask(x - left, vr, gs, lim), iy = axis_mask(y - top, vr, gs, lim);
-              if (ix && iy) c = Cand{true, d.v_seq[g], d.v_m[g], vr, ix | (iy << 16), 0};
-            }
-          }
+          x = X[g];
+          y = Y[g];
+          m = M[g];
+          r = kd == 0 ? 0.0 : RR[g];
+          sq = kd == 1 ? 0 : S[g];
+          uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
+          if (kd == 0) r = radius_of(m);
+          ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && (int)(g % NP) == gp) &&
+               rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs);
         }
-        list_append(c, Lst, cap, n);
-      }, d.cshift);
-      return n;
-    };
-    nv = collect(run, VL, OBS_VCAP, ObjList{Gpool.seq, Gpool.m, Gpool.r, Gpool.mask, nullptr, nullptr});
+        uint32_t msk = 0;
+        if (ok) {
+          uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
+          ok = ix && iy;
+          msk = ix | (iy << 16);
+        }
+        list_append(Cand{ok && kd == 0, sq, m, r, msk, 0}, PLx, capP, np);
+        list_append(Cand{ok && kd == 1, sq, m, r, msk, 0}, CLx, capC, nc);
+        list_append(Cand{ok && kd == 2, sq, m, r, msk, 0}, VLx, capV, nv);
+      }
+    }
+  };
+  ObjList PL{p_seq, p_m, nullptr, p_mask, nullptr, p_perm};
+  ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
+  ObjList VL{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
+  int np, nc, nv;
+  walk(PL, OBS_PCAP, CL, OBS_CCAP, VL, OBS_VCAP, np, nc, nv);
+  if (np > OBS_PCAP || nc > OBS_CCAP || nv > OBS_VCAP) {
+    // a list outgrew LDS: claim slices of the global pool for the overflowing
+    // lists and walk again (exact, only slower)
+    const int need = (np > OBS_PCAP ? np : 0) + (nc > OBS_CCAP ? nc : 0) + (nv > OBS_VCAP ? nv : 0);
+    int b = 0;
+    if (lane == 0) b = obs_claim(d, epoch, need);
+    b = __shfl(b, 0);
+    if (b + need > d.OBcap) {
+      if (lane == 0) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
+      np = min(np, OBS_PCAP);
+      nc = min(nc, OBS_CCAP);
+      nv = min(nv, OBS_VCAP);
+    } else {
+      auto slice = [&](ObjList Lg, bool over, ObjList Ll, int n, int &cap) {
+        if (!over) return Ll;
+        if (Lg.seq) Lg.seq += b;
+        if (Lg.m) Lg.m += b;
+        if (Lg.r) Lg.r += b;
+        Lg.mask += b;
+        if (Lg.own) Lg.own += b;
+        if (Lg.perm) Lg.perm += b;
+        b += n;
+        cap = n;
+        return Lg;
+      };
+      int cp = OBS_PCAP, cc = OBS_CCAP, cv = OBS_VCAP;
+      PL = slice(ObjList{d.ob_seq, d.ob_m, nullptr, d.ob_mask, nullptr, d.ob_perm}, np > OBS_PCAP, PL, np, cp);
+      CL = slice(ObjList{nullptr, d.ob_m, nullptr, d.ob_mask, d.ob_own, nullptr}, nc > OBS_CCAP, CL, nc, cc);
+      VL = slice(ObjList{d.ob_seq, d.ob_m, d.ob_r, d.ob_mask, nullptr, nullptr}, nv > OBS_VCAP, VL, nv, cv);
+      wave_fence();
+      walk(PL, cp, CL, cc, VL, cv, np, nc, nv);
+    }
   }
   wave_fence();  // lists written by all lanes -> read by all lanes
   // rank pellets by creation sequence (the sum order of the reference)

@@ -432,6 +432,167 @@ __global__ void k_finalize_players(Dev d) {
   }
 }
 
+// updatePlayers' per-player part + the creation-sequence numbering + the blob
+// append, in ONE launch.  Grid (tiles, arenas) of 256 players; each tile scans
+// its (new cells + new blobs, new blobs) counts, then a decoupled look-back
+// over the arena's tiles (one 64-bit word per tile: status 2 | epoch 14 |
+// seq 24 | blobs 24) gives every player its offsets, and the player assigns its
+// new cells' seqs and writes its blobs right away (field.py:112-146,121-132).
+// The bases (seq_next, n_blob) are read by every tile before it publishes; the
+// last tile, whose look-back proves all tiles have published, advances them.
+constexpr unsigned long long PL_AGG = 1ull << 62, PL_INC = 2ull << 62;
+__device__ __forceinline__ unsigned long long pl_word(unsigned long long st, uint32_t ep, uint32_t vs, uint32_t vb) {
+  return st | ((unsigned long long)(ep & 0x3FFFu) << 48) | ((unsigned long long)(vs & 0xFFFFFFu) << 24) |
+         (unsigned long long)(vb & 0xFFFFFFu);
+}
+__global__ void __launch_bounds__(256) k_players(Dev d) {
+  __shared__ int ws[4], wb[4];
+  __shared__ int s_ps, s_pb, s_ts, s_tb, s_blob0;
+  __shared__ int64_t s_seq0;
+  __shared__ uint32_t s_epoch;
+  const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ntiles = gridDim.x, NP = d.NP;
+  ArenaCtl &c = d.ctl[a];
+  unsigned long long *st = d.pl_state + (size_t)a * ntiles;
+  if (tid == 0) {
+    s_epoch = __hip_atomic_load(&c.pl_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_seq0 = c.seq_next;
+    s_blob0 = c.n_blob;
+    if (tile == 0) {  // grid radius bounds restart (re-maxed by every grid build)
+      c.rmax_cell = 0;
+      c.rmax_virus = 0;
+    }
+  }
+  const int p = tile * 256 + tid, gp = a * d.B + p;
+  int nn = 0, nb = 0;
+  if (p < d.B) {
+    update_player(d, gp);
+    nn = d.p_newc[gp];
+    nb = d.p_newb[gp];
+  }
+  const int vs = nn + nb, vb = nb;
+  int is = vs, ib = vb;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y1 = __shfl_up(is, off), y2 = __shfl_up(ib, off);
+    if (lane >= off) {
+      is += y1;
+      ib += y2;
+    }
+  }
+  if (lane == 63) {
+    ws[w] = is;
+    wb[w] = ib;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int ts = 0, tb = 0;
+    for (int k = 0; k < 4; k++) {
+      int x1 = ws[k], x2 = wb[k];
+      ws[k] = ts;
+      wb[k] = tb;
+      ts += x1;
+      tb += x2;
+    }
+    s_ts = ts;
+    s_tb = tb;
+  }
+  __syncthreads();
+  const uint32_t ep = s_epoch;
+  if (w == 0) {
+    const uint32_t ts = s_ts, tb = s_tb;
+    if (tile == 0) {
+      if (lane == 0) {
+        __hip_atomic_store(&st[0], pl_word(PL_INC, ep, ts, tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ps = s_pb = 0;
+      }
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(&st[tile], pl_word(PL_AGG, ep, ts, tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int run_s = 0, run_b = 0, hi = tile - 1;
+      for (;;) {
+        int t = hi - lane;
+        unsigned long long word = 0;
+        bool ready = true;
+        if (t >= 0) {
+          word = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ready = (word >> 62) != 0 && (uint32_t)((word >> 48) & 0x3FFFu) == (ep & 0x3FFFu);
+        }
+        if (!__all(ready)) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        unsigned long long incmask = __ballot(t >= 0 && (word >> 62) == 2);
+        int stop = incmask ? __ffsll((long long)incmask) - 1 : 64;
+        bool take = t >= 0 && lane <= stop;
+        int v1 = take ? (int)((word >> 24) & 0xFFFFFFu) : 0, v2 = take ? (int)(word & 0xFFFFFFu) : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          v1 += __shfl_xor(v1, off);
+          v2 += __shfl_xor(v2, off);
+        }
+        run_s += v1;
+        run_b += v2;
+        if (incmask || hi - 63 < 0) break;
+        hi -= 64;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(&st[tile], pl_word(PL_INC, ep, run_s + ts, run_b + tb), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        s_ps = run_s;
+        s_pb = run_b;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t seq0 = s_seq0;
+  const int blob0 = s_blob0;
+  if (tile == ntiles - 1 && tid == 0) {  // arena totals are known: advance the bases
+    const int tot = s_ps + s_ts, totb = s_pb + s_tb;
+    c.seq_base_upd = seq0;
+    c.seq_next = seq0 + tot;
+    c.n_blob_base = blob0;
+    if (blob0 + totb > d.Ecap) {
+      c.err |= ERR_BLOB_CAP;
+      c.n_blob = d.Ecap;
+    } else {
+      c.n_blob = blob0 + totb;
+    }
+  }
+  if (p < d.B && d.p_alive[gp]) {
+    const int64_t s0 = seq0 + s_ps + ws[w] + (is - vs);
+    const int boff = s_pb + wb[w] + (ib - vb);
+    const int n = d.p_ncells[gp];
+    for (int k = 0; k < n; k++) {
+      size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+      if (k >= n - nn) d.c_seq[ci] = s0 + (k - (n - nn));
+      d.c_flags[ci] = (d.c_flags[ci] & ~F_NEW) | F_INHASH;  // updateHashTables inserts every cell
+    }
+    for (int j = 0; j < nb; j++) {
+      int bi = blob0 + boff + j;
+      if (bi >= d.Ecap) break;  // ERR_BLOB_CAP set above
+      size_t g = (size_t)a * d.Ecap + bi, si = (size_t)j * NP + gp;
+      const double bm = kEjectMass * 0.8;
+      d.b_x[g] = d.sb_x[si];
+      d.b_y[g] = d.sb_y[si];
+      d.b_m[g] = bm;
+      d.b_r[g] = radius_of(bm);
+      d.b_vx[g] = 0;
+      d.b_vy[g] = 0;
+      d.b_svx[g] = d.sb_svx[si];
+      d.b_svy[g] = d.sb_svy[si];
+      d.b_svc[g] = 15;
+      d.b_seq[g] = s0 + nn + j;
+      d.b_ej[g] = d.c_seq[(size_t)d.sb_slot[si] * NP + gp];
+      d.b_flags[g] = F_ALIVE;
+    }
+  }
+  if (tid == 0 && atomicAdd(&c.pl_ticket, 1) == ntiles - 1) {  // last block of the arena bumps the epoch
+    c.pl_ticket = 0;
+    __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ------------------------------------------------------------ grids
 
 // generic counting sort by centre bucket. kind: 0 cells (pool), 1 blobs, 2 viruses
@@ -1913,6 +2074,8 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.rmax_virus = radius_of(kVirusBase);
   c.food_round = 1;
   c.scan_epoch[0] = c.scan_epoch[1] = 0;
+  c.pl_epoch = 0;
+  c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
 }
@@ -1963,9 +2126,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   const int gP = nblk(d.NP, 256);
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_update_players, dim3(gP), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_scan_players, dim3(d.A), dim3(1024), 0, s, d);
-  hipLaunchKernelGGL(k_finalize_players, dim3(gP), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
   launch_pellet_rebuild(d, s, 0, 0, 1, false);  // P0 U conversions -> P1 (eat-phase buffer)
   hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
@@ -2003,6 +2164,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.pel_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Pcap, s);
   (void)hipMemsetAsync(d.b_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Ecap, s);
   (void)hipMemsetAsync(d.scan_state, 0, sizeof(unsigned long long) * 2 * (size_t)d.A * d.scan_tiles, s);
+  (void)hipMemsetAsync(d.pl_state, 0, sizeof(unsigned long long) * (size_t)d.A * d.pl_tiles, s);
   hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
   (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1);
