@@ -47,6 +47,7 @@ struct ArenaCtl {
   uint32_t scan_epoch[2];  // decoupled look-back epoch per scan slot (grows every launch)
   int scan_ticket[2];      // slot 0: pellet rebuilds, slot 1: cell grid (may run concurrently)
   int src_n_pel, src_n_stage;
+  uint32_t dirty;     // DIRTY_*: a virus / blob died this tick (k_spawn_plan compacts)
   uint32_t pl_epoch;  // k_players look-back epoch / finished-tile ticket
   int pl_ticket;  // pellet rebuild: source counts snapshotted by the scan epilogue
   int pad1;
@@ -60,6 +61,7 @@ enum : uint32_t {
   ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2 };
+enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
 
 // event phases (sort key high word), in reference order within a tick
 enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4, PH_PP = 5, PH_SPAWN = 6 };

@@ -111,6 +111,7 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
     d.pn_m[pj] = d.b_m[gi];
     d.pn_seq[pj] = d.b_seq[gi];
     d.b_flags[gi] = 0;
+    atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
     return;
   }
   int svc = d.b_svc[gi];
@@ -1119,6 +1120,7 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
       d.v_r[gv] = radius_of(m);
       c.rmax_virus = fmax(c.rmax_virus, d.v_r[gv]);
       d.b_flags[g] = 0;
+      atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
       if (m >= thr) {  // virus split (field.py:318-325, cell.py:72-85)
         if (c.n_vir >= d.Vcap) {
           c.err |= ERR_VIRUS_CAP;
@@ -1281,6 +1283,7 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
         d.c_m[ci] = m;
         d.c_r[ci] = radius_of(m);
         d.v_flags[g] = 0;
+        atomicOr(&d.ctl[a].dirty, DIRTY_VIRUS);
         // playerCellAteVirus (field.py:350-370)
         int ncur = d.p_ncells[gp];
         int n_new = kMaxCells - ncur;
@@ -1351,7 +1354,10 @@ struct Food {
   __device__ int64_t ej(int j) const { return KIND == 0 ? -2 : d.b_ej[g(j)]; }
   __device__ void kill(int j) const {
     if (KIND == 0) d.pel_dead[g(j)] = 1;
-    else d.b_flags[g(j)] = 0;
+    else {
+      d.b_flags[g(j)] = 0;
+      atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
+    }
   }
   __device__ uint64_t *owner(int j) const { return (KIND == 0 ? d.pel_owner : d.b_owner) + g(j); }
   __device__ const int *start() const { return (KIND == 0 ? d.pstart : d.bstart) + (size_t)a * (d.H + 1); }
@@ -1847,8 +1853,11 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
   int a = blockIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
-  // order-preserving compaction of viruses and blobs (list order == creation order)
+  // order-preserving compaction of viruses and blobs (list order == creation order),
+  // only for lists that lost an entity this tick
+  const uint32_t dirty = c.dirty;
   for (int kind = 0; kind < 2; kind++) {
+    if (!(dirty & (kind == 0 ? DIRTY_VIRUS : DIRTY_BLOB))) continue;
     int n = kind == 0 ? c.n_vir : c.n_blob;
     int cap = kind == 0 ? d.Vcap : d.Ecap;
     int out = 0;
@@ -1899,8 +1908,11 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
   }
   // the virus list is compacted: re-index the virus grid for the observations
   // (membership stays the F_INHASH flag; the viruses spawned below are not hashed)
-  if (d.virus_enabled) grid_small_build<2>(d, a, gcnt, sflag);
+  // (unchanged otherwise: viruses do not move after updateViruses, and the ones
+  // appended by splits or spawns are not hashed this tick)
+  if (d.virus_enabled && (dirty & DIRTY_VIRUS)) grid_small_build<2>(d, a, gcnt, sflag);
   if (tid != 0) return;
+  c.dirty = 0;
   // spawnPellets: while len(pellets) < maxCollectibleCount
   int alive_p = c.n_pel - c.n_pel_eaten + c.n_pnew;
   int kp = 0;
@@ -2075,6 +2087,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.food_round = 1;
   c.scan_epoch[0] = c.scan_epoch[1] = 0;
   c.pl_epoch = 0;
+  c.dirty = 0;
   c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
