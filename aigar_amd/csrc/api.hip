@@ -503,8 +503,9 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
   std::vector<int64_t> ps, bseq, bej, vseq;
   std::vector<int> bsvc, vsvc;
   std::vector<uint32_t> bfl, vfl;
-  if (d2h(h, px, d.pel_x[0] + po, c.n_pel) || d2h(h, py, d.pel_y[0] + po, c.n_pel) ||
-      d2h(h, pm, d.pel_m[0] + po, c.n_pel) || d2h(h, ps, d.pel_seq[0] + po, c.n_pel))
+  const int pb = c.pcur;
+  if (d2h(h, px, d.pel_x[pb] + po, c.n_pel) || d2h(h, py, d.pel_y[pb] + po, c.n_pel) ||
+      d2h(h, pm, d.pel_m[pb] + po, c.n_pel) || d2h(h, ps, d.pel_seq[pb] + po, c.n_pel))
     return -1;
   double *bfs[8] = {d.b_x, d.b_y, d.b_m, d.b_r, d.b_vx, d.b_vy, d.b_svx, d.b_svy};
   double *vfs[8] = {d.v_x, d.v_y, d.v_m, d.v_r, d.v_vx, d.v_vy, d.v_svx, d.v_svy};
@@ -759,6 +760,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   HIPCHK(hipMemsetAsync(d.b_owner + (size_t)arena * d.Ecap, 0, 8 * (size_t)d.Ecap, h->stream));
   // look-back epochs restart too: clear this arena's tile states
   HIPCHK(hipMemsetAsync(d.pl_state + (size_t)arena * d.pl_tiles, 0, 8 * (size_t)d.pl_tiles, h->stream));
+  HIPCHK(hipMemsetAsync(d.pel_dead + (size_t)arena * d.Pcap, 0, (size_t)d.Pcap, h->stream));  // buffer 0 is current
   for (int sl = 0; sl < 2; sl++)
     HIPCHK(hipMemsetAsync(d.scan_state + ((size_t)sl * d.A + arena) * d.scan_tiles, 0, 8 * (size_t)d.scan_tiles,
                           h->stream));

@@ -116,6 +116,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   // kind with a single round of loads (per-lane base pointers), so the three
   // queries share their memory latency instead of chaining it.
   const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
+  const int pcur = ctl.pcur;  // current pellet buffer
   const int Ec = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
   const int Ev = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
   const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, 0), sv = grid_span(Q, Ev, d.cols, d.cshift);
@@ -175,11 +176,11 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
         const bool valid = t < total;
         size_t g = 0;
         if (valid) g = kd == 0 ? (size_t)a * d.Pcap + idx : (kd == 1 ? (size_t)cit[idx] : (size_t)a * d.Vcap + vit[idx]);
-        const double *X = kd == 0 ? d.pel_x[0] : (kd == 1 ? d.c_x : d.v_x);
-        const double *Y = kd == 0 ? d.pel_y[0] : (kd == 1 ? d.c_y : d.v_y);
-        const double *M = kd == 0 ? d.pel_m[0] : (kd == 1 ? d.c_m : d.v_m);
+        const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
+        const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
+        const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
         const double *RR = kd == 1 ? d.c_r : d.v_r;
-        const int64_t *S = kd == 0 ? d.pel_seq[0] : d.v_seq;
+        const int64_t *S = kd == 0 ? d.pel_seq[pcur] : d.v_seq;
         const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
         bool ok = false;
         double x = 0, y = 0, m = 0, r = 0;

@@ -791,6 +791,7 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
   int *o = start + (size_t)a * (d.H + 1);
   unsigned long long *st = d.scan_state + ((size_t)slot * d.A + a) * d.scan_tiles;
   ArenaCtl &ctl = d.ctl[a];
+  if (pfix == PR_CONVERT && ctl.p_skip) return;  // (uniform over the arena's blocks)
   if (tid == 0) s_epoch = __hip_atomic_load(&ctl.scan_epoch[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int base = tile * LB_TILE + tid * LB_PER;
   int v[LB_PER], sum = 0;
@@ -883,7 +884,10 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
       ctl.n_pel = min(s_prefix + total, d.Pcap);
       ctl.n_pnew = 0;
       ctl.n_pel_eaten = 0;
-      if (pfix == 2) ctl.tick += 1;
+      if (pfix == PR_CLOSE) {
+        ctl.tick += 1;
+        ctl.pcur = ctl.peat ^ 1;
+      }
     }
   }
   if (tid == 0) {  // last block of this launch bumps the epoch
@@ -921,24 +925,39 @@ __device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
   const int b = center_bucket_coord(d.pn_y[g], d.cols) * d.cols + center_bucket_coord(d.pn_x[g], d.cols);
   d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + b], 1);
 }
-__global__ void k_pgrid_count(Dev d, int src, int use_dead) {
+// mode PR_RESET: staging -> buffer 0; PR_CONVERT: current buffer U blob
+// conversions -> the other buffer, skipped (eat phase reads the current buffer)
+// when nothing was converted -- the common case
+__global__ void k_pgrid_count(Dev d, int mode) {
   const int gi = GTID;
   const int per = d.H + d.Pcap;
   if (gi >= d.A * per) return;
   const int a = gi / per, i = gi - a * per;
+  if (mode == PR_CONVERT) {
+    ArenaCtl &c = d.ctl[a];
+    const bool skip = c.n_pnew == 0;
+    if (i == 0) {
+      c.p_skip = skip;
+      c.peat = skip ? c.pcur : c.pcur ^ 1;
+    }
+    if (skip) return;
+  }
   if (i < d.H) {  // bucket i of the source layout
-    pgrid_count_bucket(d, a, i, use_dead);
+    pgrid_count_bucket(d, a, i, 0);
     return;
   }
   const int j = i - d.H;
   if (j < d.ctl[a].n_pnew) pgrid_rank_staged(d, a, j);
 }
 // the source counts were snapshotted by the scan's epilogue (src_n_pel, src_n_stage)
-__device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src, int use_dead) {
+__device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode) {
   const int per = 2 * d.Pcap;
   if (gi >= d.A * per) return;
   const int a = gi / per, i = gi - a * per;
   const ArenaCtl &c = d.ctl[a];
+  if (mode == PR_CONVERT && c.p_skip) return;
+  const bool use_dead = mode == PR_CLOSE;
+  const int src = mode == PR_RESET ? 1 : (mode == PR_CONVERT ? c.pcur : c.peat), dst = src ^ 1;
   const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
   double x, y, m;
   int64_t s;
@@ -946,7 +965,10 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src,
   if (i < d.Pcap) {
     if (i >= c.src_n_pel) return;
     size_t g = (size_t)a * d.Pcap + i;
-    if (use_dead && d.pel_dead[g]) return;
+    if (use_dead && d.pel_dead[g]) {  // eaten: drop it, and leave the flags clean for the next eat phase
+      d.pel_dead[g] = 0;
+      return;
+    }
     x = d.pel_x[src][g];
     y = d.pel_y[src][g];
     m = d.pel_m[src][g];
@@ -969,15 +991,14 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int src,
     return;
   }
   size_t o = (size_t)a * d.Pcap + pos;
-  int dst = src ^ 1;
   d.pel_x[dst][o] = x;
   d.pel_y[dst][o] = y;
   d.pel_m[dst][o] = m;
   d.pel_seq[dst][o] = s;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
-__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int src, int use_dead) {
-  pgrid_scatter_one(d, GTID, src, use_dead);
+__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode) {
+  pgrid_scatter_one(d, GTID, mode);
 }
 // ------------------------------------------------------------ T10 merge
 __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
@@ -1342,14 +1363,14 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
 template <int KIND>
 struct Food {
   const Dev &d;
-  int a;
-  __device__ Food(const Dev &dd, int aa) : d(dd), a(aa) {}
+  int a, pb;  // pb: the eat-phase pellet buffer (ArenaCtl::peat)
+  __device__ Food(const Dev &dd, int aa) : d(dd), a(aa), pb(KIND == 0 ? dd.ctl[aa].peat : 0) {}
   __device__ size_t g(int j) const { return (size_t)a * (KIND == 0 ? d.Pcap : d.Ecap) + j; }
-  __device__ double x(int j) const { return KIND == 0 ? d.pel_x[1][g(j)] : d.b_x[g(j)]; }
-  __device__ double y(int j) const { return KIND == 0 ? d.pel_y[1][g(j)] : d.b_y[g(j)]; }
-  __device__ double m(int j) const { return KIND == 0 ? d.pel_m[1][g(j)] : d.b_m[g(j)]; }
-  __device__ double r(int j) const { return KIND == 0 ? radius_of(d.pel_m[1][g(j)]) : d.b_r[g(j)]; }
-  __device__ int64_t seq(int j) const { return KIND == 0 ? d.pel_seq[1][g(j)] : d.b_seq[g(j)]; }
+  __device__ double x(int j) const { return KIND == 0 ? d.pel_x[pb][g(j)] : d.b_x[g(j)]; }
+  __device__ double y(int j) const { return KIND == 0 ? d.pel_y[pb][g(j)] : d.b_y[g(j)]; }
+  __device__ double m(int j) const { return KIND == 0 ? d.pel_m[pb][g(j)] : d.b_m[g(j)]; }
+  __device__ double r(int j) const { return KIND == 0 ? radius_of(d.pel_m[pb][g(j)]) : d.b_r[g(j)]; }
+  __device__ int64_t seq(int j) const { return KIND == 0 ? d.pel_seq[pb][g(j)] : d.b_seq[g(j)]; }
   __device__ bool alive(int j) const { return KIND == 0 ? !d.pel_dead[g(j)] : (d.b_flags[g(j)] & F_ALIVE); }
   __device__ int64_t ej(int j) const { return KIND == 0 ? -2 : d.b_ej[g(j)]; }
   __device__ void kill(int j) const {
@@ -2088,6 +2109,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.scan_epoch[0] = c.scan_epoch[1] = 0;
   c.pl_epoch = 0;
   c.dirty = 0;
+  c.pcur = c.peat = c.p_skip = 0;
   c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
@@ -2101,13 +2123,13 @@ struct Scratch {
   int *v;
 };
 
-// counts (unless already taken by k_spawn_all) -> scan -> scatter (+ epilogue)
-void launch_pellet_rebuild(const Dev &d, hipStream_t s, int src, int use_dead, int fix, bool counted) {
-  long nc = (long)d.A * (d.H + d.Pcap), ns = std::max((long)d.A * 2 * d.Pcap, (long)d.NP);
-  if (!counted) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, src, use_dead);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt, fix,
-                     counted ? 1 : 0, 0);
-  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, src, use_dead);
+// counts (PR_CLOSE: already taken by k_spawn_all) -> scan (+ epilogue) -> scatter
+void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
+  long nc = (long)d.A * (d.H + d.Pcap), ns = (long)d.A * 2 * d.Pcap;
+  if (mode != PR_CLOSE) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, mode);
+  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt, mode,
+                     mode == PR_CLOSE ? 1 : 0, 0);
+  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, mode);
 }
 
 template <int KIND>
@@ -2140,7 +2162,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
-  launch_pellet_rebuild(d, s, 0, 0, 1, false);  // P0 U conversions -> P1 (eat-phase buffer)
+  launch_pellet_rebuild(d, s, PR_CONVERT);  // current U blob conversions -> eat-phase buffer
   hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
                      dim3(256), 0, s, d);
@@ -2162,7 +2184,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   // P1 survivors U spawns -> P0, FOV cache, epilogue closes the tick
   // closing pellet rebuild, then the FOV cache (player state is final).  The FOV
   // is its own launch: fused into the scatter it stretched that kernel ~5x.
-  launch_pellet_rebuild(d, s, 1, 1, 2, true);
+  launch_pellet_rebuild(d, s, PR_CLOSE);  // eat-phase survivors U spawns -> new current buffer
   launch_player_fov(d, s);
 }
 
@@ -2185,7 +2207,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
-  launch_pellet_rebuild(d, s, 1, 0, 1, false);  // staging -> P0
+  launch_pellet_rebuild(d, s, PR_RESET);  // staging -> buffer 0
   launch_player_fov(d, s);
 }
 
