@@ -42,6 +42,7 @@ struct ArenaCtl {
   uint32_t err;   // sticky error bits (capacity overflow ...)
   uint32_t warn;  // sticky quirk bits (reference would raise)
   double rmax_cell, rmax_virus;
+  double vmin_mass;  // lightest virus at the mid-tick virus grid build
   uint64_t ev_order;     // serial-phase event counter
   uint32_t food_round;   // reservation epoch (grows every eat phase)
   uint32_t scan_epoch[2];  // decoupled look-back epoch per scan slot (grows every launch)

@@ -48,7 +48,7 @@ struct aigar_handle {
   hipStream_t stream = nullptr;
   bool own_stream = true;
   uint32_t obs_calls = 0;
-  int rounds = 2;  // parallel reservation rounds before the serial fallback (tools/micro/exp1.sh)
+  int rounds = 1;  // parallel reservation rounds before the serial fallback (tools/micro/exp_rounds.sh)
   int64_t *scr_k = nullptr;
   int *scr_v = nullptr;
   double *d_cmd = nullptr, *d_stats = nullptr;

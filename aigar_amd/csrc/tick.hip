@@ -718,6 +718,7 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
 constexpr int SG_CAP = 4096;
 template <int KIND>
 __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
+  __shared__ double vmin_w[16];
   const int tid = threadIdx.x, s = d.cshift;
   const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
   ArenaCtl &c = d.ctl[a];
@@ -742,8 +743,24 @@ __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
     }
     rank[i] = rk;
   }
-  if (KIND == 2) wave_atomic_max_pos(&c.rmax_virus, rloc);
+  if (KIND == 2) {
+    wave_atomic_max_pos(&c.rmax_virus, rloc);
+    // lightest virus (bounds who can eat one in playerVirusOverlap)
+    double mn = __builtin_inf();
+    for (int i = tid; i < n; i += 1024) {
+      size_t g = (size_t)a * per + i;
+      if (d.v_flags[g] & F_ALIVE) mn = fmin(mn, d.v_m[g]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off));
+    if ((tid & 63) == 0) vmin_w[tid >> 6] = mn;
+  }
   __syncthreads();
+  if (KIND == 2 && tid == 0) {
+    double mn = vmin_w[0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); k++) mn = fmin(mn, vmin_w[k]);
+    c.vmin_mass = mn;
+  }
   block_scan_excl(cnt, cnt, Hc + 1, sh);  // in place: bucket starts
   for (int i = tid; i <= Hc; i += 1024) start[i] = cnt[i];
   for (int i = tid; i < n; i += 1024) {
@@ -1232,10 +1249,17 @@ __global__ void __launch_bounds__(256) k_pv_active(Dev d) {
   const int *st = d.vstart + (size_t)a * (d.H + 1);
   const int *it = d.vitems + (size_t)a * d.Vcap;
   int E = expand_for(d.ctl[a].rmax_virus);
+  // lightest virus at the grid build (k_grid_small); viruses split during
+  // virusBlobOverlap are >= (VIRUS_BASE_SIZE + 7 * 14.4) / 2, so VIRUS_BASE_SIZE bounds them
+  const double vmin = fmin(d.ctl[a].vmin_mass, kVirusBase);
   bool anyp = false;
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    if (!(m > 1.25 * vmin)) {  // lighter than 1.25 x the lightest virus: nothing to eat
+      if (lane == 0) d.c_active[ci] = 0;
+      continue;
+    }
     Rect q = footprint(x, y, r, d.size);
     bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int j) {
       size_t g = (size_t)a * d.Vcap + j;
