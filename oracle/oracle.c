@@ -48,7 +48,8 @@ static const double MERGE_TIME_VIRUS_FACTOR = 0.85;
 #define CELL_MASS_DECAY_RATE (1 - (0.01 * SPEED_MODIFIER))
 
 /* philox streams (shared definition with aigar_amd/csrc/aigar_rng.h) */
-enum { ST_PELLET = 1, ST_VIRUS = 2, ST_PLAYER = 3, ST_ANGLE = 4, ST_INIT_PLAYER = 5, ST_POLICY = 6 };
+enum { ST_PELLET = 1, ST_VIRUS = 2, ST_PLAYER = 3, ST_ANGLE = 4, ST_INIT_PLAYER = 5, ST_POLICY = 6, ST_GREEDY = 7,
+       ST_GREEDY_LH = 8 };
 
 /* ------------------------------------------------------------ errors ---- */
 static __thread char g_err[512];
@@ -96,6 +97,12 @@ double oracle_np_sum(const double *a, int n) {
 double oracle_py_round3(double v) {
   char buf[64];
   snprintf(buf, sizeof buf, "%.3f", v);
+  return strtod(buf, NULL);
+}
+/* Python round(v, 5) (bot.py:16-21 getRelativeCellPos) */
+double oracle_py_round5(double v) {
+  char buf[64];
+  snprintf(buf, sizeof buf, "%.5f", v);
   return strtod(buf, NULL);
 }
 
@@ -271,6 +278,7 @@ typedef struct Arena {
   int64_t *ev;
   int n_ev, cap_ev;
   int err;
+  int *split_lh; /* Greedy bots' splitLikelihood (bot.py:93); NULL: derived from the Philox key */
 } Arena;
 
 typedef struct Oracle {
@@ -941,6 +949,90 @@ static void field_update(Arena *A) { /* field.py:85-92 */
 
 /* --------------------------------------------------- observation ----- */
 /* float-variant spatial hash (spatialHashTable.py:85-108) */
+/* ------------------------------------------------------ Greedy bot ---- */
+static inline double u01(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
+/* splitLikelihood = numpy.random.randint(9950, 10000) at bot creation (bot.py:93) */
+static int greedy_split_likelihood(const Arena *A, int p) {
+  if (A->split_lh) return A->split_lh[p];
+  uint64_t u[4];
+  philox_site(A->key, (uint64_t)p, ST_GREEDY_LH, 0, 0, u);
+  return (int)ph_randint(u[0], 9950, 10000);
+}
+/* Bot.makeMove for a Greedy bot (bot.py:252-269): make_greedy_bot_move
+ * (bot.py:579-633) then set_command_point (bot.py:550-577).  Candidates come
+ * in the reference's list order -- pellets, then enemy cells, then viruses,
+ * each in (canonical) set order -- and max() keeps the first maximum. */
+static void greedy_move(Arena *A, int p, int greedy_split) {
+  Player *P = &A->pl[p];
+  if (!P->alive) return;
+  double fx, fy;
+  player_fov_pos(P, &fx, &fy);
+  const double size = player_fov_size(P);
+  const int64_t x = (int64_t)fx, y = (int64_t)fy;
+  const int64_t left = x - (int64_t)(size / 2), top = y - (int64_t)(size / 2);
+  CVec q = {0}, cand = {0};
+  hash_query(&A->ph, fx, fy, size / 2, &q); /* getPelletsInFov */
+  for (int i = 0; i < q.n; i++)
+    if (in_fov(q.a[i], fx, fy, size)) cv_push(&cand, q.a[i]);
+  Cell *big = P->cells.a[0]; /* max(playerCells, key=mass): first maximum */
+  for (int k = 1; k < P->cells.n; k++)
+    if (P->cells.a[k]->mass > big->mass) big = P->cells.a[k];
+  hash_query(&A->plh, fx, fy, size / 2, &q); /* getEnemyPlayerCellsInFov */
+  for (int i = 0; i < q.n; i++)
+    if (in_fov(q.a[i], fx, fy, size) && q.a[i]->player != p && big->mass > 1.25 * q.a[i]->mass)
+      cv_push(&cand, q.a[i]);
+  if (A->virus_enabled) { /* getVirusesInFov */
+    hash_query(&A->vh, fx, fy, size / 2, &q);
+    for (int i = 0; i < q.n; i++)
+      if (in_fov(q.a[i], fx, fy, size) && big->mass > 1.25 * q.a[i]->mass) cv_push(&cand, q.a[i]);
+  }
+  uint64_t u[4] = {0, 0, 0, 0};
+  if (A->rng_mode != AIGAR_RNG_MT19937) philox_site(A->key, (uint64_t)p, ST_GREEDY, (uint64_t)A->tick, 0, u);
+  double a0, a1;
+  if (cand.n) {
+    Cell *best = NULL;
+    double bk = 0;
+    for (int i = 0; i < cand.n; i++) {
+      Cell *c = cand.a[i];
+      double sd = sqdist(c, big);
+      double k = c->mass / (sd != 0 ? sd : 1);
+      if (!best || k > bk) {
+        best = c;
+        bk = k;
+      }
+    }
+    a0 = oracle_py_round5((best->x - (double)left) / size); /* getRelativeCellPos (bot.py:16-21) */
+    a1 = oracle_py_round5((best->y - (double)top) / size);
+  } else if (A->rng_mode == AIGAR_RNG_MT19937) {
+    a0 = mt_random(&A->mt);
+    a1 = mt_random(&A->mt);
+  } else {
+    a0 = u01(u[0]);
+    a1 = u01(u[1]);
+  }
+  int split = 0, eject = 0;
+  if (greedy_split) {
+    int64_t rs, re;
+    if (A->rng_mode == AIGAR_RNG_MT19937) {
+      rs = mt_randint(&A->mt, 0, 10000);
+      re = mt_randint(&A->mt, 0, 10000);
+    } else {
+      rs = ph_randint(u[2], 0, 10000);
+      re = ph_randint(u[3], 0, 10000);
+    }
+    split = rs > greedy_split_likelihood(A, p);
+    eject = re > 100000; /* ejectLikelihood (bot.py:94) */
+  }
+  /* set_command_point (bot.py:550-577) with the 4-element action */
+  const int64_t isz = (int64_t)size;
+  P->cmdx = (double)left + a0 * (double)isz;
+  P->cmdy = (double)top + a1 * (double)isz;
+  P->do_split = split;
+  P->do_eject = eject;
+  cv_free(&q);
+  cv_free(&cand);
+}
+
 typedef struct { int cols, rows; CVec *b; } FHash;
 static void fh_insert_all(FHash *fh, double size, double gs, double left, double top, Cell **objs, int n) {
   for (int k = 0; k < n; k++) {
@@ -1180,7 +1272,7 @@ void oracle_destroy(void *h) {
     arena_free_world(A);
     for (int p = 0; p < A->B; p++) cv_free(&A->pl[p].cells);
     cv_free(&A->pellets); cv_free(&A->blobs); cv_free(&A->viruses); cv_free(&A->grave);
-    free(A->pl); free(A->dead); free(A->ev);
+    free(A->pl); free(A->dead); free(A->ev); free(A->split_lh);
     free(A->obs_fov); free(A->self_lf); free(A->self_slf); free(A->enemy_lf); free(A->enemy_slf);
     free(A->act_cur); free(A->act_prev);
   }
@@ -1456,5 +1548,25 @@ int oracle_set_mt(void *h, int arena, const uint32_t *key, int pos) {
   Arena *A = &((Oracle *)h)->ar[arena];
   memcpy(A->mt.key, key, sizeof A->mt.key);
   A->mt.pos = pos;
+  return 0;
+}
+
+/* Model.takeBotActions for an all-Greedy population (bot.py:252-269) */
+int oracle_policy_greedy(void *h, int greedy_split) {
+  Oracle *O = (Oracle *)h;
+  for (int a = 0; a < O->A; a++)
+    for (int p = 0; p < O->ar[a].B; p++) greedy_move(&O->ar[a], p, greedy_split);
+  return 0;
+}
+/* explicit splitLikelihoods (e.g. replayed from numpy's stream); NULL restores the Philox-derived ones */
+int oracle_set_split_likelihood(void *h, int arena, const int *lh) {
+  Arena *A = &((Oracle *)h)->ar[arena];
+  if (!lh) {
+    free(A->split_lh);
+    A->split_lh = NULL;
+    return 0;
+  }
+  if (!A->split_lh) A->split_lh = (int *)malloc(sizeof(int) * A->B);
+  memcpy(A->split_lh, lh, sizeof(int) * A->B);
   return 0;
 }

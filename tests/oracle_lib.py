@@ -57,6 +57,10 @@ def lib():
         L.oracle_mt_random.restype = C.c_double
         L.oracle_mt_random.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
         L.oracle_philox.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.oracle_policy_greedy.argtypes = [vp, C.c_int]
+        L.oracle_set_split_likelihood.argtypes = [vp, C.c_int, C.POINTER(C.c_int)]
+        L.oracle_py_round5.restype = C.c_double
+        L.oracle_py_round5.argtypes = [C.c_double]
         _lib = L
     return _lib
 
@@ -148,6 +152,23 @@ class Oracle:
     def set_mt(self, key, pos, arena=0):
         k = np.ascontiguousarray(key, np.uint32)
         self._chk(self.L.oracle_set_mt(self.h, arena, k.ctypes.data_as(C.POINTER(C.c_uint32)), int(pos)))
+
+    def policy_greedy(self, greedy_split=False):
+        """Model.takeBotActions with every player a Greedy bot (bot.py:252-269, 579-633)."""
+        self._chk(self.L.oracle_policy_greedy(self.h, int(bool(greedy_split))))
+
+    def set_split_likelihood(self, lh, arena=0):
+        if lh is None:
+            self.L.oracle_set_split_likelihood(self.h, arena, None)
+            return
+        a = np.ascontiguousarray(lh, np.int32)
+        self.L.oracle_set_split_likelihood(self.h, arena, a.ctypes.data_as(C.POINTER(C.c_int)))
+
+    def commands(self, arena=0):
+        """Current (x, y, split, eject) of every player of the arena."""
+        st = self.get_state(arena)
+        pf, pi = np.asarray(st["players_f"]), np.asarray(st["players_i"])
+        return np.c_[pf[:, 0], pf[:, 1], pi[:, 2], pi[:, 3]].astype(np.float64)
 
     def reset_obs_state(self):
         self._chk(self.L.oracle_reset_obs_state(self.h))

@@ -1,0 +1,50 @@
+"""Pin the oracle's Greedy bot (bot.py:252-269, 579-633, 550-577) against the
+reference: replaying the reference's own greedy runs, the oracle must produce
+the exact commands the reference bots issued every tick -- including the
+numpy draws of the random fallback and of ENABLE_GREEDY_SPLIT, checked through
+the MT19937 stream position after every takeBotActions."""
+import os
+
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import Oracle, golden_state, lib, make_config
+
+# (fixture, numpy seed of the scenario, ENABLE_GREEDY_SPLIT) -- tools/golden/gen_golden.py SCENARIOS
+GREEDY = [("c1_greedy", 0, False), ("greedy16", 1, False), ("greedy16_virus_split", 2, True)]
+
+
+def split_likelihoods(seed, n):
+    """The n numpy.random.randint(9950, 10000) draws of the bots' creation (bot.py:93),
+    the first draws after numpy.random.seed(seed) (gen_golden.py seeds right before createBot)."""
+    import ctypes as C
+    L = lib()
+    key = (C.c_uint32 * 624)()
+    pos = C.c_int(0)
+    L.oracle_mt_seed(seed, key, C.byref(pos))
+    return [int(L.oracle_mt_randint(key, C.byref(pos), 9950.0, 10000.0)) for _ in range(n)]
+
+
+@pytest.mark.parametrize("name,seed,gsplit", GREEDY)
+def test_oracle_greedy_reproduces_reference_commands(name, seed, gsplit, golden_dir):
+    z = np.load(os.path.join(golden_dir, name + ".npz"))
+    n = int(z["n_players"])
+    cfg = make_config(bots=n, field_size=int(z["size"]), virus=bool(z["virus_enabled"]),
+                      max_pellets=float(z["max_pellets"]), max_viruses=float(z["max_viruses"]),
+                      channels=int(z["obs_channels"]), extras=int(z["obs_extras"]), rng_mode=_abi.RNG_MT19937)
+    o = Oracle(cfg)
+    o.load_state(golden_state(z, "init"))
+    o.set_split_likelihood(split_likelihoods(seed, n))
+    for t in range(int(z["ticks"])):
+        o.policy_greedy(gsplit)
+        cmd = o.commands()
+        want = z["cmds"][t]
+        bad = np.argwhere(cmd != want)
+        assert not len(bad), "tick %d player %d: oracle %s reference %s" % (t, bad[0][0], cmd[bad[0][0]],
+                                                                         want[bad[0][0]])
+        st = o.get_state()
+        assert np.array_equal(st["mt_key"], z["mt_keys"][t]) and st["mt_pos"] == z["mt_pos"][t], \
+            "numpy stream position differs after the bots' moves at tick %d" % t
+        o.step(1)
+    o.close()
