@@ -72,6 +72,8 @@ def load(build_if_missing=False):
         "aigar_kernel_time": [vp, C.c_char_p, dp, C.POINTER(i32)],
         "aigar_selftest_pow": [dp, dp, dp, i32],
         "aigar_counters": [vp, i32, C.POINTER(C.c_int64), i32],
+        "aigar_policy_greedy": [vp, i32, vp, i32],
+        "aigar_set_split_likelihood": [vp, i32, C.POINTER(C.c_int32)],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -134,6 +136,20 @@ class Stepper:
 
     def policy_random(self, p_split=0.0, p_eject=0.0, seed=0):
         self._chk(self.L.aigar_policy_random(self.h, float(p_split), float(p_eject), int(seed)))
+
+    def policy_greedy(self, greedy_split=False, mask=None):
+        """Greedy bots' moves (bot.py:579-633) for the players where mask != 0 (all if None)."""
+        if isinstance(mask, np.ndarray):
+            mask = np.ascontiguousarray(mask, np.uint8).reshape(self.NP)
+        p, dev = _ptr(mask)
+        self._chk(self.L.aigar_policy_greedy(self.h, int(bool(greedy_split)), p, dev))
+
+    def set_split_likelihood(self, lh, arena=0):
+        if lh is None:
+            self._chk(self.L.aigar_set_split_likelihood(self.h, arena, None))
+            return
+        a = np.ascontiguousarray(lh, np.int32).reshape(self.B)
+        self._chk(self.L.aigar_set_split_likelihood(self.h, arena, a.ctypes.data_as(C.POINTER(C.c_int32))))
 
     def step(self, n=1):
         self._chk(self.L.aigar_step(self.h, int(n)))

@@ -21,6 +21,7 @@ void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t 
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
 void launch_player_stats(const Dev &d, hipStream_t s, double *out);
 void launch_player_fov(const Dev &d, hipStream_t s);
+void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask);
 void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd);
 }  // namespace aigar
 
@@ -52,6 +53,7 @@ struct aigar_handle {
   int64_t *scr_k = nullptr;
   int *scr_v = nullptr;
   double *d_cmd = nullptr, *d_stats = nullptr;
+  uint8_t *d_mask = nullptr;
   void *d_obs = nullptr;
   std::vector<void *> allocs;
   bool profile = false;
@@ -227,15 +229,17 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(pl_state, unsigned long long, A * d.pl_tiles);
   AL(ticket, int, 4);
   AL(ob_used, unsigned long long, 1);
+  AL(p_split_lh, int, NP);
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
 #undef AL
   h->scr_k = dalloc<int64_t>(h, A * d.Wcap);
   h->scr_v = dalloc<int>(h, A * d.Wcap);
   h->d_cmd = dalloc<double>(h, NP * 4);
+  h->d_mask = dalloc<uint8_t>(h, NP);
   h->d_stats = dalloc<double>(h, NP * 5);
   h->d_obs = dalloc<double>(h, NP * (size_t)d.L);
-  ok = ok && h->scr_k && h->scr_v && h->d_cmd && h->d_stats && h->d_obs;
+  ok = ok && h->scr_k && h->scr_v && h->d_cmd && h->d_stats && h->d_obs && h->d_mask;
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
   if (!ok) {
@@ -770,6 +774,37 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
     HIPCHK(hipMemsetAsync(p + p0 * GG, 0, 8 * B * GG, h->stream));
   launch_player_fov(d, h->stream);  // FOV cache of the loaded players
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int aigar_policy_greedy(aigar_handle *h, int greedy_split, const uint8_t *mask, int on_device) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const uint8_t *m = mask;
+  if (mask && !on_device) {
+    HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)h->d.NP, hipMemcpyHostToDevice, h->stream));
+    m = h->d_mask;
+  }
+  {
+    Mark mk(h, "policy");
+    launch_policy_greedy(h->d, h->stream, greedy_split ? 1 : 0, m);
+  }
+  HIPCHK(hipGetLastError());
+  if (mask && !on_device) HIPCHK(hipStreamSynchronize(h->stream));  // (host mask buffer reused next call)
+  return 0;
+}
+
+extern "C" int aigar_set_split_likelihood(aigar_handle *h, int arena, const int32_t *lh) {
+  if (!h) return fail("null handle");
+  if (arena < 0 || arena >= h->d.A) return fail("arena out of range");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  int *dst = h->d.p_split_lh + (size_t)arena * h->d.B;
+  if (!lh) {
+    HIPCHK(hipMemsetAsync(dst, 0, sizeof(int) * h->d.B, h->stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(dst, lh, sizeof(int) * h->d.B, hipMemcpyHostToDevice, h->stream));
+  }
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }

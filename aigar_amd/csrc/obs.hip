@@ -80,6 +80,66 @@ __device__ __forceinline__ int obs_claim(const Dev &d, uint32_t epoch, int n) {
   return ((uint32_t)(assumed >> 32) == epoch) ? (int)(assumed & 0xFFFFFFFFull) : 0;
 }
 
+// The FOV queries of the reference -- getPelletsInFov, getEnemyPlayerCellsInFov,
+// getVirusesInFov (field.py:434-456): hash lookup around the FOV box, then
+// Cell.isInFov -- as ONE wave-wide walk: every grid row the box touches (pellet,
+// cell and virus grids) gets a lane that fetches its item range, the ranges
+// are flattened with a prefix sum, and each step hands 64 candidates of any
+// kind to f(valid, kind, g) (kind 0 pellet slot, 1 cell pool index, 2 virus
+// slot; g is the global index), so the three queries share their memory
+// latency instead of chaining it.  f is called by every lane (it may ballot).
+template <class F>
+__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool want_p, bool want_v, F f) {
+  const int lane = threadIdx.x & 63;
+  const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
+  const ArenaCtl &ctl = d.ctl[a];
+  const int Ec = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
+  const int Ev = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
+  const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, 0), sv = grid_span(Q, Ev, d.cols, d.cshift);
+  const int np_rows = (qok && want_p) ? sp.by1 - sp.by0 + 1 : 0;
+  const int nc_rows = qok ? sc.by1 - sc.by0 + 1 : 0;
+  const int nv_rows = (qok && want_v) ? sv.by1 - sv.by0 + 1 : 0;
+  const int nrows = np_rows + nc_rows + nv_rows;
+  const size_t H1 = (size_t)a * (d.H + 1);
+  const int *pst = d.pstart + H1, *cst = d.cstart + H1, *vst = d.vstart + H1;
+  const int *cit = d.citems + (size_t)a * kMaxCells * d.B, *vit = d.vitems + (size_t)a * d.Vcap;
+  for (int r0 = 0; r0 < nrows; r0 += 64) {
+    const int R = r0 + lane, nr = min(64, nrows - r0);
+    int lo = 0, len = 0, kind = 0;
+    if (R < nrows) {
+      const int *st;
+      int row, bx0, bx1, stride;
+      if (R < np_rows) {
+        st = pst; row = sp.by0 + R; bx0 = sp.bx0; bx1 = sp.bx1; stride = sp.stride;
+      } else if (R < np_rows + nc_rows) {
+        kind = 1; st = cst; row = sc.by0 + (R - np_rows); bx0 = sc.bx0; bx1 = sc.bx1; stride = sc.stride;
+      } else {
+        kind = 2; st = vst; row = sv.by0 + (R - np_rows - nc_rows); bx0 = sv.bx0; bx1 = sv.bx1; stride = sv.stride;
+      }
+      lo = st[row * stride + bx0];
+      len = st[row * stride + bx1 + 1] - lo;
+    }
+    int inc = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    const int excl = inc - len, total = __shfl(inc, 63);
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      const int t = t0 + lane;
+      int rw = 0;
+      for (int k = 1; k < nr; k++) rw = (__shfl(excl, k) <= t) ? k : rw;
+      const int idx = __shfl(lo, rw) + (t - __shfl(excl, rw));
+      const int kd = __shfl(kind, rw);
+      const bool valid = t < total;
+      size_t g = 0;
+      if (valid) g = kd == 0 ? (size_t)a * d.Pcap + idx : (kd == 1 ? (size_t)cit[idx] : (size_t)a * d.Vcap + vit[idx]);
+      f(valid, kd, g);
+    }
+  }
+}
+
 template <typename OutT>
 __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch) {
   __shared__ int64_t p_seq[OBS_PCAP];
@@ -115,19 +175,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   // are flattened with a prefix sum, and each step inspects 64 candidates of any
   // kind with a single round of loads (per-lane base pointers), so the three
   // queries share their memory latency instead of chaining it.
-  const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
   const int pcur = ctl.pcur;  // current pellet buffer
-  const int Ec = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
-  const int Ev = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
-  const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, 0), sv = grid_span(Q, Ev, d.cols, d.cshift);
-  const int np_rows = (qok && (d.obs_ch & AIGAR_OBS_PELLET)) ? sp.by1 - sp.by0 + 1 : 0;
-  const int nc_rows = qok ? sc.by1 - sc.by0 + 1 : 0;
-  const int nv_rows = (qok && d.virus_enabled) ? sv.by1 - sv.by0 + 1 : 0;
-  const int nrows = np_rows + nc_rows + nv_rows;
-  const size_t H1 = (size_t)a * (d.H + 1);
-  const int *pst = d.pstart + H1, *cst = d.cstart + H1, *vst = d.vstart + H1;
-  const int *cit = d.citems + (size_t)a * kMaxCells * d.B, *vit = d.vitems + (size_t)a * d.Vcap;
-  const unsigned long long lt = (1ull << lane) - 1;
 
   auto walk = [&](ObjList &PLx, int capP, ObjList &CLx, int capC, ObjList &VLx, int capV, int &np, int &nc,
                   int &nv) {
@@ -144,69 +192,37 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
       }
       list_append(c, CLx, capC, nc);
     }
-    for (int r0 = 0; r0 < nrows; r0 += 64) {
-      const int R = r0 + lane, nr = min(64, nrows - r0);
-      int lo = 0, len = 0, kind = 0;
-      if (R < nrows) {
-        const int *st;
-        int row, bx0, bx1, stride;
-        if (R < np_rows) {
-          st = pst; row = sp.by0 + R; bx0 = sp.bx0; bx1 = sp.bx1; stride = sp.stride;
-        } else if (R < np_rows + nc_rows) {
-          kind = 1; st = cst; row = sc.by0 + (R - np_rows); bx0 = sc.bx0; bx1 = sc.bx1; stride = sc.stride;
-        } else {
-          kind = 2; st = vst; row = sv.by0 + (R - np_rows - nc_rows); bx0 = sv.bx0; bx1 = sv.bx1; stride = sv.stride;
-        }
-        lo = st[row * stride + bx0];
-        len = st[row * stride + bx1 + 1] - lo;
+    wave_fov_walk(d, a, Q, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, [&](bool valid, int kd, size_t g) {
+      const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
+      const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
+      const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
+      const double *RR = kd == 1 ? d.c_r : d.v_r;
+      const int64_t *S = kd == 0 ? d.pel_seq[pcur] : d.v_seq;
+      const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
+      bool ok = false;
+      double x = 0, y = 0, m = 0, r = 0;
+      int64_t sq = 0;
+      if (valid) {
+        x = X[g];
+        y = Y[g];
+        m = M[g];
+        r = kd == 0 ? 0.0 : RR[g];
+        sq = kd == 1 ? 0 : S[g];
+        uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
+        if (kd == 0) r = radius_of(m);
+        ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && (int)(g % NP) == gp) &&
+             rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs);
       }
-      int inc = len;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        int y = __shfl_up(inc, off);
-        if (lane >= off) inc += y;
+      uint32_t msk = 0;
+      if (ok) {
+        uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
+        ok = ix && iy;
+        msk = ix | (iy << 16);
       }
-      const int excl = inc - len, total = __shfl(inc, 63);
-      for (int t0 = 0; t0 < total; t0 += 64) {
-        const int t = t0 + lane;
-        int rw = 0;
-        for (int k = 1; k < nr; k++) rw = (__shfl(excl, k) <= t) ? k : rw;
-        const int idx = __shfl(lo, rw) + (t - __shfl(excl, rw));
-        const int kd = __shfl(kind, rw);
-        const bool valid = t < total;
-        size_t g = 0;
-        if (valid) g = kd == 0 ? (size_t)a * d.Pcap + idx : (kd == 1 ? (size_t)cit[idx] : (size_t)a * d.Vcap + vit[idx]);
-        const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
-        const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
-        const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
-        const double *RR = kd == 1 ? d.c_r : d.v_r;
-        const int64_t *S = kd == 0 ? d.pel_seq[pcur] : d.v_seq;
-        const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
-        bool ok = false;
-        double x = 0, y = 0, m = 0, r = 0;
-        int64_t sq = 0;
-        if (valid) {
-          x = X[g];
-          y = Y[g];
-          m = M[g];
-          r = kd == 0 ? 0.0 : RR[g];
-          sq = kd == 1 ? 0 : S[g];
-          uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
-          if (kd == 0) r = radius_of(m);
-          ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && (int)(g % NP) == gp) &&
-               rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs);
-        }
-        uint32_t msk = 0;
-        if (ok) {
-          uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
-          ok = ix && iy;
-          msk = ix | (iy << 16);
-        }
-        list_append(Cand{ok && kd == 0, sq, m, r, msk, 0}, PLx, capP, np);
-        list_append(Cand{ok && kd == 1, sq, m, r, msk, 0}, CLx, capC, nc);
-        list_append(Cand{ok && kd == 2, sq, m, r, msk, 0}, VLx, capV, nv);
-      }
-    }
+      list_append(Cand{ok && kd == 0, sq, m, r, msk, 0}, PLx, capP, np);
+      list_append(Cand{ok && kd == 1, sq, m, r, msk, 0}, CLx, capC, nc);
+      list_append(Cand{ok && kd == 2, sq, m, r, msk, 0}, VLx, capV, nv);
+    });
   };
   ObjList PL{p_seq, p_m, nullptr, p_mask, nullptr, p_perm};
   ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
@@ -361,6 +377,135 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
     if (ex & AIGAR_EX_2LAST_ACT)
       for (int k = 0; k < 4; k++) row[o++] = (OutT)d.o_act_prev[(size_t)gp * 4 + k];
   }
+}
+
+// Python round(v, 5) (getRelativeCellPos, bot.py:16-21): round-half-even of
+// the exact binary value to a multiple of 1e-5, as the double nearest k/1e5
+__device__ __forceinline__ double py_round5(double v) {
+  double p = v * 100000.0;
+  double e = fma(v, 100000.0, -p);  // p + e == 1e5 * v exactly
+  double k0 = floor(p), f, dd;
+  if (p == k0 && e < 0) {
+    f = k0 - 1;
+    dd = 1.0;
+  } else {
+    f = k0;
+    dd = p - k0;
+  }
+  double g = dd - 0.5;
+  int sgn = (g != 0) ? (g > 0 ? 1 : -1) : (e > 0 ? 1 : (e < 0 ? -1 : 0));
+  double k = (sgn > 0) ? f + 1 : (sgn < 0) ? f : ((fmod(f, 2.0) == 0.0) ? f : f + 1);
+  double r = k / 100000.0;
+  if (r == 0.0) r = copysign(0.0, v);
+  return r;
+}
+
+// Model.takeBotActions for Greedy bots (bot.py:252-269): make_greedy_bot_move
+// (bot.py:579-633) then set_command_point (bot.py:550-577).  One wavefront per
+// bot: the three FOV queries in one walk, every lane keeps its best
+// mass/distance^2 candidate, a wave reduction picks the maximum with the
+// reference's tie rule (first in list order: pellets, enemy cells, viruses,
+// each by creation sequence).  mask (optional): which players are Greedy bots.
+__global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, const uint8_t *mask) {
+  const int gp = blockIdx.x, lane = threadIdx.x, NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  if (!d.p_alive[gp] || (mask && !mask[gp])) return;  // makeMove: dead players keep their command
+  const ArenaCtl &ctl = d.ctl[a];
+  const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
+  const int64_t ix = (int64_t)fx, iy = (int64_t)fy;
+  const int64_t left = ix - (int64_t)(fs / 2), top = iy - (int64_t)(fs / 2);
+  // biggest own cell: max(playerCells, key=mass) keeps the first maximum
+  const int ncell = d.p_ncells[gp];
+  double bm = -1, bx = 0, by = 0;
+  if (lane < ncell) {
+    size_t ci = (size_t)d.p_list[lane * NP + gp] * NP + gp;
+    bm = d.c_m[ci];
+    bx = d.c_x[ci];
+    by = d.c_y[ci];
+  }
+  int bl = lane;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double om = __shfl_xor(bm, off);
+    int ol = __shfl_xor(bl, off);
+    if (om > bm || (om == bm && ol < bl)) {
+      bm = om;
+      bl = ol;
+    }
+  }
+  bx = __shfl(bx, bl);
+  by = __shfl(by, bl);
+  const Rect Q = footprint(fx, fy, fs / 2, d.size);
+  const int pcur = ctl.pcur;
+  double best = -1;
+  uint64_t bord = ~0ull;
+  double tx = 0, ty = 0;
+  wave_fov_walk(d, a, Q, true, d.virus_enabled, [&](bool valid, int kd, size_t g) {
+    if (!valid) return;
+    const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
+    const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
+    const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
+    const double *RR = kd == 1 ? d.c_r : d.v_r;
+    const int64_t *S = kd == 0 ? d.pel_seq[pcur] : (kd == 1 ? d.c_seq : d.v_seq);
+    const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
+    const double x = X[g], y = Y[g], m = M[g];
+    const double r = kd == 0 ? radius_of(m) : RR[g];
+    const uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
+    if ((fl & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
+    if (kd == 1 && (int)(g % NP) == gp) return;
+    if (!(rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs))) return;
+    if (kd != 0 && !(bm > 1.25 * m)) return;  // the biggest own cell must be able to eat it
+    const double sd = (x - bx) * (x - bx) + (y - by) * (y - by);
+    const double k = m / (sd != 0 ? sd : 1);
+    const uint64_t ord = ((uint64_t)kd << 56) | (uint64_t)S[g];
+    if (k > best || (k == best && ord < bord)) {
+      best = k;
+      bord = ord;
+      tx = x;
+      ty = y;
+    }
+  });
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double ok = __shfl_xor(best, off);
+    uint64_t oo = __shfl_xor(bord, off);
+    double ox = __shfl_xor(tx, off), oy = __shfl_xor(ty, off);
+    if (ok > best || (ok == best && oo < bord)) {
+      best = ok;
+      bord = oo;
+      tx = ox;
+      ty = oy;
+    }
+  }
+  if (lane != 0) return;
+  uint64_t u[4];
+  philox((uint64_t)p, ST_GREEDY, (uint64_t)ctl.tick, 0, ctl.key0, ctl.key1, u);
+  double a0, a1;
+  if (bord != ~0ull) {  // getRelativeCellPos(bestCell, left, top, size)
+    a0 = py_round5((tx - (double)left) / fs);
+    a1 = py_round5((ty - (double)top) / fs);
+  } else {
+    a0 = u01(u[0]);
+    a1 = u01(u[1]);
+  }
+  int split = 0, eject = 0;
+  if (greedy_split) {  // ENABLE_GREEDY_SPLIT: randint(0, 10000) > splitLikelihood
+    int lh = d.p_split_lh[gp];
+    if (lh <= 0) {
+      uint64_t v[4];
+      philox((uint64_t)p, ST_GREEDY_LH, 0, 0, ctl.key0, ctl.key1, v);
+      lh = (int)ph_randint(v[0], 9950, 10000);
+    }
+    split = ph_randint(u[2], 0, 10000) > lh;
+    eject = ph_randint(u[3], 0, 10000) > 100000;  // ejectLikelihood (bot.py:94)
+  }
+  const int64_t isz = (int64_t)fs;  // set_command_point: left + action * int(size)
+  d.p_cmdx[gp] = (double)left + a0 * (double)isz;
+  d.p_cmdy[gp] = (double)top + a1 * (double)isz;
+  d.p_split[gp] = split;
+  d.p_eject[gp] = eject;
+}
+void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask) {
+  hipLaunchKernelGGL(k_policy_greedy, dim3(d.NP), dim3(64), 0, s, d, greedy_split, mask);
 }
 
 // synthetic bot population: random action in [0,1]^2 through set_command_point

@@ -151,6 +151,16 @@ int aigar_set_commands(aigar_handle *h, const double *cmd, int on_device);
  * set_command_point (bot.py:550-577) and splits/ejects with p_split/p_eject. */
 int aigar_policy_random(aigar_handle *h, double p_split, double p_eject, uint64_t seed);
 
+/* Model.takeBotActions for Greedy bots (bot.py:252-269 -> make_greedy_bot_move
+ * bot.py:579-633 -> set_command_point bot.py:550-577): sets the command of every
+ * alive player whose mask byte is non-zero (mask NULL: every player).
+ * greedy_split = ENABLE_GREEDY_SPLIT (networkParameters.py:17).  Random draws
+ * (fallback target, split dice) come from the Philox stream. */
+int aigar_policy_greedy(aigar_handle *h, int greedy_split, const uint8_t *mask, int on_device);
+/* Greedy bots' splitLikelihood (bot.py:93), [bots_per_arena] for one arena;
+ * NULL: derive them from the Philox key (the default). */
+int aigar_set_split_likelihood(aigar_handle *h, int arena, const int32_t *lh);
+
 /* n_ticks x Field.update() with the current commands (field.py:85-92). */
 int aigar_step(aigar_handle *h, int n_ticks);
 

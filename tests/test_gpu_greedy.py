@@ -1,0 +1,82 @@
+"""GPU: the device Greedy bot policy (k_policy_greedy) against the oracle's
+(pinned to the reference by test_oracle_greedy.py), and directly against the
+reference's own greedy commands where they do not depend on a random draw."""
+import os
+
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import Oracle, golden_state, make_config
+import parity
+from test_oracle_greedy import GREEDY, split_likelihoods
+
+pytestmark = pytest.mark.gpu
+_lib = pytest.importorskip("aigar_amd._lib")
+
+
+def commands(st):
+    pf, pi = np.asarray(st["players_f"]), np.asarray(st["players_i"])
+    return np.c_[pf[:, 0], pf[:, 1], pi[:, 2], pi[:, 3]].astype(np.float64)
+
+
+@pytest.mark.parametrize("bots,virus,gsplit,seed", [(16, False, False, 1), (48, True, True, 2), (200, True, True, 3)])
+def test_greedy_population_matches_oracle(bots, virus, gsplit, seed):
+    cfg = make_config(bots=bots, virus=virus, max_viruses=30 if virus else -1.0,
+                      channels=_abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY, extras=0x3)
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    g.reset(seed)
+    o.reset(seed)
+    for t in range(120):
+        g.policy_greedy(gsplit)
+        o.policy_greedy(gsplit)
+        cg, co = commands(g.get_state()), commands(o.get_state())
+        bad = np.argwhere(cg != co)
+        assert not len(bad), "tick %d bot %d: gpu %s oracle %s" % (t, bad[0][0], cg[bad[0][0]], co[bad[0][0]])
+        g.step(1)
+        o.step(1)
+        assert np.array_equal(g.events(), o.events()), "events differ at tick %d" % t
+    dif = parity.diff_states(g.get_state(), o.get_state())
+    assert not dif, dif
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("name,seed,gsplit", GREEDY)
+def test_greedy_matches_reference_commands_at_checkpoints(name, seed, gsplit, golden_dir):
+    """At every reference checkpoint state, the device's greedy command equals
+    the reference bot's for every bot whose move involved no random draw
+    (the MT- and Philox-mode oracles agree on exactly those)."""
+    z = np.load(os.path.join(golden_dir, name + ".npz"))
+    n = int(z["n_players"])
+    lh = split_likelihoods(seed, n)
+    cfg_mt = make_config(bots=n, field_size=int(z["size"]), virus=bool(z["virus_enabled"]),
+                         max_pellets=float(z["max_pellets"]), max_viruses=float(z["max_viruses"]),
+                         channels=int(z["obs_channels"]), extras=int(z["obs_extras"]), rng_mode=_abi.RNG_MT19937)
+    cfg_ph = parity.golden_config(z)
+    g, om, op = _lib.Stepper(cfg_ph), Oracle(cfg_mt), Oracle(cfg_ph)
+    for orc in (om, op):
+        orc.set_split_likelihood(lh)
+    g.set_split_likelihood(lh)
+    checked = 0
+    for ck in [0] + [int(t) for t in z["ck_ticks"] if int(t) < int(z["ticks"])]:
+        pre = "init" if ck == 0 else "ck%d" % ck
+        st_mt = golden_state(z, pre)
+        st_ph = parity.philox_dict(z, pre)
+        om.load_state(st_mt)
+        op.load_state(st_ph)
+        g.load_state(st_ph)
+        om.policy_greedy(gsplit)
+        op.policy_greedy(gsplit)
+        g.policy_greedy(gsplit)
+        ref = z["cmds"][ck]
+        cm, cp, cg = om.commands(), op.commands(), commands(g.get_state())
+        assert np.array_equal(cm, ref), "MT oracle vs reference at tick %d" % ck
+        det = np.all(cm == cp, axis=1)  # no random draw involved
+        assert np.array_equal(cg[det], ref[det]), "device vs reference at tick %d" % ck
+        assert np.array_equal(cg, cp), "device vs Philox oracle at tick %d" % ck
+        checked += int(det.sum())
+    if n > 1:  # (the lone C1 bot mostly sees no pellet and moves at random)
+        assert checked > 0
+    for x in (g, om, op):
+        x.close()
