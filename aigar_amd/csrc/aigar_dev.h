@@ -52,6 +52,7 @@ struct ArenaCtl {
   int peat;           // pellet buffer of this tick's eat phase (pcur when nothing was converted)
   int p_skip;         // the conversion rebuild was skipped this tick
   uint32_t dirty;     // DIRTY_*: a virus / blob died this tick (k_spawn_plan compacts)
+  int food_undone[3];  // cells that failed reservation round r (index r % 3)
   uint32_t pl_epoch;  // k_players look-back epoch / finished-tile ticket
   int pl_ticket;  // pellet rebuild: source counts snapshotted by the scan epilogue
   int pad1;

@@ -1444,6 +1444,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
   __shared__ uint8_t s_sel[4][PREP_CAND];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int gp = blockIdx.x * 4 + w;
+  if (gp < d.NP && gp % d.B == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP || !d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   if (KIND == 1 && d.ctl[a].n_blob == 0) return;  // no blobs: nothing to reserve (commit skips too)
@@ -1511,6 +1512,13 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
       if (lane == 0) {
         d.f_cnt[ci] = kOverflow;
         d.f_done[ci] = 0;
+        int wi = atomicAdd(&d.ctl[a].n_pend, 1);  // straight to the serial pass
+        if (wi < d.Wcap) {
+          d.work[(size_t)a * d.Wcap + wi] = (int)ci;
+          d.work2[(size_t)a * d.Wcap + wi] = (int)prio;
+        } else {
+          set_err(d, a, ERR_WORK_CAP);
+        }
       }
       const Span g = grid_span(q, 1, cols, F.shift());
       for (int by = g.by0; by <= g.by1; by++) {
@@ -1567,9 +1575,15 @@ __device__ void food_eat_loop(const Dev &d, const Food<KIND> &F, int a, size_t c
 template <int KIND>
 __global__ void k_food_commit(Dev d, int round, int last) {
   int gp = GTID;
-  if (gp >= d.NP || !d.p_alive[gp]) return;
+  if (gp >= d.NP) return;
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
-  if (KIND == 1 && d.ctl[a].n_blob == 0) return;
+  ArenaCtl &c = d.ctl[a];
+  // round r reads how many cells failed round r-1 (nothing left: skip), counts
+  // its own failures, and clears the counter round r+1 will use
+  if (round > 1 && c.food_undone[(round - 1) % 3] == 0) return;
+  if (p == 0) c.food_undone[(round + 1) % 3] = 0;
+  if (!d.p_alive[gp]) return;
+  if (KIND == 1 && c.n_blob == 0) return;
   Food<KIND> F(d, a);
   int n = d.p_ncells[gp];
   for (int k = 0; k < n; k++) {
@@ -1577,7 +1591,8 @@ __global__ void k_food_commit(Dev d, int round, int last) {
     if (d.f_done[ci]) continue;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
     int cnt = d.f_cnt[ci];
-    bool own = cnt != kOverflow;
+    if (cnt == kOverflow) continue;  // already in the serial work list (k_food_prep)
+    bool own = true;
     const int *lst = d.f_list + ci * FCAP;
     if (own) {
       uint64_t key = food_key(d.ctl[a].food_round + round, prio);
@@ -1586,7 +1601,7 @@ __global__ void k_food_commit(Dev d, int round, int last) {
     if (own) {
       food_eat_loop<KIND>(d, F, a, ci, prio, lst, cnt);
       d.f_done[ci] = 1;
-    } else if (!last && cnt != kOverflow) {
+    } else if (!last) {
       // reserve for the next round right away.  Safe without a separate pass: a
       // cell that still has to wait for a lower-priority neighbour made its
       // round-(r+1) reservation no later than this kernel, so the neighbour's
@@ -1594,7 +1609,8 @@ __global__ void k_food_commit(Dev d, int round, int last) {
       // a round-(r+1) key only loses a round (it re-reserves and wins next time).
       uint64_t key = food_key(d.ctl[a].food_round + round + 1, prio);
       for (int t = 0; t < cnt; t++) atomicMax((unsigned long long *)F.owner(lst[t]), (unsigned long long)key);
-    } else if (last) {
+      atomicAdd(&c.food_undone[round % 3], 1);
+    } else {
       int w = atomicAdd(&d.ctl[a].n_pend, 1);
       if (w < d.Wcap) {
         d.work[(size_t)a * d.Wcap + w] = (int)ci;
@@ -1605,46 +1621,117 @@ __global__ void k_food_commit(Dev d, int round, int last) {
     }
   }
 }
+// Cells the reservation rounds could not settle, in priority order (player,
+// list position), one wavefront per arena.  The sequential eat loop runs on
+// all lanes uniformly; each cell's candidates are gathered lane-parallel with
+// their state into LDS (within one cell's turn only that cell changes them).
+constexpr int FS_CAP = 512;
 template <int KIND>
-__global__ void k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
-  int a = blockIdx.x;
-  if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
+  __shared__ int64_t s_key[FS_CAP];
+  __shared__ int s_val[FS_CAP], s_srt[FS_CAP];
+  __shared__ double s_x[FS_CAP], s_y[FS_CAP], s_m[FS_CAP], s_r[FS_CAP];
+  const int a = blockIdx.x, lane = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
-  int nw = min(c.n_pend, d.Wcap);
-  c.n_pend = 0;
-  c.stat[2 + KIND] += nw;
-  c.food_round += rounds + 2;  // next phase's keys dominate every key written in this one
+  const int nw = min(c.n_pend, d.Wcap);
+  wave_fence();
+  if (lane == 0) {
+    c.n_pend = 0;
+    c.stat[2 + KIND] += nw;
+    c.food_round += rounds + 2;  // next phase's keys dominate every key written in this one
+  }
   if (nw == 0) return;
   Food<KIND> F(d, a);
   int *w = d.work + (size_t)a * d.Wcap;
   int *wp = d.work2 + (size_t)a * d.Wcap;
-  int64_t *ck = scr_k + (size_t)a * d.Wcap;
-  int *cv = scr_v + (size_t)a * d.Wcap;
-  for (int k = 0; k < nw; k++) ck[k] = wp[k];
-  isort_kv(ck, w, nw);  // priority order (player index, list position)
-  // the sorted priorities now sit in ck[0..nw); move them out of the scratch
-  int *prios = wp;
-  for (int k = 0; k < nw; k++) prios[k] = (int)ck[k];
+  if (nw <= FS_CAP) {  // priority order: rank sort in LDS (priorities are unique)
+    for (int k = lane; k < nw; k += 64) {
+      s_val[k] = w[k];
+      s_key[k] = wp[k];
+    }
+    wave_fence();
+    for (int k = lane; k < nw; k += 64) {
+      int64_t key = s_key[k];
+      int rk = 0;
+      for (int y = 0; y < nw; y++) rk += s_key[y] < key;
+      s_srt[rk] = k;
+    }
+    wave_fence();
+    for (int k = lane; k < nw; k += 64) {  // (w, wp are free now: write back sorted)
+      w[k] = s_val[s_srt[k]];
+      wp[k] = (int)s_key[s_srt[k]];
+    }
+  } else if (lane == 0) {
+    int64_t *ck = scr_k + (size_t)a * d.Wcap;
+    for (int k = 0; k < nw; k++) ck[k] = wp[k];
+    isort_kv(ck, w, nw);
+    for (int k = 0; k < nw; k++) wp[k] = (int)ck[k];
+  }
+  wave_fence();
+  const unsigned long long lt = (1ull << lane) - 1;
   for (int wi = 0; wi < nw; wi++) {
-    size_t ci = (size_t)w[wi];
-    double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci];
-    int64_t cseq = d.c_seq[ci];
-    Rect q = footprint(x, y, r, d.size);
+    const size_t ci = (size_t)w[wi];
+    const uint32_t prio = (uint32_t)wp[wi];
+    const double x = d.c_x[ci], y = d.c_y[ci];
+    double m = d.c_m[ci], r = d.c_r[ci];
+    const int64_t cseq = d.c_seq[ci];
+    const Rect q = footprint(x, y, r, d.size);
     int nc = 0;
-    grid_visit(F.start(), F.items(), d.cols, q, 1, [&](int j) {
-      if (!F.alive(j) || F.ej(j) == cseq) return;
-      if (!rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q)) return;
-      if (nc < d.Wcap) {
-        ck[nc] = F.seq(j);
-        cv[nc] = j;
-        nc++;
-      } else {
-        set_err(d, a, ERR_CAND_CAP);
+    wave_grid_for(F.start(), F.items(), d.cols, q, 1, [&](bool valid, int j) {
+      double fx = 0, fy = 0, fm = 0, fr = 0;
+      bool keep = valid && F.alive(j) && F.ej(j) != cseq;
+      if (keep) {
+        fx = F.x(j);
+        fy = F.y(j);
+        fm = F.m(j);
+        fr = KIND == 0 ? radius_of(fm) : F.r(j);
+        keep = rect_hit(footprint(fx, fy, fr, d.size), q);
       }
+      unsigned long long bal = __ballot(keep);
+      int slot = nc + __popcll(bal & lt);
+      if (keep && slot < FS_CAP) {
+        s_key[slot] = F.seq(j);
+        s_val[slot] = j;
+        s_x[slot] = fx;
+        s_y[slot] = fy;
+        s_m[slot] = fm;
+        s_r[slot] = fr;
+      }
+      nc += __popcll(bal);
     }, F.shift());
-    isort_kv(ck, cv, nc);
-    food_eat_loop<KIND>(d, F, a, ci, (uint32_t)prios[wi], cv, nc);
-    d.f_done[ci] = 1;
+    if (nc > FS_CAP) {
+      set_err(d, a, ERR_CAND_CAP);
+      nc = FS_CAP;
+    }
+    wave_fence();
+    for (int k = lane; k < nc; k += 64) {  // candidate order: creation sequence
+      int64_t key = s_key[k];
+      int rk = 0;
+      for (int y = 0; y < nc; y++) rk += s_key[y] < key;
+      s_srt[rk] = k;
+    }
+    wave_fence();
+    int eaten = 0;
+    for (int t = 0; t < nc; t++) {  // food_eat_loop, on the turn-start snapshot
+      const int k = s_srt[t];
+      const double fm = s_m[k];
+      if (!(overlap(x, y, m, r, s_x[k], s_y[k], fm, s_r[k]) && can_eat(m, fm))) continue;
+      if (lane == 0) {
+        ev_push(d, a, KIND == 0 ? PH_PELLET : PH_BLOB, ((uint64_t)prio << 16) | (uint64_t)t, KIND == 0 ? 6 : 7, cseq,
+                s_key[k]);
+        F.kill(s_val[k]);
+      }
+      m = grow_mass(m, fm);  // eatCell -> adjustCellSize -> grow (field.py:337-344)
+      r = radius_of(m);
+      eaten++;
+    }
+    if (lane == 0) {
+      d.c_m[ci] = m;
+      d.c_r[ci] = r;
+      d.f_done[ci] = 1;
+      if (KIND == 0 && eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
+    }
+    wave_fence();  // kills and the new mass are read by the next cell's gather
   }
 }
 
@@ -1722,11 +1809,14 @@ __device__ __forceinline__ void active_st(const Dev &d, size_t i, uint8_t v) {
 // stores, so program order alone orders them -- while the grid queries
 // (candidate gathering, re-activation after growth) are spread over the lanes.
 // Cross-lane data: the LDS candidate lists, the pending bitmap and c_active.
-constexpr int PP_LCAP = 1024;
+constexpr int PP_LCAP = 512;
 __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *scr_v) {
   extern __shared__ uint32_t pend[];  // pending-player bitmap (B bits)
+  // candidates of the current turn, with their state at turn start (only the
+  // turn's own cell changes them: what it eats dies, and it stops when eaten)
   __shared__ int64_t s_key[PP_LCAP];
   __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
+  __shared__ double s_x[PP_LCAP], s_y[PP_LCAP], s_m[PP_LCAP], s_r[PP_LCAP];
   const int a = blockIdx.x, lane = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int B = d.B, NW = (B + 31) / 32;
@@ -1772,12 +1862,23 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
       const Rect q0 = cell_rect(d, pc);
       int nc = 0;
       wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
-        bool keep = valid && (d.c_flags[e] & F_ALIVE) && (e % NP) != gp && rect_hit(cell_rect(d, e), q0);
+        double ex = 0, ey = 0, er = 0;
+        bool keep = valid && (d.c_flags[e] & F_ALIVE) && (e % NP) != gp;
+        if (keep) {
+          ex = d.c_x[e];
+          ey = d.c_y[e];
+          er = d.c_r[e];
+          keep = rect_hit(footprint(ex, ey, er, d.size), q0);
+        }
         unsigned long long bal = __ballot(keep);
         int slot = nc + __popcll(bal & lt);
         if (keep && slot < PP_LCAP) {
           s_key[slot] = d.c_seq[e];
           s_val[slot] = e;
+          s_x[slot] = ex;
+          s_y[slot] = ey;
+          s_m[slot] = d.c_m[e];
+          s_r[slot] = er;
         }
         nc += __popcll(bal);
       });
@@ -1790,35 +1891,45 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
         int64_t k = s_key[x];
         int rk = 0;
         for (int y = 0; y < nc; y++) rk += s_key[y] < k;
-        s_srt[rk] = s_val[x];
+        s_srt[rk] = x;
       }
       wave_fence();
+      const double px = d.c_x[pc], py = d.c_y[pc];
+      const int64_t pseq = d.c_seq[pc];
+      double pm = d.c_m[pc], pr = d.c_r[pc];
       for (int t = 0; t < nc; t++) {
-        const size_t o = (size_t)s_srt[t];
-        if (!(d.c_flags[o] & F_ALIVE)) continue;
-        if (!overlap(d.c_x[pc], d.c_y[pc], d.c_m[pc], d.c_r[pc], d.c_x[o], d.c_y[o], d.c_m[o], d.c_r[o])) continue;
+        const int k = s_srt[t];
+        const size_t o = (size_t)s_val[k];
+        const double ox = s_x[k], oy = s_y[k], om = s_m[k], orr = s_r[k];
+        if (!overlap(px, py, pm, pr, ox, oy, om, orr)) continue;
         size_t g, v;
-        const bool pc_eats = can_eat(d.c_m[pc], d.c_m[o]);
+        const bool pc_eats = can_eat(pm, om);
         if (pc_eats) {
           g = pc;
           v = o;
-        } else if (can_eat(d.c_m[o], d.c_m[pc])) {
+        } else if (can_eat(om, pm)) {
           g = o;
           v = pc;
         } else {
           continue;
         }
         // eatPlayerCell (field.py:346-348)
-        if (lane == 0) ev_push(d, a, PH_PP, order, 8, d.c_seq[g], d.c_seq[v]);
+        if (lane == 0) ev_push(d, a, PH_PP, order, 8, pc_eats ? pseq : s_key[k], pc_eats ? s_key[k] : pseq);
         order++;
-        double m = grow_mass(d.c_m[g], d.c_m[v]);
+        const double m = pc_eats ? grow_mass(pm, om) : grow_mass(om, pm);
+        const double mr = radius_of(m);
         d.c_m[g] = m;
-        d.c_r[g] = radius_of(m);
-        rmax = fmax(rmax, d.c_r[g]);
+        d.c_r[g] = mr;
+        if (pc_eats) {
+          pm = m;
+          pr = mr;
+        }
+        rmax = fmax(rmax, mr);
         remove_cell(d, a, v, order, lane == 0);
         // re-activate every later turn whose outcome the growth of g may change
         const int gpl = (int)(g % NP);
-        const double gx = d.c_x[g], gy = d.c_y[g], gm = d.c_m[g], gr = d.c_r[g];
+        const double gx = pc_eats ? px : ox, gy = pc_eats ? py : oy, gm = m, gr = mr;
+        wave_fence();  // (the removal above is read by the re-activation walk)
         wave_grid_for(st, it, d.cols, cell_rect(d, g), expand_for(rmax), [&](bool valid, int e) {
           if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
           if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;

@@ -6,8 +6,8 @@ drivers keep working:
   Field   src/model/field.py     (addPlayer, initialize, reset, update, FOV/list getters)
   Player  src/model/player.py    (setCommands, getCells, getFovPos/Size, getTotalMass, ...)
   Cell    src/model/cell.py      (read-only view: getters and predicates)
-  Bot     src/model/bot.py       (Random / NN bots: makeMove, set_command_point,
-                                  getStateRepresentation)
+  Bot     src/model/bot.py       (Greedy / Random / NN bots: makeMove,
+                                  set_command_point, getStateRepresentation)
   Model   src/model/model.py     (createPlayer, createBot, initialize, resetModel, update)
 
 The world lives on the GPU.  `Field.update()` pushes every player's command and
@@ -22,9 +22,11 @@ Differences a caller can see:
  - canonical order: every set-derived list (FOV queries) is ordered by creation
    sequence instead of CPython object addresses;
  - randomness comes from the device's Philox stream (seeded by `seed`), not from
-   numpy's global MT19937 (colours are not modelled);
- - Greedy bots are not available yet (device greedy policy is the next item,
-   SURVEY.md §8f).
+   numpy's global MT19937 (colours are not modelled); Random bots still draw
+   from numpy like the reference;
+ - Greedy bots move on the device, all in one launch per tick
+   (`Model.takeBotActions`); their splitLikelihood comes from the Philox stream
+   unless set with `Field.set_split_likelihood`.
 """
 import math
 
@@ -414,6 +416,27 @@ class Field:
             self._cache["obs"] = self.stepper.observe()
         return self._cache["obs"]
 
+    def _greedy_moves(self, mask, greedy_split):
+        """make_greedy_bot_move + set_command_point on the device for the masked players;
+        the resulting commands replace theirs in the host command buffer."""
+        self.stepper.set_commands(self._cmd)  # keep the other players' commands
+        self.stepper.policy_greedy(greedy_split, mask)
+        st = self.stepper.get_state()
+        pf, pi = np.asarray(st["players_f"]), np.asarray(st["players_i"])
+        sel = np.asarray(mask, bool)
+        self._cmd[sel, 0], self._cmd[sel, 1] = pf[sel, 0], pf[sel, 1]
+        self._cmd[sel, 2], self._cmd[sel, 3] = pi[sel, 2], pi[sel, 3]
+        for p in self.players:
+            if sel[p.index]:
+                p.commandPoint = [float(self._cmd[p.index, 0]), float(self._cmd[p.index, 1])]
+                p.doSplit, p.doEject = bool(self._cmd[p.index, 2]), bool(self._cmd[p.index, 3])
+        self._cache.pop("state", None)
+        self._cache.pop("views", None)
+
+    def set_split_likelihood(self, lh):
+        """Greedy bots' splitLikelihood per player (bot.py:93); None: Philox-derived."""
+        self.stepper.set_split_likelihood(lh)
+
     def _set_actions(self, bots):
         cur = np.zeros((len(self.players), 4))
         prev = np.zeros((len(self.players), 4))
@@ -426,14 +449,14 @@ class Field:
 
 
 class Bot:
-    """bot.py:23-710, Random and NN bot types.  NN bots get their actions from
-    the caller (`currentAction` / `set_command_point`), as the reference's
-    learners supply them."""
+    """bot.py:23-710.  Greedy bots move on the device (k_policy_greedy, batched
+    over all Greedy bots by Model.takeBotActions); Random bots draw from numpy
+    like the reference; NN bots get their actions from the caller
+    (`currentAction` / `set_command_point`), as the reference's learners supply them."""
 
     def __init__(self, player, field, bot_type, learningAlg=None, parameters=None):
-        if bot_type not in ("Random", "NN"):
-            raise NotImplementedError("bot type %r: only Random and NN bots run on the device stepper so far"
-                                      % bot_type)
+        if bot_type not in ("Greedy", "Random", "NN"):
+            raise NotImplementedError("bot type %r is not one of Greedy, Random, NN" % bot_type)
         self.player, self.field, self.type = player, field, bot_type
         self.learningAlg = learningAlg
         self.parameters = parameters
@@ -470,6 +493,11 @@ class Bot:
     def makeMove(self):  # bot.py:252-269
         self.totalMasses.append(self.player.getTotalMass())
         if not self.player.getIsAlive():
+            return
+        if self.type == "Greedy":  # one bot at a time (Model.takeBotActions batches them)
+            mask = np.zeros(len(self.field.players), np.uint8)
+            mask[self.player.index] = 1
+            self.field._greedy_moves(mask, self._param("ENABLE_GREEDY_SPLIT", False))
             return
         if self.type == "Random":
             self.make_random_bot_move()
@@ -550,9 +578,17 @@ class Model:
         self.field.reset()
         self.counter = 0
 
-    def takeBotActions(self):
+    def takeBotActions(self):  # model.py:113-115
+        greedy = [b for b in self.bots if b.type == "Greedy"]
+        if greedy:  # every Greedy bot in one device launch (their moves are independent)
+            mask = np.zeros(len(self.players), np.uint8)
+            for b in greedy:
+                b.totalMasses.append(b.player.getTotalMass())
+                mask[b.player.index] = 1
+            self.field._greedy_moves(mask, bool(getattr(self.parameters, "ENABLE_GREEDY_SPLIT", False)))
         for bot in self.bots:
-            bot.makeMove()
+            if bot.type != "Greedy":
+                bot.makeMove()
 
     def resetBots(self):
         for bot in self.bots:

@@ -77,7 +77,7 @@ def pmc_traffic(kernel_prefix, workload):
     return None, None
 
 
-def cpu_baseline(name, budget_s=12.0, seed=1):
+def cpu_baseline(name, budget_s=12.0, seed=1, policy="random"):
     """Single-thread C oracle (CPU port of the reference) on the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle  # test infrastructure: the checker / CPU baseline only
@@ -101,13 +101,19 @@ def cpu_baseline(name, budget_s=12.0, seed=1):
         cmd[:, 3] = rng.random(bots) < pe
         return cmd
 
+    def act():
+        if policy == "greedy":
+            o.policy_greedy(True)
+        else:
+            o.set_commands(commands())
+
     for _ in range(2):  # warm-up
-        o.set_commands(commands())
+        act()
         o.step(1)
         o.observe()
     n, t0 = 0, time.perf_counter()
     while True:
-        o.set_commands(commands())
+        act()
         o.step(1)
         o.observe()
         n += 1
@@ -116,8 +122,8 @@ def cpu_baseline(name, budget_s=12.0, seed=1):
     dt = time.perf_counter() - t0
     o.close()
     return {"value": bots * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%s world, %d steps (policy + Field.update + obs for all %d bots) after 2 warm-up steps, "
-                      "oracle/oracle.c single thread, %.1f s" % (name.upper(), n, bots, dt)}
+            "sample": "%s world, %d steps (%s policy + Field.update + obs for all %d bots) after 2 warm-up "
+                      "steps, oracle/oracle.c single thread, %.1f s" % (name.upper(), n, policy, bots, dt)}
 
 
 def main():
@@ -129,6 +135,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--policy", default="random", choices=["random", "greedy"],
+                    help="synthetic population: Philox random actions, or the reference's Greedy bots "
+                         "(bot.py:579-633, ENABLE_GREEDY_SPLIT) on the device")
     args = ap.parse_args()
 
     import torch
@@ -149,7 +158,10 @@ def main():
     stp.reset(replicas.rank_seed(args.seed, rank))
 
     def one_step():
-        stp.policy_random(ps, pe, args.seed)
+        if args.policy == "greedy":
+            stp.policy_greedy(True)
+        else:
+            stp.policy_random(ps, pe, args.seed)
         stp.step(1)
         stp.observe(obs)
 
@@ -202,11 +214,15 @@ def main():
         "metric": "env-steps/sec at 4096 bots x 100k pellets; 1/2/4/8 MI355X scaling",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic (Philox bot population, random-action policy)",
-        "config": {"workload": "%s: %s%d bots, %d pellets, %s viruses, split p=%g, eject p=%g, field %d, "
-                               "obs %d floats/bot" % (name.upper(), "%d arenas x " % arenas if arenas > 1 else "",
-                                                      bots // arenas, int(pellets), "1152" if virus else "no", ps,
-                                                      pe, field, stp.obs_len),
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (Philox bot population, %s)" % ("reference Greedy bots on the device" if args.policy == "greedy"
+                                                           else "random-action policy"),
+        "config": {"workload": "%s: %s%d bots, %d pellets, %s viruses, %s, field %d, obs %d floats/bot" % (
+            name.upper(), "%d arenas x " % arenas if arenas > 1 else "", bots // arenas, int(pellets),
+            "1152" if virus else "no",
+            "greedy bots with ENABLE_GREEDY_SPLIT" if args.policy == "greedy" else "split p=%g, eject p=%g" % (ps, pe),
+            field, stp.obs_len),
+                   "policy": args.policy,
                    "parallelism": "replicas%d" % world if world > 1 else "single-gpu"},
         "roofline": roofline,
         "breakdown_ms_per_step": {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
@@ -217,7 +233,7 @@ def main():
                                            if k != "ticks"}},
     }
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget, policy=args.policy)
     if rank == 0:
         print(json.dumps(out), flush=True)
     stp.close()

@@ -105,7 +105,7 @@ def test_unsupported_paths_fail_loudly():
     pl = M.Player("x")
     f.addPlayer(pl)
     with pytest.raises(NotImplementedError):
-        M.Bot(pl, f, "Greedy")
+        M.Bot(pl, f, "Smart")
 
 
 def test_cell_view_predicates():

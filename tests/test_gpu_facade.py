@@ -94,3 +94,27 @@ def test_model_update_matches_oracle_and_getters():
     orc.close()
     model.resetModel()
     assert model.counter == 0 and field.getWidth() == 260
+
+
+def test_greedy_model_matches_oracle_greedy():
+    """Model with Greedy bots: the facade's batched device moves equal the oracle's greedy policy."""
+    params = reference_like_parameters(virus=True, split=True, eject=False, n_bots=24)
+    params.ENABLE_GREEDY_SPLIT = True
+    model = M.Model(False, False, params, seed=5, field_size=400, max_viruses=10)
+    for _ in range(24):
+        model.createBot("Greedy")
+    model.initialize()
+    field = model.getField()
+    orc = Oracle(field._config())
+    orc.reset(5)
+    for t in range(50):
+        model.takeBotActions()
+        orc.policy_greedy(True)
+        cmd = field._cmd.copy()
+        assert np.array_equal(cmd, orc.commands()), "tick %d" % t
+        for b in model.getBots():  # the reference objects see the same commands
+            assert b.getPlayer().getCommandPoint() == [cmd[b.player.index, 0], cmd[b.player.index, 1]]
+        field.update()
+        orc.step(1)
+        assert not parity.diff_states(field._snapshot(), orc.get_state())
+    orc.close()
