@@ -49,7 +49,7 @@ struct aigar_handle {
   hipStream_t stream = nullptr;
   bool own_stream = true;
   uint32_t obs_calls = 0;
-  int rounds = 4;  // reservation rounds before the serial fallback; empty rounds exit at once
+  int rounds = 2;  // reservation rounds before the serial fallback; empty rounds exit at once
                    // (tools/micro/exp_rounds.sh, greedy_rounds.sh)
   int64_t *scr_k = nullptr;
   int *scr_v = nullptr;
