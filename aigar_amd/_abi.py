@@ -22,6 +22,18 @@ EV_CELL_EAT_PELLET, EV_CELL_EAT_BLOB, EV_CELL_EAT_CELL, EV_PLAYER_DEATH, EV_RESP
 FLAG_EVENTS = 0x1
 
 
+class RewardParams(C.Structure):
+    """aigar_reward_params (include/aigar.h); defaults of networkParameters.py:50,69-72."""
+    _fields_ = [("mass_as_reward", C.c_int32), ("pad", C.c_int32), ("reward_term", C.c_double),
+                ("death_term", C.c_double), ("death_factor", C.c_double), ("reward_scale", C.c_double)]
+
+    @classmethod
+    def from_parameters(cls, p=None):
+        g = (lambda n, dflt: getattr(p, n, dflt)) if p is not None else (lambda n, dflt: dflt)
+        return cls(int(bool(g("MASS_AS_REWARD", False))), 0, float(g("REWARD_TERM", 0)), float(g("DEATH_TERM", -40)),
+                   float(g("DEATH_FACTOR", 1.5)), float(g("REWARD_SCALE", 2)))
+
+
 class Config(C.Structure):
     _fields_ = [
         ("n_arenas", C.c_int32), ("bots_per_arena", C.c_int32), ("field_size", C.c_int32),

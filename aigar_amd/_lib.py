@@ -73,6 +73,8 @@ def load(build_if_missing=False):
         "aigar_selftest_pow": [dp, dp, dp, i32],
         "aigar_counters": [vp, i32, C.POINTER(C.c_int64), i32],
         "aigar_policy_greedy": [vp, i32, vp, i32],
+        "aigar_apply_actions": [vp, vp, i32, i32, i32, i32, i32],
+        "aigar_rewards": [vp, vp, C.POINTER(_abi.RewardParams), i32, i32],
         "aigar_set_split_likelihood": [vp, i32, C.POINTER(C.c_int32)],
     }
     for name, args in sig.items():
@@ -143,6 +145,24 @@ class Stepper:
             mask = np.ascontiguousarray(mask, np.uint8).reshape(self.NP)
         p, dev = _ptr(mask)
         self._chk(self.L.aigar_policy_greedy(self.h, int(bool(greedy_split)), p, dev))
+
+    def apply_actions(self, act, enable_split=True, skipping=False, record=True):
+        """Learner actions act[NP, n] (n = 2..4, numpy or device tensor) through set_command_point."""
+        if isinstance(act, np.ndarray):
+            act = np.ascontiguousarray(act, np.float64).reshape(self.NP, -1)
+        n = int(act.shape[1])
+        p, dev = _ptr(act)
+        self._chk(self.L.aigar_apply_actions(self.h, p, n, int(bool(enable_split)), int(bool(skipping)),
+                                             int(bool(record)), dev))
+
+    def rewards(self, params=None, update_last=True, out=None):
+        """Bot.getReward for every player (NaN where the reference has None)."""
+        prm = params if isinstance(params, _abi.RewardParams) else _abi.RewardParams.from_parameters(params)
+        if out is None:
+            out = np.zeros(self.NP, np.float64)
+        p, dev = _ptr(out)
+        self._chk(self.L.aigar_rewards(self.h, p, C.byref(prm), int(bool(update_last)), dev))
+        return out
 
     def set_split_likelihood(self, lh, arena=0):
         if lh is None:

@@ -89,7 +89,8 @@ struct Dev {
   int *p_alive, *p_respawn, *p_ncells, *p_split, *p_eject, *p_pend;
   double *p_cmdx, *p_cmdy;
   double *p_fx, *p_fy, *p_fs, *p_mass;
-  int *p_split_lh;  // Greedy bots' splitLikelihood (bot.py:93); <= 0: derived from the Philox key  // FOV cache (getFovPos/getFovSize/getTotalMass at tick end)
+  int *p_split_lh;
+  double *o_last_mass;  // NN bots' lastMass (bot.py:229-230); NaN = None  // Greedy bots' splitLikelihood (bot.py:93); <= 0: derived from the Philox key  // FOV cache (getFovPos/getFovSize/getTotalMass at tick end)
   uint8_t *p_list;  // [16][NP]
   int *p_newc, *p_newb, *p_seqoff, *p_bloboff;
   // cells [16*NP]

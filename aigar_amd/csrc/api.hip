@@ -21,6 +21,9 @@ void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t 
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
 void launch_player_stats(const Dev &d, hipStream_t s, double *out);
 void launch_player_fov(const Dev &d, hipStream_t s);
+void launch_apply_actions(const Dev &d, hipStream_t s, const double *act, int n_act, int enable_split, int skipping,
+                          int record);
+void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last);
 void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask);
 void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd);
 }  // namespace aigar
@@ -231,6 +234,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(ticket, int, 4);
   AL(ob_used, unsigned long long, 1);
   AL(p_split_lh, int, NP);
+  AL(o_last_mass, double, NP);
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
 #undef AL
@@ -290,6 +294,8 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   const size_t NP = d.NP, GG = (size_t)d.G * d.G, A = d.A, H1 = (size_t)d.H + 1;
   hipLaunchKernelGGL(k_fill_d, dim3((NP + 255) / 256), dim3(256), 0, h->stream, d.p_cmdx, NP, -1.0);
   hipLaunchKernelGGL(k_fill_d, dim3((NP + 255) / 256), dim3(256), 0, h->stream, d.p_cmdy, NP, -1.0);
+  hipLaunchKernelGGL(k_fill_d, dim3((NP + 255) / 256), dim3(256), 0, h->stream, d.o_last_mass, NP,
+                     __builtin_nan(""));  // NN bots' lastMass = None (bot.py:125-130)
   HIPCHK(hipMemsetAsync(d.cstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.vstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.bstart, 0, sizeof(int) * A * H1, h->stream));
@@ -772,6 +778,8 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   HIPCHK(hipMemcpyAsync(d.ctl + arena, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
   // bot-side observation history restarts (NN bot reset, bot.py:151-158)
   HIPCHK(hipMemsetAsync(d.o_lastfov + p0, 0, 8 * B, h->stream));
+  hipLaunchKernelGGL(k_fill_d, dim3((B + 255) / 256), dim3(256), 0, h->stream, d.o_last_mass + p0, (size_t)B,
+                     __builtin_nan(""));
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
     HIPCHK(hipMemsetAsync(p + p0 * GG, 0, 8 * B * GG, h->stream));
   launch_player_fov(d, h->stream);  // FOV cache of the loaded players
@@ -807,6 +815,36 @@ extern "C" int aigar_set_split_likelihood(aigar_handle *h, int arena, const int3
     HIPCHK(hipMemcpyAsync(dst, lh, sizeof(int) * h->d.B, hipMemcpyHostToDevice, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int aigar_apply_actions(aigar_handle *h, const double *act, int n_act, int enable_split, int skipping,
+                                   int record, int on_device) {
+  if (!h || !act) return fail("null argument");
+  if (n_act < 2 || n_act > 4) return fail("apply_actions: n_act must be 2, 3 or 4");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const double *src = act;
+  if (!on_device) {
+    HIPCHK(hipMemcpyAsync(h->d_cmd, act, sizeof(double) * n_act * h->d.NP, hipMemcpyHostToDevice, h->stream));
+    src = h->d_cmd;
+  }
+  launch_apply_actions(h->d, h->stream, src, n_act, enable_split, skipping, record);
+  HIPCHK(hipGetLastError());
+  if (!on_device) HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int aigar_rewards(aigar_handle *h, double *out, const aigar_reward_params *p, int update_last,
+                             int on_device) {
+  if (!h || !out || !p) return fail("null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  double *dst = on_device ? out : h->d_stats;
+  launch_rewards(h->d, h->stream, dst, *p, update_last);
+  HIPCHK(hipGetLastError());
+  if (!on_device) {
+    HIPCHK(hipMemcpyAsync(out, h->d_stats, sizeof(double) * h->d.NP, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
   return 0;
 }
 

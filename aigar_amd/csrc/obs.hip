@@ -527,6 +527,64 @@ __global__ void k_policy_random(Dev d, double p_split, double p_eject, uint64_t 
   d.p_eject[gp] = u01(u[3]) < p_eject;
 }
 
+// set_command_point (bot.py:550-577) for external actions act[NP][n_act]
+// (n_act 2, 3 or 4); during skipped frames split/eject are dropped (bot.py:266-267).
+// record: updateValues (bot.py:180-193) -- lastAction <- currentAction <- act.
+__global__ void k_apply_actions(Dev d, const double *act, int n_act, int enable_split, int skipping, int record) {
+  int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;  // makeMove: dead players do not move
+  const double *ac = act + (size_t)gp * n_act;
+  const double a0 = ac[0], a1 = ac[1];
+  int split = 0, eject = 0;
+  if (!skipping && n_act == 4) {
+    split = ac[2] > 0.5;
+    eject = ac[3] > 0.5;
+  } else if (!skipping && n_act == 3 && enable_split) {
+    split = ac[2] > 0.5;
+  }
+  const int64_t x = (int64_t)d.p_fx[gp], y = (int64_t)d.p_fy[gp];
+  const double fs = d.p_fs[gp];
+  const int64_t left = x - (int64_t)(fs / 2), top = y - (int64_t)(fs / 2), size = (int64_t)fs;
+  d.p_cmdx[gp] = (double)left + a0 * (double)size;
+  d.p_cmdy[gp] = (double)top + a1 * (double)size;
+  d.p_split[gp] = split;
+  d.p_eject[gp] = eject;
+  if (record)
+    for (int k = 0; k < 4; k++) {
+      d.o_act_prev[(size_t)gp * 4 + k] = d.o_act_cur[(size_t)gp * 4 + k];
+      d.o_act_cur[(size_t)gp * 4 + k] = k < n_act ? ac[k] : 0.0;
+    }
+}
+void launch_apply_actions(const Dev &d, hipStream_t s, const double *act, int n_act, int enable_split, int skipping,
+                          int record) {
+  hipLaunchKernelGGL(k_apply_actions, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, act, n_act, enable_split,
+                     skipping, record);
+}
+
+// Bot.getReward (bot.py:654-667) for every player; NaN where the reference
+// returns None (no lastMass yet).  update_last: the end of move_NN on a
+// decision frame (bot.py:229-230) -- lastMass <- total mass of live players.
+__global__ void k_rewards(Dev d, double *out, aigar_reward_params prm, int update_last) {
+  int gp = GTID;
+  if (gp >= d.NP) return;
+  const bool alive = d.p_alive[gp];
+  const double mass = alive ? d.p_mass[gp] : 0.0, last = d.o_last_mass[gp];
+  double r;
+  if (prm.mass_as_reward) {
+    r = alive ? mass - prm.reward_term : prm.death_term - prm.reward_term;
+  } else if (isnan(last)) {
+    r = __builtin_nan("");
+  } else {
+    double rw = alive ? mass - last : -1 * last * prm.death_factor + prm.death_term;
+    r = rw * prm.reward_scale - prm.reward_term;
+  }
+  out[gp] = r;
+  if (update_last && alive) d.o_last_mass[gp] = mass;
+}
+void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last) {
+  hipLaunchKernelGGL(k_rewards, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, out, p, update_last);
+}
+
 __global__ void k_player_stats(Dev d, double *out) {
   int gp = GTID;
   if (gp >= d.NP) return;

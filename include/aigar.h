@@ -161,6 +161,25 @@ int aigar_policy_greedy(aigar_handle *h, int greedy_split, const uint8_t *mask, 
  * NULL: derive them from the Philox key (the default). */
 int aigar_set_split_likelihood(aigar_handle *h, int arena, const int32_t *lh);
 
+/* External (learner) actions for every player: act[A*B][n_act], n_act = 2, 3 or 4,
+ * mapped through set_command_point (bot.py:550-577).  skipping: a frame-skip
+ * frame, split/eject dropped (bot.py:266-267); record: a decision frame, the
+ * observation's last / second-last action extras advance (bot.py:180-193). */
+int aigar_apply_actions(aigar_handle *h, const double *act, int n_act, int enable_split, int skipping, int record,
+                        int on_device);
+
+/* Bot.getReward (bot.py:654-667) for every player into out[A*B] (NaN = None);
+ * update_last: lastMass <- total mass for live players (end of move_NN). */
+typedef struct aigar_reward_params {
+  int32_t mass_as_reward;  /* MASS_AS_REWARD (networkParameters.py:50) */
+  int32_t pad;
+  double reward_term;      /* REWARD_TERM  */
+  double death_term;       /* DEATH_TERM   */
+  double death_factor;     /* DEATH_FACTOR */
+  double reward_scale;     /* REWARD_SCALE */
+} aigar_reward_params;
+int aigar_rewards(aigar_handle *h, double *out, const aigar_reward_params *p, int update_last, int on_device);
+
 /* n_ticks x Field.update() with the current commands (field.py:85-92). */
 int aigar_step(aigar_handle *h, int n_ticks);
 

@@ -36,11 +36,13 @@ def test_library_exports_every_declared_symbol():
 
 def test_struct_layouts_match_header():
     # sizes of the ctypes mirrors vs a C compile of the header
-    src = '#include "%s"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%%zu %%zu %%zu\\n", ' \
-          'sizeof(aigar_config), sizeof(aigar_state), offsetof(aigar_state, players_f));return 0;}' % HEADER
+    src = '#include "%s"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%%zu %%zu %%zu %%zu\\n", ' \
+          'sizeof(aigar_config), sizeof(aigar_state), offsetof(aigar_state, players_f), ' \
+          'sizeof(aigar_reward_params));return 0;}' % HEADER
     exe = "/tmp/aigar_hdr_check"
     subprocess.run(["gcc", "-x", "c", "-", "-o", exe], input=src.encode(), check=True)
-    cfg, st, off = map(int, subprocess.check_output([exe]).split())
+    cfg, st, off, rp = map(int, subprocess.check_output([exe]).split())
+    assert rp == C.sizeof(_abi.RewardParams)
     assert cfg == C.sizeof(_abi.Config)
     assert st == C.sizeof(_abi.State)
     assert off == _abi.State.players_f.offset
