@@ -142,10 +142,18 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool 
 
 template <typename OutT>
 __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch) {
-  __shared__ int64_t p_seq[OBS_PCAP];
+  // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
+  // masks in creation order (no indirection in the per-square sums)
+  __shared__ union {
+    int64_t seq;
+    double m;
+  } p_sx[OBS_PCAP];
   __shared__ double p_m[OBS_PCAP];
   __shared__ uint32_t p_mask[OBS_PCAP];
-  __shared__ int p_perm[OBS_PCAP];
+  __shared__ union {
+    int perm;
+    uint32_t mask;
+  } p_px[OBS_PCAP];
   __shared__ double c_mass[OBS_CCAP];
   __shared__ uint32_t c_mask[OBS_CCAP];
   __shared__ uint8_t c_own[OBS_CCAP];
@@ -168,6 +176,20 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   const double lim = fs - 1;
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
   const ArenaCtl &ctl = d.ctl[a];
+  // last-frame history grids: independent of the queries, fetched up front
+  // (first two squares of each lane; larger grids read the rest in the loop)
+  double h_slf[2] = {0, 0}, h_elf[2] = {0, 0};
+  {
+    const bool pslf = d.obs_ch & AIGAR_OBS_SELF_LF, pelf = d.obs_ch & AIGAR_OBS_ENEMY_LF;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int t = lane + 64 * j;
+      if (t < GG) {
+        if (pslf) h_slf[j] = d.o_self_lf[(size_t)gp * GG + t];
+        if (pelf) h_elf[j] = d.o_en_lf[(size_t)gp * GG + t];
+      }
+    }
+  }
 
   // ---- getPelletsInFov / getEnemyPlayerCellsInFov / getVirusesInFov
   // (field.py:434-456) as ONE walk: every grid row the FOV touches (pellet,
@@ -224,7 +246,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
       list_append(Cand{ok && kd == 2, sq, m, r, msk, 0}, VLx, capV, nv);
     });
   };
-  ObjList PL{p_seq, p_m, nullptr, p_mask, nullptr, p_perm};
+  ObjList PL{&p_sx[0].seq, p_m, nullptr, p_mask, nullptr, &p_px[0].perm};
   ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
   ObjList VL{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
   int np, nc, nv;
@@ -264,11 +286,42 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   }
   wave_fence();  // lists written by all lanes -> read by all lanes
   // rank pellets by creation sequence (the sum order of the reference)
-  for (int i = lane; i < np; i += 64) {
-    int64_t sq = PL.seq[i];
-    int rk = 0;
-    for (int j = 0; j < np; j++) rk += (PL.seq[j] < sq);
-    PL.perm[rk] = i;
+  const bool in_lds = PL.seq == &p_sx[0].seq;  // (else the list overflowed into the global pool)
+  const double *sm = nullptr;
+  const uint32_t *smk = nullptr;
+  if (in_lds) {  // np <= OBS_PCAP = 4 x 64: keep (rank, m, mask) in registers, then store in order
+    int rk4[OBS_PCAP / 64];
+    double m4[OBS_PCAP / 64];
+    uint32_t k4[OBS_PCAP / 64];
+#pragma unroll
+    for (int j = 0; j < OBS_PCAP / 64; j++) {
+      const int i = lane + 64 * j;
+      rk4[j] = -1;
+      if (i < np) {
+        int64_t sq = p_sx[i].seq;
+        int rk = 0;
+        for (int q = 0; q < np; q++) rk += (p_sx[q].seq < sq);
+        rk4[j] = rk;
+        m4[j] = p_m[i];
+        k4[j] = p_mask[i];
+      }
+    }
+    wave_fence();
+#pragma unroll
+    for (int j = 0; j < OBS_PCAP / 64; j++)
+      if (rk4[j] >= 0) {
+        p_sx[rk4[j]].m = m4[j];
+        p_px[rk4[j]].mask = k4[j];
+      }
+    sm = &p_sx[0].m;
+    smk = &p_px[0].mask;
+  } else {
+    for (int i = lane; i < np; i += 64) {
+      int64_t sq = PL.seq[i];
+      int rk = 0;
+      for (int j = 0; j < np; j++) rk += (PL.seq[j] < sq);
+      PL.perm[rk] = i;
+    }
   }
   wave_fence();
 
@@ -302,11 +355,19 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
     if (within && ix < 16) {
       double s = 0;
       bool anyp = false;
-      for (int k = 0; k < np; k++) {
-        int e = PL.perm[k];
-        if ((PL.mask[e] & need) == need) {
-          s += PL.m[e];
-          anyp = true;
+      if (in_lds) {
+        for (int k = 0; k < np; k++)
+          if ((smk[k] & need) == need) {
+            s += sm[k];
+            anyp = true;
+          }
+      } else {
+        for (int k = 0; k < np; k++) {
+          int e = PL.perm[k];
+          if ((PL.mask[e] & need) == need) {
+            s += PL.m[e];
+            anyp = true;
+          }
         }
       }
       if (anyp) vp = s;
@@ -351,7 +412,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
       sslf[t] = slf[t];
     }
     if (o_slf >= 0) {
-      row[o_slf + t] = (OutT)slf[t];
+      row[o_slf + t] = (OutT)(t < 64 ? h_slf[0] : (t < 128 ? h_slf[1] : slf[t]));
       slf[t] = vs;
     }
     if (o_eslf >= 0) {
@@ -359,7 +420,7 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
       eslf[t] = elf[t];
     }
     if (o_elf >= 0) {
-      row[o_elf + t] = (OutT)elf[t];
+      row[o_elf + t] = (OutT)(t < 64 ? h_elf[0] : (t < 128 ? h_elf[1] : elf[t]));
       elf[t] = ve;
     }
   }
