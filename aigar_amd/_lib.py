@@ -11,7 +11,7 @@ import numpy as np
 from . import _abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(HERE, "libaigar_hip.so")
+SO_PATH = os.environ.get("AIGAR_SO") or os.path.join(HERE, "libaigar_hip.so")  # (AIGAR_SO: diagnostics builds)
 
 _lib = None
 

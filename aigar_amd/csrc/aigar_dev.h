@@ -78,6 +78,7 @@ struct Dev {
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
   double pow_n032[17];  // pow_cr(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)
+  int cshift_c;  // player-cell grid: smallest shift with <= 4096 cells (k_cgrid_count / k_cgrid_scatter)
   int Pcap, Ecap, Vcap, Wcap, EVcap;
   int virus_enabled;
   double max_pellets, max_viruses;
@@ -128,6 +129,7 @@ struct Dev {
   int *vcnt, *vstart, *vitems, *v_rank;
   // cell grid
   int *ccnt, *cstart, *citems, *c_rank;
+  int *cgcnt;  // [A][2][4100] coarse cell-grid counts (<= 4096 cells), by tick parity
   // occupancy bitmap of the player hash [A][ceil(H/64)]
   unsigned long long *occ;
   int occ_words;

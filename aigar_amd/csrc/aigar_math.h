@@ -23,6 +23,23 @@
 
 namespace aigar_math {
 
+// fmod(a, b) for a >= 0, b > 0, a / b < 2^50 (bucket and grid-square offsets),
+// exactly, without the long fmod routine: q = trunc(a * inv_b) is within one
+// of floor(a / b); when q is right, a - q*b is the exact remainder (always
+// representable) and the single-rounding fma returns it unchanged; a q one too
+// large (small too) shows as r < 0 (r >= b) and the fma is redone with q -/+ 1.
+// Returns +0 for a zero remainder, as Python's float % does for b > 0.
+AIGAR_HD double mod_pos(double a, double b, double inv_b) {
+  double q = trunc(a * inv_b);
+  double r = fma(-q, b, a);
+  if (r < 0) {
+    r = fma(-(q - 1), b, a);
+  } else if (r >= b) {
+    r = fma(-(q + 1), b, a);
+  }
+  return r == 0 ? 0.0 : r;
+}
+
 struct dd {
   double hi, lo;
 };

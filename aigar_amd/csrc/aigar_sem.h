@@ -161,8 +161,11 @@ struct Rect {
 };
 AIGAR_D Rect footprint(double px, double py, double rad, int size) {
   double cl = py_max(0.0, px - rad), ct = py_max(0.0, py - rad);
-  long bl = (long)(cl - py_mod(cl, (double)kBucket)), bt = (long)(ct - py_mod(ct, (double)kBucket));
-  long lx = (long)py_min((double)size, px + rad + 1), ly = (long)py_min((double)size, py + rad + 1);
+  // (cl, ct >= 0: py_mod by the exact multiply + fma remainder, aigar_math::mod_pos)
+  // (32-bit integers: coordinates are bounded by the field size)
+  int bl = (int)(cl - aigar_math::mod_pos(cl, (double)kBucket, 1.0 / kBucket)),
+      bt = (int)(ct - aigar_math::mod_pos(ct, (double)kBucket, 1.0 / kBucket));
+  int lx = (int)py_min((double)size, px + rad + 1), ly = (int)py_min((double)size, py + rad + 1);
   Rect r;
   r.x0 = (int)(bl / kBucket);
   r.y0 = (int)(bt / kBucket);

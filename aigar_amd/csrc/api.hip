@@ -184,6 +184,9 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (k_grid_small)
   while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
     d.cshift++;
+  d.cshift_c = 0;  // player-cell grid: as fine as one block's LDS histogram allows
+  while ((((d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c) * ((d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c)) > 4096)
+    d.cshift_c++;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return fail("hipStreamCreate failed");
@@ -220,6 +223,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(v_flags, uint32_t, V); AL(v_active, uint8_t, V);
   AL(vcnt, int, A * H1); AL(vstart, int, A * H1); AL(vitems, int, V); AL(v_rank, int, V);
   AL(ccnt, int, A * H1); AL(cstart, int, A * H1); AL(citems, int, C); AL(c_rank, int, C);
+  AL(cgcnt, int, A * 2 * 4100);
   AL(occ, unsigned long long, A * d.occ_words);
   AL(dead, int, NP); AL(work, int, A * d.Wcap); AL(work2, int, A * d.Wcap);
   AL(f_list, int, C * FCAP); AL(f_cnt, uint8_t, C); AL(f_done, uint8_t, C);
@@ -297,6 +301,7 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   hipLaunchKernelGGL(k_fill_d, dim3((NP + 255) / 256), dim3(256), 0, h->stream, d.o_last_mass, NP,
                      __builtin_nan(""));  // NN bots' lastMass = None (bot.py:125-130)
   HIPCHK(hipMemsetAsync(d.cstart, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.cgcnt, 0, sizeof(int) * A * 2 * 4100, h->stream));
   HIPCHK(hipMemsetAsync(d.vstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.bstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.o_lastfov, 0, sizeof(double) * NP, h->stream));
@@ -687,11 +692,11 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   }
   // cell grid (for observations before the next tick)
   std::vector<int> start, order;
-  host_grid(d.cols, gx, gy, start, order);
+  host_grid(d.cols, gx, gy, start, order, d.cshift_c);
   std::vector<int> items(order.size());
   for (size_t i = 0; i < order.size(); i++) items[i] = gid[order[i]];
   const size_t H1 = (size_t)d.H + 1;
-  HIPCHK(hipMemcpyAsync(d.cstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(d.cstart + arena * H1, start.data(), 4 * start.size(), hipMemcpyHostToDevice, h->stream));
   if (!items.empty())
     HIPCHK(hipMemcpyAsync(d.citems + (size_t)arena * CB, items.data(), 4 * items.size(), hipMemcpyHostToDevice,
                           h->stream));
@@ -772,6 +777,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   // look-back epochs restart too: clear this arena's tile states
   HIPCHK(hipMemsetAsync(d.pl_state + (size_t)arena * d.pl_tiles, 0, 8 * (size_t)d.pl_tiles, h->stream));
   HIPCHK(hipMemsetAsync(d.pel_dead + (size_t)arena * d.Pcap, 0, (size_t)d.Pcap, h->stream));  // buffer 0 is current
+  HIPCHK(hipMemsetAsync(d.cgcnt + (size_t)arena * 2 * 4100, 0, sizeof(int) * 2 * 4100, h->stream));
   for (int sl = 0; sl < 2; sl++)
     HIPCHK(hipMemsetAsync(d.scan_state + ((size_t)sl * d.A + arena) * d.scan_tiles, 0, 8 * (size_t)d.scan_tiles,
                           h->stream));

@@ -13,6 +13,8 @@
 // every pellet-mass sum runs in the reference's order.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "aigar_dev.h"
 #include "aigar_sem.h"
 #include "aigar_wave.h"
@@ -21,18 +23,58 @@ namespace aigar {
 
 #define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
 
-constexpr int OBS_PCAP = 256;  // visible pellets per bot kept in LDS
+#ifndef AIGAR_OBS_PCAP
+#define AIGAR_OBS_PCAP 256
+#endif
+constexpr int OBS_PCAP = AIGAR_OBS_PCAP;  // visible pellets per bot kept in LDS
 constexpr int OBS_CCAP = 64;   // visible player cells
 constexpr int OBS_VCAP = 32;   // visible viruses
 
+#ifdef AIGAR_OBS_TIMING  // diagnostics build: per-wave phase timestamps (tools/micro/obs_timing.py)
+constexpr int OBS_TS = 8;
+__device__ unsigned long long g_obs_ts[65536 * OBS_TS];
+#define OBS_STAMP(k) \
+  if (lane == 0) obs_ts_l[k] = wall_clock64()
+#else
+#define OBS_STAMP(k)
+#endif
+
 // x / y index masks of the reference's float-hash insertion loops
-__device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, double lim) {
+__device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, double inv_gs, double lim) {
   double cl = py_max(0.0, p - r);
-  double bl = cl - py_mod(cl, gs);
+  double bl = cl - aigar_math::mod_pos(cl, gs, inv_gs);  // (cl >= 0, gs > 0)
   double lx = py_min(lim, p + r);
   uint32_t m = 0;
   for (double x = bl; x <= lx; x += gs) m |= 1u << min(31, (int)(x / gs));
   return m;
+}
+
+// Pellet radius (cell.py:210-212): spawned pellets weigh 1, 2 or 3
+// (field.py:20-26), whose radii fold to constants (sqrt and division are
+// correctly rounded: the constants are Python's math.sqrt(m / math.pi), checked
+// against the device formula by tests/test_gpu_selftest.py); other masses
+// (converted blobs) take the full formula.
+constexpr double kPelletR1 = 0x1.20dd750429b6dp-1, kPelletR2 = 0x1.9884533d43651p-1,
+                 kPelletR3 = 0x1.f45437857749ap-1;
+__device__ __forceinline__ double pellet_radius(double m) {
+  constexpr double r1 = kPelletR1, r2 = kPelletR2, r3 = kPelletR3;
+  if (m == 1.0) return r1;
+  if (m == 2.0) return r2;
+  if (m == 3.0) return r3;
+  return radius_of(m);
+}
+
+// lane k's value, broadcast to the wave (v_readlane into scalar registers; k is wave-uniform)
+__device__ __forceinline__ double readlane_d(double v, int k) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, k);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int k) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)v, k);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(v >> 32), k);
+  return (int64_t)(((unsigned long long)hi << 32) | lo);
 }
 
 // One list of visible objects (structure of arrays).  Lives in LDS; when a
@@ -88,14 +130,16 @@ __device__ __forceinline__ int obs_claim(const Dev &d, uint32_t epoch, int n) {
 // kind to f(valid, kind, g) (kind 0 pellet slot, 1 cell pool index, 2 virus
 // slot; g is the global index), so the three queries share their memory
 // latency instead of chaining it.  f is called by every lane (it may ballot).
-template <class F>
-__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool want_p, bool want_v, F f) {
+// pre() runs once, after the row-range loads are issued and before they are
+// used (the caller's own-cell appends overlap that latency).
+template <class P, class F>
+__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool want_p, bool want_v, P pre, F f) {
   const int lane = threadIdx.x & 63;
   const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
   const ArenaCtl &ctl = d.ctl[a];
   const int Ec = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
   const int Ev = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
-  const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, 0), sv = grid_span(Q, Ev, d.cols, d.cshift);
+  const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, d.cshift_c), sv = grid_span(Q, Ev, d.cols, d.cshift);
   const int np_rows = (qok && want_p) ? sp.by1 - sp.by0 + 1 : 0;
   const int nc_rows = qok ? sc.by1 - sc.by0 + 1 : 0;
   const int nv_rows = (qok && want_v) ? sv.by1 - sv.by0 + 1 : 0;
@@ -103,9 +147,10 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool 
   const size_t H1 = (size_t)a * (d.H + 1);
   const int *pst = d.pstart + H1, *cst = d.cstart + H1, *vst = d.vstart + H1;
   const int *cit = d.citems + (size_t)a * kMaxCells * d.B, *vit = d.vitems + (size_t)a * d.Vcap;
+  if (nrows <= 0) pre();
   for (int r0 = 0; r0 < nrows; r0 += 64) {
     const int R = r0 + lane, nr = min(64, nrows - r0);
-    int lo = 0, len = 0, kind = 0;
+    int lo = 0, hi = 0, kind = 0;
     if (R < nrows) {
       const int *st;
       int row, bx0, bx1, stride;
@@ -117,8 +162,10 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool 
         kind = 2; st = vst; row = sv.by0 + (R - np_rows - nc_rows); bx0 = sv.bx0; bx1 = sv.bx1; stride = sv.stride;
       }
       lo = st[row * stride + bx0];
-      len = st[row * stride + bx1 + 1] - lo;
+      hi = st[row * stride + bx1 + 1];
     }
+    if (r0 == 0) pre();
+    const int len = hi - lo;
     int inc = len;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -140,8 +187,13 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool 
   }
 }
 
+#ifdef AIGAR_OBS_WPE
+#define OBS_ATTR __attribute__((amdgpu_waves_per_eu(AIGAR_OBS_WPE, 8)))
+#else  // 4 waves/SIMD: 4096 bots = 16 waves per CU, one residency round on 256 CUs
+#define OBS_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
+#endif
 template <typename OutT>
-__global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch) {
+__global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch) {
   // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
   // masks in creation order (no indirection in the per-square sums)
   __shared__ union {
@@ -163,32 +215,63 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
 
   const int gp = blockIdx.x, lane = threadIdx.x;
   const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
+#ifdef AIGAR_OBS_TIMING
+  __shared__ unsigned long long obs_ts_l[OBS_TS];
+  if (lane == 0) obs_ts_l[5] = (unsigned long long)__smid();
+#endif
+  OBS_STAMP(0);
   OutT *row = out + (size_t)gp * L;
-  if (!d.p_alive[gp]) {  // getStateRepresentation returns None for dead players
+  // one round of independent loads: liveness, the FOV cache written at the end
+  // of the tick (store_player_fov) and the own cells' slots
+  const bool alive = d.p_alive[gp];
+  const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
+  const int ncell = d.p_ncells[gp];
+  const int oslot = lane < kMaxCells ? (int)d.p_list[lane * NP + gp] : 0;
+  if (!alive) {  // getStateRepresentation returns None for dead players
     for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
     return;
   }
-  // FOV cache written at the end of the tick (store_player_fov)
-  const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
-  const int ncell = d.p_ncells[gp];
-  const double left = fx - fs / 2, top = fy - fs / 2, gs = fs / G;
+  // own cells (getPortionOfCellsInFov(player.getCells())), loaded up front
+  double ox = 0, oy = 0, orad = 0, omass = 0;
+  if (lane < ncell) {
+    const size_t ci = (size_t)oslot * NP + gp;
+    ox = d.c_x[ci];
+    oy = d.c_y[ci];
+    orad = d.c_r[ci];
+    omass = d.c_m[ci];
+  }
+  const double left = fx - fs / 2, top = fy - fs / 2, gs = fs / G, inv_gs = 1.0 / gs;
   const int cols = (int)ceil(fs / gs);
   const double lim = fs - 1;
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
+  // owner of cell pool index g = slot * NP + player, without a 64-bit modulo
+  const double inv_np = 1.0 / NP;
+  auto pool_owner = [&](size_t g) {
+    const int gi = (int)g;
+    int o = gi - (int)((double)gi * inv_np) * NP;
+    o += o < 0 ? NP : 0;
+    return o >= NP ? o - NP : o;
+  };
   const ArenaCtl &ctl = d.ctl[a];
   // last-frame history grids: independent of the queries, fetched up front
   // (first two squares of each lane; larger grids read the rest in the loop)
-  double h_slf[2] = {0, 0}, h_elf[2] = {0, 0};
+  // (GG <= 128: the loop below then issues no load, so no wait on its own stores)
+  double h_slf0 = 0, h_slf1 = 0, h_elf0 = 0, h_elf1 = 0;  // (scalars: no stack slot)
+  double h_sslf0 = 0, h_sslf1 = 0, h_eslf0 = 0, h_eslf1 = 0;
   {
-    const bool pslf = d.obs_ch & AIGAR_OBS_SELF_LF, pelf = d.obs_ch & AIGAR_OBS_ENEMY_LF;
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const int t = lane + 64 * j;
-      if (t < GG) {
-        if (pslf) h_slf[j] = d.o_self_lf[(size_t)gp * GG + t];
-        if (pelf) h_elf[j] = d.o_en_lf[(size_t)gp * GG + t];
-      }
-    }
+    const uint32_t och = d.obs_ch;
+    const bool pslf = och & (AIGAR_OBS_SELF_LF | AIGAR_OBS_SELF_SLF), pelf = och & (AIGAR_OBS_ENEMY_LF | AIGAR_OBS_ENEMY_SLF);
+    const bool psslf = och & AIGAR_OBS_SELF_SLF, peslf = och & AIGAR_OBS_ENEMY_SLF;
+    const size_t hb = (size_t)gp * GG + lane;
+    const bool in0 = lane < GG, in1 = lane + 64 < GG;
+    if (pslf && in0) h_slf0 = d.o_self_lf[hb];
+    if (pelf && in0) h_elf0 = d.o_en_lf[hb];
+    if (pslf && in1) h_slf1 = d.o_self_lf[hb + 64];
+    if (pelf && in1) h_elf1 = d.o_en_lf[hb + 64];
+    if (psslf && in0) h_sslf0 = d.o_self_slf[hb];
+    if (peslf && in0) h_eslf0 = d.o_en_slf[hb];
+    if (psslf && in1) h_sslf1 = d.o_self_slf[hb + 64];
+    if (peslf && in1) h_eslf1 = d.o_en_slf[hb + 64];
   }
 
   // ---- getPelletsInFov / getEnemyPlayerCellsInFov / getVirusesInFov
@@ -200,21 +283,17 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   const int pcur = ctl.pcur;  // current pellet buffer
 
   auto walk = [&](ObjList &PLx, int capP, ObjList &CLx, int capC, ObjList &VLx, int capV, int &np, int &nc,
-                  int &nv) {
+                  int &nv) __attribute__((always_inline)) {
     np = nc = nv = 0;
-    {  // own cells first: getPortionOfCellsInFov(player.getCells())
+    auto own_cells = [&]() {  // own cells first: getPortionOfCellsInFov(player.getCells())
       Cand c{false, 0, 0, 0, 0, 1};
-      if (lane < ncell) {
-        size_t ci = (size_t)d.p_list[lane * NP + gp] * NP + gp;
-        double x = d.c_x[ci], y = d.c_y[ci], r = d.c_r[ci], m = d.c_m[ci];
-        if (in_fov(x, y, r, fx, fy, fs)) {
-          uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
-          if (ix && iy) c = Cand{true, 0, m, r, ix | (iy << 16), 1};
-        }
+      if (lane < ncell && in_fov(ox, oy, orad, fx, fy, fs)) {
+        uint32_t ix = axis_mask(ox - left, orad, gs, inv_gs, lim), iy = axis_mask(oy - top, orad, gs, inv_gs, lim);
+        if (ix && iy) c = Cand{true, 0, omass, orad, ix | (iy << 16), 1};
       }
       list_append(c, CLx, capC, nc);
-    }
-    wave_fov_walk(d, a, Q, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, [&](bool valid, int kd, size_t g) {
+    };
+    wave_fov_walk(d, a, Q, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, own_cells, [&](bool valid, int kd, size_t g) {
       const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
       const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
       const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
@@ -231,13 +310,13 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
         r = kd == 0 ? 0.0 : RR[g];
         sq = kd == 1 ? 0 : S[g];
         uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
-        if (kd == 0) r = radius_of(m);
-        ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && (int)(g % NP) == gp) &&
+        if (kd == 0) r = pellet_radius(m);
+        ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && pool_owner(g) == gp) &&
              rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs);
       }
       uint32_t msk = 0;
       if (ok) {
-        uint32_t ix = axis_mask(x - left, r, gs, lim), iy = axis_mask(y - top, r, gs, lim);
+        uint32_t ix = axis_mask(x - left, r, gs, inv_gs, lim), iy = axis_mask(y - top, r, gs, inv_gs, lim);
         ok = ix && iy;
         msk = ix | (iy << 16);
       }
@@ -246,11 +325,18 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
       list_append(Cand{ok && kd == 2, sq, m, r, msk, 0}, VLx, capV, nv);
     });
   };
+  int np, nc, nv;
+  OBS_STAMP(1);
+  {  // (lists known to be the LDS arrays here: ds_write appends)
+    ObjList P0{&p_sx[0].seq, p_m, nullptr, p_mask, nullptr, nullptr};
+    ObjList C0{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
+    ObjList V0{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
+    walk(P0, OBS_PCAP, C0, OBS_CCAP, V0, OBS_VCAP, np, nc, nv);
+  }
+  OBS_STAMP(2);
   ObjList PL{&p_sx[0].seq, p_m, nullptr, p_mask, nullptr, &p_px[0].perm};
   ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
   ObjList VL{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
-  int np, nc, nv;
-  walk(PL, OBS_PCAP, CL, OBS_CCAP, VL, OBS_VCAP, np, nc, nv);
   if (np > OBS_PCAP || nc > OBS_CCAP || nv > OBS_VCAP) {
     // a list outgrew LDS: claim slices of the global pool for the overflowing
     // lists and walk again (exact, only slower)
@@ -324,6 +410,10 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
     }
   }
   wave_fence();
+  OBS_STAMP(3);
+#ifdef AIGAR_OBS_TIMING
+  if (lane == 0) obs_ts_l[6] = (unsigned long long)np | ((unsigned long long)nc << 20) | ((unsigned long long)nv << 40);
+#endif
 
   // ---- per grid square (bot.py:387-456); lane owns squares t = lane + 64*j
   const uint32_t ch = d.obs_ch;
@@ -343,39 +433,64 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
   if (ch & AIGAR_OBS_ENEMY_LF) { o_elf = off; off += GG; }
   double *slf = d.o_self_lf + (size_t)gp * GG, *sslf = d.o_self_slf + (size_t)gp * GG;
   double *elf = d.o_en_lf + (size_t)gp * GG, *eslf = d.o_en_slf + (size_t)gp * GG;
+  // square centres, accumulated as the reference does (mx += gs per column,
+  // bot.py:389-398): lane j holds column / row j's, read back by shuffle
+  double colx = left + gs / 2, rowy = top + gs / 2;
+  if (G <= 64)
+    for (int i = 0; i < min(lane, G - 1); i++) {
+      colx += gs;
+      rowy += gs;
+    }
+  const double inv_G = 1.0 / G, inv_cols = 1.0 / cols;
+  // t / n for 0 <= t, n < 2^20: double reciprocal, then one correction step
+  auto idiv = [](int t, int n, double inv_n) {
+    int q = (int)((double)t * inv_n);
+    q -= (q * n > t) ? 1 : 0;
+    q += ((q + 1) * n <= t) ? 1 : 0;
+    return q;
+  };
+  // instantiated twice: with the LDS lists themselves (ds_read, no wait on the
+  // row stores in flight) and with generic pointers (a list in the overflow pool)
+  // The per-square scans read list entry k through accessors: PEL(k) -> (mass,
+  // mask) of the k-th pellet in creation order, CEL(k) -> (mass, mask, own),
+  // VIR(k) -> (radius, mass, seq, mask).
+  auto squares = [&](auto hist_regs, auto PEL, auto CEL, auto VIR) __attribute__((always_inline)) {
   for (int t = lane; t < GG; t += 64) {
-    int c = t / G, r = t - c * G;
-    double mx = left + gs / 2, my = top + gs / 2;
-    for (int i = 0; i < r; i++) mx += gs;
-    for (int i = 0; i < c; i++) my += gs;
-    int ix = t % cols, iy = t / cols;
+    const int c = idiv(t, G, inv_G), r = t - c * G;
+    double mx, my;
+    if (G <= 64) {  // (wave-uniform)
+      mx = __shfl(colx, r);
+      my = __shfl(rowy, c);
+    } else {
+      mx = left + gs / 2;
+      my = top + gs / 2;
+      for (int i = 0; i < r; i++) mx += gs;
+      for (int i = 0; i < c; i++) my += gs;
+    }
+    const int iy = idiv(t, cols, inv_cols), ix = t - iy * cols;
     uint32_t need = (1u << ix) | (1u << (16 + iy));
     double vp = 0, ve = 0, vs = 0, vv = 0;
     bool within = !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
     if (within && ix < 16) {
       double s = 0;
       bool anyp = false;
-      if (in_lds) {
-        for (int k = 0; k < np; k++)
-          if ((smk[k] & need) == need) {
-            s += sm[k];
-            anyp = true;
-          }
-      } else {
-        for (int k = 0; k < np; k++) {
-          int e = PL.perm[k];
-          if ((PL.mask[e] & need) == need) {
-            s += PL.m[e];
-            anyp = true;
-          }
-        }
+      for (int k = 0; k < np; k++) {  // creation order
+        double m;
+        uint32_t mk;
+        PEL(k, m, mk);
+        const bool hit = (mk & need) == need;
+        s = hit ? s + m : s;
+        anyp |= hit;
       }
       if (anyp) vp = s;
       bool fe = false, fo = false;
       for (int k = 0; k < nc; k++) {
-        if ((CL.mask[k] & need) != need) continue;
-        double m = CL.m[k];
-        if (CL.own[k]) {
+        double m;
+        uint32_t mk;
+        bool own;
+        CEL(k, m, mk, own);
+        if ((mk & need) != need) continue;
+        if (own) {
           if (!fo || m > vs) vs = m;
           fo = true;
         } else {
@@ -387,12 +502,15 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
       double br = 0;
       int64_t bs = 0;
       for (int k = 0; k < nv; k++) {
-        if ((VL.mask[k] & need) != need) continue;
-        double rr = VL.r[k];
-        if (!fv || rr > br || (rr == br && VL.seq[k] < bs)) {
+        double rr, vmk;
+        int64_t sq;
+        uint32_t mk;
+        VIR(k, rr, vmk, sq, mk);
+        if ((mk & need) != need) continue;
+        if (!fv || rr > br || (rr == br && sq < bs)) {
           br = rr;
-          bs = VL.seq[k];
-          vv = VL.m[k];
+          bs = sq;
+          vv = vmk;
         }
         fv = true;
       }
@@ -400,30 +518,98 @@ __global__ void __launch_bounds__(64) k_observe(Dev d, OutT *out, uint32_t epoch
     double lb = py_min(py_max(mx - gs / 2, 0.0), fieldSize), tb = py_min(py_max(my - gs / 2, 0.0), fieldSize);
     double rb = py_max(py_min(mx + gs / 2, fieldSize), 0.0), bb = py_max(py_min(my + gs / 2, fieldSize), 0.0);
     double freeA = (rb - lb) * (bb - tb);
-    double vw = py_round3(1 - (freeA / (gs * gs)));
+    // a square wholly inside the field: freeA / (gs*gs) is exactly 1 -> round(0, 3) = +0
+    double vw = (freeA == gs * gs) ? 0.0 : py_round3(1 - (freeA / (gs * gs)));
     if (o_pel >= 0) row[o_pel + t] = (OutT)vp;
     if (o_self >= 0) row[o_self + t] = (OutT)vs;
     if (o_wall >= 0) row[o_wall + t] = (OutT)vw;
     if (o_enemy >= 0) row[o_enemy + t] = (OutT)ve;
     if (o_all >= 0) row[o_all + t] = (OutT)py_max(ve, vs);
     if (o_vir >= 0) row[o_vir + t] = (OutT)vv;
+    double o_sl, o_ss, o_el, o_es;  // history before this frame
+    if constexpr (decltype(hist_regs)::value) {
+      o_sl = t < 64 ? h_slf0 : h_slf1;
+      o_ss = t < 64 ? h_sslf0 : h_sslf1;
+      o_el = t < 64 ? h_elf0 : h_elf1;
+      o_es = t < 64 ? h_eslf0 : h_eslf1;
+    } else {
+      o_sl = (o_slf >= 0 || o_sslf >= 0) ? slf[t] : 0.0;
+      o_ss = o_sslf >= 0 ? sslf[t] : 0.0;
+      o_el = (o_elf >= 0 || o_eslf >= 0) ? elf[t] : 0.0;
+      o_es = o_eslf >= 0 ? eslf[t] : 0.0;
+    }
     if (o_sslf >= 0) {
-      row[o_sslf + t] = (OutT)sslf[t];
-      sslf[t] = slf[t];
+      row[o_sslf + t] = (OutT)o_ss;
+      sslf[t] = o_sl;
     }
     if (o_slf >= 0) {
-      row[o_slf + t] = (OutT)(t < 64 ? h_slf[0] : (t < 128 ? h_slf[1] : slf[t]));
+      row[o_slf + t] = (OutT)o_sl;
       slf[t] = vs;
     }
     if (o_eslf >= 0) {
-      row[o_eslf + t] = (OutT)eslf[t];
-      eslf[t] = elf[t];
+      row[o_eslf + t] = (OutT)o_es;
+      eslf[t] = o_el;
     }
     if (o_elf >= 0) {
-      row[o_elf + t] = (OutT)(t < 64 ? h_elf[0] : (t < 128 ? h_elf[1] : elf[t]));
+      row[o_elf + t] = (OutT)o_el;
       elf[t] = ve;
     }
   }
+  };
+  const bool all_lds = in_lds && CL.mask == c_mask && VL.mask == v_mask;
+  if (all_lds && np <= 64 && nc <= 64 && nv <= 64 && GG <= 128) {
+    // common case: entry k of every list sits in lane k's registers and is read
+    // with v_readlane into scalar registers (no LDS round trip per entry)
+    const double rpm = lane < np ? sm[lane] : 0.0, rcm = lane < nc ? c_mass[lane] : 0.0;
+    const uint32_t rpk = lane < np ? smk[lane] : 0u, rck = lane < nc ? c_mask[lane] : 0u;
+    const int rco = lane < nc ? c_own[lane] : 0;
+    const double rvr = lane < nv ? v_rad[lane] : 0.0, rvm = lane < nv ? v_mass[lane] : 0.0;
+    const int64_t rvs = lane < nv ? v_seqs[lane] : 0;
+    const uint32_t rvk = lane < nv ? v_mask[lane] : 0u;
+    squares(
+        std::true_type{},
+        [&](int k, double &m, uint32_t &mk) {
+          m = readlane_d(rpm, k);
+          mk = (uint32_t)__builtin_amdgcn_readlane((int)rpk, k);
+        },
+        [&](int k, double &m, uint32_t &mk, bool &own) {
+          m = readlane_d(rcm, k);
+          mk = (uint32_t)__builtin_amdgcn_readlane((int)rck, k);
+          own = __builtin_amdgcn_readlane(rco, k) != 0;
+        },
+        [&](int k, double &rr, double &vmk, int64_t &sq, uint32_t &mk) {
+          rr = readlane_d(rvr, k);
+          vmk = readlane_d(rvm, k);
+          sq = readlane_i64(rvs, k);
+          mk = (uint32_t)__builtin_amdgcn_readlane((int)rvk, k);
+        });
+  } else {
+    const double *pm = in_lds ? sm : PL.m;
+    const uint32_t *pk = in_lds ? smk : PL.mask;
+    const int *pperm = in_lds ? nullptr : PL.perm;
+    squares(
+        std::false_type{},
+        [&](int k, double &m, uint32_t &mk) {
+          const int e = pperm ? pperm[k] : k;
+          m = pm[e];
+          mk = pk[e];
+        },
+        [&](int k, double &m, uint32_t &mk, bool &own) {
+          m = CL.m[k];
+          mk = CL.mask[k];
+          own = CL.own[k] != 0;
+        },
+        [&](int k, double &rr, double &vmk, int64_t &sq, uint32_t &mk) {
+          rr = VL.r[k];
+          vmk = VL.m[k];
+          sq = VL.seq[k];
+          mk = VL.mask[k];
+        });
+  }
+  OBS_STAMP(4);
+#ifdef AIGAR_OBS_TIMING
+  if (lane < OBS_TS && gp < 65536) g_obs_ts[(size_t)gp * OBS_TS + lane] = obs_ts_l[lane];
+#endif
   if (lane == 0) {  // getAdditionalFeatures (bot.py:302-323)
     const uint32_t ex = d.obs_ex;
     int o = off;
@@ -500,7 +686,7 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   double best = -1;
   uint64_t bord = ~0ull;
   double tx = 0, ty = 0;
-  wave_fov_walk(d, a, Q, true, d.virus_enabled, [&](bool valid, int kd, size_t g) {
+  wave_fov_walk(d, a, Q, true, d.virus_enabled, [] {}, [&](bool valid, int kd, size_t g) {
     if (!valid) return;
     const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
     const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
@@ -509,7 +695,7 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
     const int64_t *S = kd == 0 ? d.pel_seq[pcur] : (kd == 1 ? d.c_seq : d.v_seq);
     const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
     const double x = X[g], y = Y[g], m = M[g];
-    const double r = kd == 0 ? radius_of(m) : RR[g];
+    const double r = kd == 0 ? pellet_radius(m) : RR[g];
     const uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
     if ((fl & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
     if (kd == 1 && (int)(g % NP) == gp) return;
@@ -695,3 +881,13 @@ void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd) {
 }
 
 }  // namespace aigar
+
+#ifdef AIGAR_OBS_TIMING
+extern "C" int aigar_debug_obs_ts(unsigned long long *out, int n) {
+  n = n < 65536 ? n : 65536;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(aigar::g_obs_ts), sizeof(unsigned long long) * n * aigar::OBS_TS) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif

@@ -716,6 +716,7 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
 // 2^cshift (<= SG_CAP cells, chosen at create): LDS-atomic ranks, block scan,
 // coalesced start[] store, scatter.  One launch instead of count/scan/scatter.
 constexpr int SG_CAP = 4096;
+constexpr int CG_STRIDE = SG_CAP + 4;  // per-arena, per-parity stride of Dev::cgcnt (16-byte aligned rows)
 template <int KIND>
 __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
   __shared__ double vmin_w[16];
@@ -772,6 +773,97 @@ __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
   }
   __syncthreads();
 }
+// Player-cell grid, coarse (2^cshift_c fine buckets per side, <= SG_CAP cells).
+// k_cgrid_count takes atomic ranks in a small count array -- one per tick
+// parity; the other parity is re-zeroed here for the next tick -- and every
+// k_cgrid_scatter block re-scans those <= SG_CAP + 1 counts in LDS, so the
+// grid needs two launches and no multi-block scan.  Consumers apply the exact
+// footprint test, so the coarser buckets only add candidates.
+__device__ __forceinline__ int cgrid_cols(const Dev &d) { return (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c; }
+__device__ __forceinline__ int cgrid_bucket(const Dev &d, double x, double y) {
+  const int sh = d.cshift_c;
+  return (center_bucket_coord(y, d.cols) >> sh) * cgrid_cols(d) + (center_bucket_coord(x, d.cols) >> sh);
+}
+__device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int parity) {
+  return d.cgcnt + ((size_t)a * 2 + parity) * CG_STRIDE;
+}
+__global__ void __launch_bounds__(256) k_cgrid_count(Dev d) {
+  const int a = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x, per = kMaxCells * d.B;
+  const int cc = cgrid_cols(d), par = d.ctl[a].tick & 1;
+  if (i <= cc * cc) cgrid_counts(d, a, par ^ 1)[i] = 0;  // next tick's counts
+  const bool in = i < per;
+  const int slot = in ? i / d.B : 0, p = in ? i - slot * d.B : 0;
+  const size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
+  const bool ok = in && (d.c_flags[g] & F_ALIVE);
+  double x = 0, y = 0, r = 0;
+  if (ok) {
+    x = d.c_x[g];
+    y = d.c_y[g];
+    r = d.c_r[g];
+  }
+  wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? r : 0.0);
+  if (!ok) return;
+  d.c_rank[(size_t)a * per + i] = atomicAdd(&cgrid_counts(d, a, par)[cgrid_bucket(d, x, y)], 1);
+}
+__global__ void __launch_bounds__(256) k_cgrid_scatter(Dev d) {
+  __shared__ int sc[CG_STRIDE];
+  __shared__ int wsum[4];
+  const int a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = blockIdx.x * 256 + tid, per = kMaxCells * d.B;
+  const int cc = cgrid_cols(d), n = cc * cc;  // buckets (start[n] = total)
+  // this thread's cell first (independent of the scan): its loads overlap the counts'
+  const bool in = i < per;
+  const int slot = in ? i / d.B : 0, p = in ? i - slot * d.B : 0;
+  const size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
+  bool ok = in && (d.c_flags[g] & F_ALIVE);
+  double x = 0, y = 0;
+  int rk = 0;
+  if (ok) {
+    x = d.c_x[g];
+    y = d.c_y[g];
+    rk = d.c_rank[(size_t)a * per + i];
+  }
+  // exclusive scan of the <= 4096 counts: 16 per thread (4 aligned int4 loads)
+  const int4 *c4 = reinterpret_cast<const int4 *>(cgrid_counts(d, a, d.ctl[a].tick & 1));
+  int v[16], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int j = tid * 16 + 4 * k;
+    int4 q = j < n ? c4[j >> 2] : make_int4(0, 0, 0, 0);
+    v[4 * k] = j < n ? q.x : 0;
+    v[4 * k + 1] = j + 1 < n ? q.y : 0;
+    v[4 * k + 2] = j + 2 < n ? q.z : 0;
+    v[4 * k + 3] = j + 3 < n ? q.w : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) sum += v[k];
+  int inc = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int t = __shfl_up(inc, off);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int run = inc - sum;
+  for (int k = 0; k < w; k++) run += wsum[k];
+  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int j = tid * 16 + k;
+    if (j < n) sc[j] = run;
+    run += v[k];
+  }
+  if (tid == 0) sc[n] = total;
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    int *start = d.cstart + (size_t)a * (d.H + 1);
+    for (int j = tid; j <= n; j += 256) start[j] = sc[j];
+  }
+  if (!ok) return;
+  d.citems[(size_t)a * per + sc[cgrid_bucket(d, x, y)] + rk] = (int)g;
+}
+
 // blocks [0, A): blob grids; [A, 2A): virus grids (when enabled)
 __global__ void __launch_bounds__(1024) k_grid_small(Dev d) {
   __shared__ int cnt[SG_CAP + 1];
@@ -1760,7 +1852,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
       // and every growth re-activates the cells overlapping the grown one
       double me = d.c_m[e];
       return overlap(x, y, m, r, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(m, me) || can_eat(me, m));
-    });
+    }, d.cshift_c);
     if (lane == 0) d.c_active[ci] = any;
     anyp |= any;
   }
@@ -1881,7 +1973,7 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
           s_r[slot] = er;
         }
         nc += __popcll(bal);
-      });
+      }, d.cshift_c);
       if (nc > PP_LCAP) {
         set_err(d, a, ERR_CAND_CAP);
         nc = PP_LCAP;
@@ -1936,7 +2028,7 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
           active_st(d, (size_t)e, 1);
           int pe = (int)(e % NP) - a * B;
           if (pe > P) atomicOr(&pend[pe >> 5], 1u << (pe & 31));
-        });
+        }, d.cshift_c);
         active_st(d, g, 1);
         if (gpl - a * B > P && lane == 0) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
         wave_fence();
@@ -2306,7 +2398,12 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
     hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
   }
-  launch_grid<0>(d, s, d.ccnt, d.cstart);
+  {  // player-cell grid (coarse): counts + scatter with an in-block scan
+    const long per = (long)kMaxCells * d.B;
+    const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
+    hipLaunchKernelGGL(k_cgrid_count, dim3(nblk(std::max(per, (long)cc * cc + 1), 256), d.A), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_cgrid_scatter, dim3(nblk(per, 256), d.A), dim3(256), 0, s, d);
+  }
   launch_food<0>(d, s, rounds, scr);
   launch_food<1>(d, s, rounds, scr);
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);

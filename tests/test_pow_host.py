@@ -16,3 +16,15 @@ def test_fast_pow_matches_slow_series(tmp_path):
     assert "mismatches=0" in out.stdout, out.stdout
     err = float(out.stdout.split("(2^")[1].split(")")[0])
     assert err < -72.0, out.stdout  # bound used by the rounding test is 2^-70
+
+
+def test_mod_pos_matches_python_float_mod(tmp_path):
+    """aigar_math::mod_pos (multiply + exact fma remainder) == Python's a % b
+    for the non-negative offsets the grid footprints use (host build)."""
+    exe = str(tmp_path / "check_mod")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I",
+                           os.path.join(ROOT, "aigar_amd", "csrc"), os.path.join(ROOT, "tools", "gen", "check_mod.cpp"),
+                           "-o", exe])
+    out = subprocess.run([exe, "300000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout, out.stdout
