@@ -9,6 +9,24 @@
 
 namespace aigar {
 
+__device__ __forceinline__ void atomic_max_pos(double *addr, double v) {  // v >= 0
+  atomicMax((unsigned long long *)addr, (unsigned long long)__double_as_longlong(v));
+}
+// max over the wavefront, then one atomic per wave (all lanes must call; invalid
+// lanes pass 0).  A wave whose lanes target different arenas falls back to per-lane atomics.
+__device__ __forceinline__ void wave_atomic_max_pos(double *addr, double v) {
+  unsigned long long ad = (unsigned long long)addr, a0 = __shfl(ad, 0);
+  if (__all(ad == a0)) {
+    double m = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    if (__lane_id() == 0 && m > 0) atomic_max_pos(addr, m);
+  } else if (v > 0) {
+    atomic_max_pos(addr, v);
+  }
+}
+
+
 // Wave-parallel walk over the grid rows around q (expanded by E): the rows'
 // item ranges are loaded by one lane each and flattened with a prefix sum, so
 // 64 items are inspected per step whatever the row layout.  f(valid, item) is
@@ -70,7 +88,7 @@ __device__ __forceinline__ void wave_fence() {
 // getFovSize / getFovPos / getTotalMass of one player (player.py:129,156-167),
 // sequential over its cells in list order (numpy pairwise sums below 128)
 struct Fov {
-  double fx, fy, fs, mass;
+  double fx, fy, fs, mass, rmax;
   int n;
 };
 __device__ inline Fov player_fov(const Dev &d, int gp) {
@@ -92,6 +110,7 @@ __device__ inline Fov player_fov(const Dev &d, int gp) {
   f.fs = aigar_math::pow_cr(rb, 0.475) * d.pow_n032[n] * 35;  // (table: same correctly rounded values)
   f.fx = np_sum(xs, n) / f.mass;
   f.fy = np_sum(ys, n) / f.mass;
+  f.rmax = rb;
   return f;
 }
 // per-player FOV cache, refreshed once the world state of a tick is final

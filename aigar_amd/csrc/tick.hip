@@ -48,23 +48,6 @@ __device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int
   e[4] = y;
 }
 
-__device__ __forceinline__ void atomic_max_pos(double *addr, double v) {  // v >= 0
-  atomicMax((unsigned long long *)addr, (unsigned long long)__double_as_longlong(v));
-}
-// max over the wavefront, then one atomic per wave (all lanes must call; invalid
-// lanes pass 0).  A wave whose lanes target different arenas falls back to per-lane atomics.
-__device__ __forceinline__ void wave_atomic_max_pos(double *addr, double v) {
-  unsigned long long ad = (unsigned long long)addr, a0 = __shfl(ad, 0);
-  if (__all(ad == a0)) {
-    double m = v;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
-    if (__lane_id() == 0 && m > 0) atomic_max_pos(addr, m);
-  } else if (v > 0) {
-    atomic_max_pos(addr, v);
-  }
-}
-
 // centre-bucket grid iteration: every entity whose centre bucket lies in the
 // query rectangle grown by E buckets (E covers the largest footprint).
 template <class F>
@@ -298,8 +281,6 @@ __global__ void __launch_bounds__(256) k_update_players(Dev d) {
 }
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d) {
   int gi = GTID;
-  // clear the player-hash occupancy bitmap for this tick's spawns (k_occupancy refills it)
-  for (size_t w = (size_t)gi; w < (size_t)d.A * d.occ_words; w += (size_t)gridDim.x * blockDim.x) d.occ[w] = 0;
   if (gi < kMaxCells * d.NP) {
     update_cell(d, gi);
     return;
@@ -2095,9 +2076,12 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
   oy = (double)yp;
 }
 
+__device__ void spawn_counts(const Dev &d, int a, int init);
+constexpr int OCC_LDS = 4096;  // occupancy words kept in LDS (32 KiB: fields up to 10240 units)
 __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
   __shared__ int sflag[1024];
   __shared__ int gcnt[SG_CAP + 1];
+  __shared__ unsigned long long s_occ[OCC_LDS];
   int a = blockIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
@@ -2159,7 +2143,45 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
   // (unchanged otherwise: viruses do not move after updateViruses, and the ones
   // appended by splits or spawns are not hashed this tick)
   if (d.virus_enabled && (dirty & DIRTY_VIRUS)) grid_small_build<2>(d, a, gcnt, sflag);
-  if (tid != 0) return;
+  __shared__ int s_spawn;
+  if (tid == 0) {
+    spawn_counts(d, a, init);
+    s_spawn = !init && (c.n_spawn_pl > 0 || c.n_spawn_v > 0);
+  }
+  __syncthreads();
+  // player-hash occupancy for getSpawnPos (field.py:283-301): one bit per fine
+  // bucket a live player cell's footprint touches, built only when a player or
+  // a virus spawns this tick (in LDS when it fits, else with global atomics)
+  if (s_spawn) {
+    const int W = d.occ_words, NP = d.NP;
+    const bool lds = W <= OCC_LDS;
+    unsigned long long *gocc = d.occ + (size_t)a * W;
+    for (int i = tid; i < W; i += T) {
+      if (lds) s_occ[i] = 0;
+      else gocc[i] = 0;
+    }
+    __syncthreads();
+    for (int p = tid; p < d.B; p += T) {
+      const int gp = a * d.B + p, n = d.p_ncells[gp];
+      for (int k = 0; k < n; k++) {
+        const Rect r = cell_rect(d, (size_t)d.p_list[k * NP + gp] * NP + gp);
+        for (int by = r.y0; by <= r.y1; by++)
+          for (int bx = r.x0; bx <= r.x1; bx++) {
+            const int b = by * d.cols + bx;
+            if (lds) atomicOr(&s_occ[b >> 6], 1ull << (b & 63));
+            else atomicOr(&gocc[b >> 6], 1ull << (b & 63));
+          }
+      }
+    }
+    __syncthreads();
+    if (lds)
+      for (int i = tid; i < W; i += T) gocc[i] = s_occ[i];
+  }
+}
+
+// spawnStuff's counts (field.py:227-280): pellets and viruses to add, players to respawn
+__device__ void spawn_counts(const Dev &d, int a, int init) {
+  ArenaCtl &c = d.ctl[a];
   c.dirty = 0;
   // spawnPellets: while len(pellets) < maxCollectibleCount
   int alive_p = c.n_pel - c.n_pel_eaten + c.n_pnew;
@@ -2405,10 +2427,9 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
     hipLaunchKernelGGL(k_cgrid_scatter, dim3(nblk(per, 256), d.A), dim3(256), 0, s, d);
   }
   launch_food<0>(d, s, rounds, scr);
-  launch_food<1>(d, s, rounds, scr);
+  launch_food<1>(d, s, 1, scr);  // blob conflicts are rare: one reservation round, the rest serial
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
-  hipLaunchKernelGGL(k_occupancy, dim3(nblk((long)d.A * kMaxCells * d.B, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);  // + end-of-tick virus grid
   const long n_spawn = (long)d.NP + (long)d.A * d.Pcap + (d.virus_enabled ? (long)d.A * d.Vcap : 0) +
                        (long)d.A * d.H;
