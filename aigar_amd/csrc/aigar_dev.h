@@ -48,9 +48,9 @@ struct ArenaCtl {
   uint32_t scan_epoch[2];  // decoupled look-back epoch per scan slot (grows every launch)
   int scan_ticket[2];      // slot 0: pellet rebuilds, slot 1: cell grid (may run concurrently)
   int src_n_pel, src_n_stage;
+  int src_n_conv;  // blob conversions among the staged records (eaten ones are dropped)
   int pcur;           // pellet buffer holding the current (end-of-tick) pellets
   int peat;           // pellet buffer of this tick's eat phase (pcur when nothing was converted)
-  int p_skip;         // the conversion rebuild was skipped this tick
   uint32_t dirty;     // DIRTY_*: a virus / blob died this tick (k_spawn_plan compacts)
   int food_undone[3];  // cells that failed reservation round r (index r % 3)
   uint32_t pl_epoch;  // k_players look-back epoch / finished-tile ticket
@@ -68,7 +68,7 @@ enum : uint32_t {
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
 // pellet rebuild modes (also the scan's epilogue selector)
-enum : int { PR_NONE = 0, PR_RESET = 1, PR_CLOSE = 2, PR_CONVERT = 3 };
+enum : int { PR_NONE = 0, PR_RESET = 1, PR_CLOSE = 2 };
 
 // event phases (sort key high word), in reference order within a tick
 enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4, PH_PP = 5, PH_SPAWN = 6 };

@@ -84,7 +84,7 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
   if (i >= d.ctl[a].n_blob || !(d.b_flags[gi] & F_ALIVE)) return;
   if (d.b_svc[gi] == 0) {  // stopped blob becomes a pellet (addPellet)
     int j = atomicAdd(&d.ctl[a].n_pnew, 1);
-    if (j >= d.Pcap) {
+    if (d.ctl[a].n_pel + j >= d.Pcap) {  // (eat-phase index n_pel + j must fit, see Food)
       set_err(d, a, ERR_PELLET_CAP);
       return;
     }
@@ -881,7 +881,6 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
   int *o = start + (size_t)a * (d.H + 1);
   unsigned long long *st = d.scan_state + ((size_t)slot * d.A + a) * d.scan_tiles;
   ArenaCtl &ctl = d.ctl[a];
-  if (pfix == PR_CONVERT && ctl.p_skip) return;  // (uniform over the arena's blocks)
   if (tid == 0) s_epoch = __hip_atomic_load(&ctl.scan_epoch[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int base = tile * LB_TILE + tid * LB_PER;
   int v[LB_PER], sum = 0;
@@ -971,12 +970,14 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
     if (pfix) {
       ctl.src_n_pel = ctl.n_pel;
       ctl.src_n_stage = ctl.n_pnew + (extra ? ctl.n_spawn_p : 0);
+      ctl.src_n_conv = extra ? ctl.n_pnew : 0;
       ctl.n_pel = min(s_prefix + total, d.Pcap);
       ctl.n_pnew = 0;
       ctl.n_pel_eaten = 0;
       if (pfix == PR_CLOSE) {
         ctl.tick += 1;
         ctl.pcur = ctl.peat ^ 1;
+        ctl.peat = ctl.pcur;  // the next eat phase reads the buffer built here
       }
     }
   }
@@ -1015,23 +1016,13 @@ __device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
   const int b = center_bucket_coord(d.pn_y[g], d.cols) * d.cols + center_bucket_coord(d.pn_x[g], d.cols);
   d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + b], 1);
 }
-// mode PR_RESET: staging -> buffer 0; PR_CONVERT: current buffer U blob
-// conversions -> the other buffer, skipped (eat phase reads the current buffer)
-// when nothing was converted -- the common case
+// mode PR_RESET: staging -> buffer 0 (the closing rebuild of a tick takes its
+// counts in k_spawn_all)
 __global__ void k_pgrid_count(Dev d, int mode) {
   const int gi = GTID;
   const int per = d.H + d.Pcap;
   if (gi >= d.A * per) return;
   const int a = gi / per, i = gi - a * per;
-  if (mode == PR_CONVERT) {
-    ArenaCtl &c = d.ctl[a];
-    const bool skip = c.n_pnew == 0;
-    if (i == 0) {
-      c.p_skip = skip;
-      c.peat = skip ? c.pcur : c.pcur ^ 1;
-    }
-    if (skip) return;
-  }
   if (i < d.H) {  // bucket i of the source layout
     pgrid_count_bucket(d, a, i, 0);
     return;
@@ -1045,9 +1036,9 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
   if (gi >= d.A * per) return;
   const int a = gi / per, i = gi - a * per;
   const ArenaCtl &c = d.ctl[a];
-  if (mode == PR_CONVERT && c.p_skip) return;
   const bool use_dead = mode == PR_CLOSE;
-  const int src = mode == PR_RESET ? 1 : (mode == PR_CONVERT ? c.pcur : c.peat), dst = src ^ 1;
+  // (PR_CLOSE: the scan's epilogue already made the destination current)
+  const int src = mode == PR_RESET ? 1 : c.pcur ^ 1, dst = src ^ 1;
   const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
   double x, y, m;
   int64_t s;
@@ -1069,6 +1060,13 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
     int j = i - d.Pcap;
     if (j >= c.src_n_stage) return;
     size_t g = (size_t)a * d.Pcap + j;
+    if (use_dead && j < c.src_n_conv) {  // blob conversion: eat-phase index src_n_pel + j
+      const size_t ge = (size_t)a * d.Pcap + c.src_n_pel + j;
+      if (d.pel_dead[ge]) {
+        d.pel_dead[ge] = 0;
+        return;
+      }
+    }
     x = d.pn_x[g];
     y = d.pn_y[g];
     m = d.pn_m[g];
@@ -1457,17 +1455,35 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
 
 // ------------------------------------------------------------ T14/T15 food
 // foods: KIND 0 pellets (eat-phase buffer 1, records sorted by bucket), 1 blobs
+// Pellets of the eat phase: the current bucket-sorted buffer, indices [0, n0),
+// plus this tick's blob conversions (addPellet in updateBlobs), still in the
+// staging list, as indices [n0, n0 + nst) -- they join the sorted buffer at the
+// closing rebuild, so no rebuild runs before the eat phase.  Dead flags and
+// reservation words are indexed by the same j.
 template <int KIND>
 struct Food {
   const Dev &d;
   int a, pb;  // pb: the eat-phase pellet buffer (ArenaCtl::peat)
-  __device__ Food(const Dev &dd, int aa) : d(dd), a(aa), pb(KIND == 0 ? dd.ctl[aa].peat : 0) {}
+  int n0, nst;
+  __device__ Food(const Dev &dd, int aa)
+      : d(dd), a(aa), pb(KIND == 0 ? dd.ctl[aa].peat : 0), n0(KIND == 0 ? dd.ctl[aa].n_pel : 0),
+        nst(KIND == 0 ? dd.ctl[aa].n_pnew : 0) {}
   __device__ size_t g(int j) const { return (size_t)a * (KIND == 0 ? d.Pcap : d.Ecap) + j; }
-  __device__ double x(int j) const { return KIND == 0 ? d.pel_x[pb][g(j)] : d.b_x[g(j)]; }
-  __device__ double y(int j) const { return KIND == 0 ? d.pel_y[pb][g(j)] : d.b_y[g(j)]; }
-  __device__ double m(int j) const { return KIND == 0 ? d.pel_m[pb][g(j)] : d.b_m[g(j)]; }
-  __device__ double r(int j) const { return KIND == 0 ? radius_of(d.pel_m[pb][g(j)]) : d.b_r[g(j)]; }
-  __device__ int64_t seq(int j) const { return KIND == 0 ? d.pel_seq[pb][g(j)] : d.b_seq[g(j)]; }
+  __device__ size_t gs(int j) const { return (size_t)a * d.Pcap + (j - n0); }  // staging slot
+  __device__ double x(int j) const { return KIND == 0 ? (j < n0 ? d.pel_x[pb][g(j)] : d.pn_x[gs(j)]) : d.b_x[g(j)]; }
+  __device__ double y(int j) const { return KIND == 0 ? (j < n0 ? d.pel_y[pb][g(j)] : d.pn_y[gs(j)]) : d.b_y[g(j)]; }
+  __device__ double m(int j) const { return KIND == 0 ? (j < n0 ? d.pel_m[pb][g(j)] : d.pn_m[gs(j)]) : d.b_m[g(j)]; }
+  __device__ double r(int j) const { return KIND == 0 ? radius_of(m(j)) : d.b_r[g(j)]; }
+  __device__ int64_t seq(int j) const {
+    return KIND == 0 ? (j < n0 ? d.pel_seq[pb][g(j)] : d.pn_seq[gs(j)]) : d.b_seq[g(j)];
+  }
+  // the staged conversions as extra candidates of a grid walk (f as for wave_grid_for)
+  template <class Fn>
+  __device__ void for_staged(Fn f) const {
+    if (KIND != 0) return;
+    const int lane = threadIdx.x & 63;
+    for (int t0 = 0; t0 < nst; t0 += 64) f(t0 + lane < nst, n0 + t0 + lane);
+  }
   __device__ bool alive(int j) const { return KIND == 0 ? !d.pel_dead[g(j)] : (d.b_flags[g(j)] & F_ALIVE); }
   __device__ int64_t ej(int j) const { return KIND == 0 ? -2 : d.b_ej[g(j)]; }
   __device__ void kill(int j) const {
@@ -1535,7 +1551,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
     Rect q = footprint(x, y, r, d.size);
     int cnt = 0;
     double lsum = 0;
-    wave_grid_for(st, items, cols, q, 1, [&](bool valid, int j) {
+    auto visit = [&](bool valid, int j) {
       bool keep = false;
       double fx = 0, fy = 0, fm = 0;
       if (valid && F.alive(j) && F.ej(j) != cseq) {
@@ -1557,7 +1573,8 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
         }
       }
       cnt += __popcll(bal);
-    }, F.shift());
+    };
+    wave_grid_for(st, items, cols, q, 1, visit, F.shift(), F.n0, F.nst);  // (+ staged conversions)
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
     double sum = wave_sum(lsum);
@@ -1602,6 +1619,10 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
             atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
         }
       }
+      F.for_staged([&](bool valid, int j) {
+        if (valid && F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q))
+          atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
+      });
       continue;
     }
     int *lst = d.f_list + ci * FCAP;
@@ -1750,7 +1771,7 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
     const int64_t cseq = d.c_seq[ci];
     const Rect q = footprint(x, y, r, d.size);
     int nc = 0;
-    wave_grid_for(F.start(), F.items(), d.cols, q, 1, [&](bool valid, int j) {
+    auto gather = [&](bool valid, int j) {
       double fx = 0, fy = 0, fm = 0, fr = 0;
       bool keep = valid && F.alive(j) && F.ej(j) != cseq;
       if (keep) {
@@ -1771,7 +1792,8 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
         s_r[slot] = fr;
       }
       nc += __popcll(bal);
-    }, F.shift());
+    };
+    wave_grid_for(F.start(), F.items(), d.cols, q, 1, gather, F.shift(), F.n0, F.nst);  // (+ staged conversions)
     if (nc > FS_CAP) {
       set_err(d, a, ERR_CAND_CAP);
       nc = FS_CAP;
@@ -2325,7 +2347,13 @@ __global__ void __launch_bounds__(256) k_spawn_all(Dev d) {
   int gi = GTID;
   if (gi < d.NP) return spawn_player(d, gi, 0);
   gi -= d.NP;
-  if (gi < d.A * d.Pcap) return spawn_pellet(d, gi, true);
+  if (gi < d.A * d.Pcap) {
+    const int a = gi / d.Pcap, j = gi - a * d.Pcap;
+    const ArenaCtl &c = d.ctl[a];
+    // blob conversions that survived the eat phase join the closing rebuild
+    if (j < c.n_pnew && !d.pel_dead[(size_t)a * d.Pcap + c.n_pel + j]) pgrid_rank_staged(d, a, j);
+    return spawn_pellet(d, gi, true);
+  }
   gi -= d.A * d.Pcap;
   if (d.virus_enabled) {
     if (gi < d.A * d.Vcap) return spawn_virus(d, gi);
@@ -2358,7 +2386,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.scan_epoch[0] = c.scan_epoch[1] = 0;
   c.pl_epoch = 0;
   c.dirty = 0;
-  c.pcur = c.peat = c.p_skip = 0;
+  c.pcur = c.peat = 0;
   c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
@@ -2411,7 +2439,6 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
-  launch_pellet_rebuild(d, s, PR_CONVERT);  // current U blob conversions -> eat-phase buffer
   hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
                      dim3(256), 0, s, d);

@@ -76,11 +76,14 @@ def test_vec_env_runs_on_device_tensors():
     env = AgarVecEnv(64, p, field_size=600, max_viruses=10)
     obs = env.reset(3)
     assert obs.shape == (64, 7 * 121 + 7) and obs.is_cuda
+    was_alive = ~torch.isnan(obs[:, 0])
     for _ in range(10):
         act = torch.rand((64, 4), dtype=torch.float64, device="cuda")
         obs, rew, alive = env.step(act)
         assert rew.shape == (64,) and alive.dtype == torch.bool and torch.isfinite(rew).all()
-        # the observation's last-action extras are the action just taken (bot.py:316-319)
-        live = alive.nonzero().flatten()
+        # the observation's last-action extras are the action just taken (bot.py:316-319);
+        # a player dead when the action came keeps its old one (makeMove returns, bot.py:257)
+        live = (alive & was_alive).nonzero().flatten()
         assert torch.equal(obs[live, 7 * 121 + 3:7 * 121 + 7], act[live])
+        was_alive = alive
     env.close()
