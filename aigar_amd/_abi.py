@@ -22,6 +22,15 @@ EV_CELL_EAT_PELLET, EV_CELL_EAT_BLOB, EV_CELL_EAT_CELL, EV_PLAYER_DEATH, EV_RESP
 FLAG_EVENTS = 0x1
 
 
+POLICY_NONE, POLICY_RANDOM, POLICY_GREEDY = 0, 1, 2
+
+
+class RunParams(C.Structure):
+    """aigar_run_params (include/aigar.h): the policy replayed inside aigar_run's step graph."""
+    _fields_ = [("policy", C.c_int32), ("greedy_split", C.c_int32), ("p_split", C.c_double),
+                ("p_eject", C.c_double), ("seed", C.c_uint64)]
+
+
 class RewardParams(C.Structure):
     """aigar_reward_params (include/aigar.h); defaults of networkParameters.py:50,69-72."""
     _fields_ = [("mass_as_reward", C.c_int32), ("pad", C.c_int32), ("reward_term", C.c_double),

@@ -76,6 +76,7 @@ def load(build_if_missing=False):
         "aigar_apply_actions": [vp, vp, i32, i32, i32, i32, i32],
         "aigar_rewards": [vp, vp, C.POINTER(_abi.RewardParams), i32, i32],
         "aigar_set_split_likelihood": [vp, i32, C.POINTER(C.c_int32)],
+        "aigar_run": [vp, i32, C.POINTER(_abi.RunParams), vp, i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -173,6 +174,22 @@ class Stepper:
 
     def step(self, n=1):
         self._chk(self.L.aigar_step(self.h, int(n)))
+
+    def run(self, n, policy="random", out=None, p_split=0.0, p_eject=0.0, seed=0, greedy_split=False):
+        """n whole env steps (policy + Field.update + observation into the DEVICE tensor out,
+        or no observation when out is None), replayed from one captured hipGraph."""
+        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM, "greedy": _abi.POLICY_GREEDY}[policy]
+        prm = _abi.RunParams(pol, int(bool(greedy_split)), float(p_split), float(p_eject), int(seed))
+        p, dt = None, 0
+        if out is not None:
+            if not getattr(out, "is_cuda", False):
+                raise ValueError("aigar_run writes observations to a device tensor")
+            dt = 0 if str(out.dtype) == "torch.float64" else 1
+            if tuple(out.shape) != (self.NP, self.obs_len):
+                raise ValueError("observation tensor must be [%d, %d]" % (self.NP, self.obs_len))
+            p = C.c_void_p(out.data_ptr())
+        self._chk(self.L.aigar_run(self.h, int(n), C.byref(prm), p, dt))
+        return out
 
     def observe(self, out=None, dtype=np.float64):
         if out is None:

@@ -89,9 +89,9 @@ struct Dev {
   // players [NP]
   int *p_alive, *p_respawn, *p_ncells, *p_split, *p_eject, *p_pend;
   double *p_cmdx, *p_cmdy;
-  double *p_fx, *p_fy, *p_fs, *p_mass;
-  int *p_split_lh;
-  double *o_last_mass;  // NN bots' lastMass (bot.py:229-230); NaN = None  // Greedy bots' splitLikelihood (bot.py:93); <= 0: derived from the Philox key  // FOV cache (getFovPos/getFovSize/getTotalMass at tick end)
+  double *p_fx, *p_fy, *p_fs, *p_mass;  // FOV cache (getFovPos/getFovSize/getTotalMass at tick end)
+  int *p_split_lh;       // Greedy bots' splitLikelihood (bot.py:93); <= 0: derived from the Philox key
+  double *o_last_mass;  // NN bots' lastMass (bot.py:229-230); NaN = None
   uint8_t *p_list;  // [16][NP]
   int *p_newc, *p_newb, *p_seqoff, *p_bloboff;
   // cells [16*NP]
@@ -156,6 +156,7 @@ struct Dev {
   // observation overflow pool (bots that see more objects than their LDS lists hold)
   int OBcap;
   unsigned long long *ob_used;  // {observe call epoch:32 | overflow slots taken:32}
+  uint32_t *ob_epoch;  // device-side epoch for graph-replayed observes (bumped by k_player_fov)
   int64_t *ob_seq;
   double *ob_m, *ob_r;
   uint32_t *ob_mask;

@@ -66,9 +66,14 @@ struct aigar_handle {
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> marks;
   std::vector<hipEvent_t> event_pool;
   hipGraphExec_t graph = nullptr;
+  hipStream_t cap_stream = nullptr;  // private stream graphs are captured on (the caller's may be the null stream)
   bool use_graph = true;  // AIGAR_NO_GRAPH=1 disables (direct launches)
   bool graph_failed = false;
-  uint64_t policy_calls = 0;
+  // aigar_run: one whole env step (policy + Field.update + observation) as a graph
+  hipGraphExec_t run_graph = nullptr;
+  aigar_run_params run_key{};
+  void *run_out = nullptr;
+  int run_dtype = -1;
 };
 
 extern "C" const char *aigar_last_error(void) { return g_err.c_str(); }
@@ -97,6 +102,7 @@ static int obs_len_of(const aigar_config &c) {
 
 static void free_all(aigar_handle *h) {
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  if (h->run_graph) (void)hipGraphExecDestroy(h->run_graph);
   for (void *p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -107,6 +113,7 @@ static void free_all(aigar_handle *h) {
   }
   for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
   if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
+  if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
 }
 
 static hipEvent_t pool_event(aigar_handle *h) {
@@ -237,6 +244,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(pl_state, unsigned long long, A * d.pl_tiles);
   AL(ticket, int, 4);
   AL(ob_used, unsigned long long, 1);
+  AL(ob_epoch, uint32_t, 1);
   AL(p_split_lh, int, NP);
   AL(o_last_mass, double, NP);
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
@@ -329,9 +337,35 @@ extern "C" int aigar_set_commands(aigar_handle *h, const double *cmd, int on_dev
 extern "C" int aigar_policy_random(aigar_handle *h, double p_split, double p_eject, uint64_t seed) {
   if (!h) return fail("null handle");
   Mark m(h, "policy");
-  launch_policy(h->d, h->stream, p_split, p_eject, seed + (h->policy_calls++ << 20));
+  launch_policy(h->d, h->stream, p_split, p_eject, seed);  // draws keyed by (seed, tick, player)
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+// Capture launch(stream) into an executable graph on the handle's private
+// capture stream: graphs are then replayed on whatever stream the caller gave
+// (torch's default stream is the legacy null stream, which cannot capture).
+template <class F>
+static hipGraphExec_t capture_graph(aigar_handle *h, F launch) {
+  if (!h->cap_stream && hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking) != hipSuccess) {
+    h->cap_stream = nullptr;
+    return nullptr;
+  }
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  bool ok = hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  if (ok) {
+    launch(h->cap_stream);
+    ok = hipStreamEndCapture(h->cap_stream, &g) == hipSuccess && g;
+  }
+  if (ok) ok = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+  if (g) (void)hipGraphDestroy(g);
+  if (!ok) {
+    if (ge) (void)hipGraphExecDestroy(ge);
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return ge;
 }
 
 __global__ void k_step_begin(Dev d) {
@@ -346,25 +380,52 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every step
     hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
   if (h->use_graph && !h->graph && !h->graph_failed && n_ticks > 0) {
-    // capture one Field.update() (~40 kernel launches) once; replay it per tick
-    hipGraph_t g = nullptr;
-    bool ok = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
-    if (ok) {
-      launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
-      ok = hipStreamEndCapture(h->stream, &g) == hipSuccess && g;
-    }
-    if (ok) ok = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0) == hipSuccess;
-    if (g) (void)hipGraphDestroy(g);
-    if (!ok) {
-      h->graph = nullptr;
-      h->graph_failed = true;
-      (void)hipGetLastError();
-    }
+    // capture one Field.update() (~25 kernel launches) once; replay it per tick
+    h->graph = capture_graph(h, [&](hipStream_t cs) { launch_tick(h->d, cs, h->rounds, h->scr_k, h->scr_v); });
+    if (!h->graph) h->graph_failed = true;
   }
   for (int t = 0; t < n_ticks; t++) {
     Mark m(h, "tick");
     if (h->graph) HIPCHK(hipGraphLaunch(h->graph, h->stream));
     else launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// One batched env step -- Model.update's takeBotActions + Field.update + every
+// bot's getStateRepresentation (model.py:100-112, bot.py:272-299) -- captured
+// once as a single hipGraph and replayed n_steps times: no host round trip
+// between the policy, the tick's ~25 kernels and the observation.
+static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_params &p, void *out, int dtype) {
+  if (p.policy == AIGAR_POLICY_RANDOM) launch_policy(h->d, s, p.p_split, p.p_eject, p.seed);
+  else if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr);
+  launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v);
+  if (out) launch_observe(h->d, s, out, dtype, 0);  // epoch 0: the device-side epoch
+}
+
+extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p, void *obs_out, int dtype) {
+  if (!h || !p) return fail("null argument");
+  if (n_steps < 0) return fail("n_steps < 0");
+  if (p->policy < AIGAR_POLICY_NONE || p->policy > AIGAR_POLICY_GREEDY) return fail("unknown policy %d", p->policy);
+  if (obs_out && dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every call (all n_steps accumulate)
+    hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  const bool same = h->run_graph && memcmp(&h->run_key, p, sizeof *p) == 0 && h->run_out == obs_out &&
+                    h->run_dtype == (obs_out ? dtype : -1);
+  if (h->use_graph && !same && n_steps > 0) {
+    if (h->run_graph) (void)hipGraphExecDestroy(h->run_graph);
+    h->run_graph = capture_graph(h, [&](hipStream_t cs) { launch_env_step(h, cs, *p, obs_out, dtype); });
+    if (!h->run_graph) return fail("aigar_run: graph capture failed");
+    h->run_key = *p;
+    h->run_out = obs_out;
+    h->run_dtype = obs_out ? dtype : -1;
+  }
+  for (int t = 0; t < n_steps; t++) {
+    Mark m(h, "run");
+    if (h->run_graph) HIPCHK(hipGraphLaunch(h->run_graph, h->stream));
+    else launch_env_step(h, h->stream, *p, obs_out, dtype);
   }
   HIPCHK(hipGetLastError());
   return 0;

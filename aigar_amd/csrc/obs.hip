@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
 
   const int gp = blockIdx.x, lane = threadIdx.x;
   const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
+  if (epoch == 0) epoch = *d.ob_epoch;  // graph replay (aigar_run): the tick's closing kernel set it
 #ifdef AIGAR_OBS_TIMING
   __shared__ unsigned long long obs_ts_l[OBS_TS];
   if (lane == 0) obs_ts_l[5] = (unsigned long long)__smid();
@@ -875,6 +876,9 @@ __global__ void k_player_fov(Dev d) {
     rb = f.rmax;
   }
   wave_atomic_max_pos(&d.ctl[a].rmax_cell, rb);  // (per-lane atomics when a wave spans arenas)
+  // a fresh overflow-pool epoch for an observe replayed from a graph (epoch
+  // argument 0); host-issued observes pass epochs below 2^31, these sit above
+  if (gp == 0) *d.ob_epoch = 0x80000000u | ((*d.ob_epoch + 1) & 0x7FFFFFFFu);
 }
 void launch_player_fov(const Dev &d, hipStream_t s) {
   hipLaunchKernelGGL(k_player_fov, dim3((d.NP + 255) / 256), dim3(256), 0, s, d);

@@ -10,6 +10,10 @@ rank steps its own C3 arena (independent replicas, weak scaling, no collective
 in the data path); the timed region is bracketed by barrier + synchronize and
 the max over ranks is taken.
 
+The timed steps are issued with aigar_run: each step (policy + tick +
+observation) is one hipGraph replay.  The per-phase breakdown and the roofline
+kernel's duration come from the following steps issued as separate calls.
+
 Prints ONE JSON line (rank 0).  Extra objects: "roofline" for the dominant
 kernel (k_observe, HIP-event timed live on the stepper's stream) and
 "cpu_baseline" (the C oracle, i.e. a single-thread CPU port of the reference,
@@ -67,7 +71,12 @@ def pmc_traffic(kernel_prefix, workload):
     summary (profiles/r*_pmc_<workload>.json, written by tools/pmc.sh +
     tools/pmc_summary.py on the same bench command).  None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % workload)))
+    import re
+
+    def version(f):  # profiles/r01_v18_pmc_c3.json -> (1, 18): numeric, not lexicographic
+        m = re.search(r"r(\d+)_v(\d+)_pmc", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % workload)), key=version)
     if not files:
         return None, None
     data = json.load(open(files[-1]))
@@ -157,7 +166,10 @@ def main():
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
     stp.reset(replicas.rank_seed(args.seed, rank))
 
-    def one_step():
+    def run(n):  # n whole steps (policy + tick + observation), one graph replayed n times
+        stp.run(n, args.policy, obs, p_split=ps, p_eject=pe, seed=args.seed, greedy_split=True)
+
+    def one_step():  # the same step as separate calls, each bracketed by HIP events
         if args.policy == "greedy":
             stp.policy_greedy(True)
         else:
@@ -165,27 +177,31 @@ def main():
         stp.step(1)
         stp.observe(obs)
 
-    for _ in range(args.warmup):
-        one_step()
+    run(args.warmup)
     torch.cuda.synchronize()
     stp.sync()
     stats = stp.player_stats()
-    stp.profile(True)
     replicas.barrier(dist)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
+    run(args.steps)
     torch.cuda.synchronize()
     replicas.barrier(dist)
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    stp.sync()  # raises on any device-side capacity error
+    elapsed = replicas.max_over_ranks(dist, elapsed, device="cuda")
+    # per-phase breakdown and the roofline kernel's duration: the next
+    # min(steps, 50) steps issued as separate calls, HIP events on the stepper's stream
+    stp.profile(True)
+    for _ in range(min(args.steps, 50)):
+        one_step()
+    torch.cuda.synchronize()
     obs_ms, obs_n = stp.kernel_time("observe")
     tick_ms, tick_n = stp.kernel_time("tick")
     pol_ms, pol_n = stp.kernel_time("policy")
     stp.profile(False)
-    stp.sync()  # raises on any device-side capacity error
-    elapsed = replicas.max_over_ranks(dist, elapsed, device="cuda")
+    stp.sync()
     st = stp.get_state()
     work = stp.counters()
     value = replicas.job_throughput(bots * args.steps, world, elapsed)

@@ -148,7 +148,9 @@ int aigar_set_commands(aigar_handle *h, const double *cmd, int on_device);
 
 /* Synthetic bot population on the device (benchmark / smoke driver): every
  * alive player draws an action in [0,1]^2 mapped through the reference's
- * set_command_point (bot.py:550-577) and splits/ejects with p_split/p_eject. */
+ * set_command_point (bot.py:550-577) and splits/ejects with p_split/p_eject.
+ * The draws are Philox-keyed by (world key, seed, tick, player): a function of
+ * the state, not of how many times the policy was called. */
 int aigar_policy_random(aigar_handle *h, double p_split, double p_eject, uint64_t seed);
 
 /* Model.takeBotActions for Greedy bots (bot.py:252-269 -> make_greedy_bot_move
@@ -182,6 +184,28 @@ int aigar_rewards(aigar_handle *h, double *out, const aigar_reward_params *p, in
 
 /* n_ticks x Field.update() with the current commands (field.py:85-92). */
 int aigar_step(aigar_handle *h, int n_ticks);
+
+/* One whole batched env step, n_steps times: the bot policy (Model.takeBotActions,
+ * model.py:100-105), Field.update() (field.py:85-92) and, when obs_out is not
+ * NULL, every bot's getStateRepresentation (bot.py:272-299) into the DEVICE
+ * buffer obs_out[A*B][aigar_obs_len()] (dtype as aigar_observe).  The step is
+ * captured once as a single hipGraph (re-captured when the parameters or the
+ * buffer change) and replayed, so no host round trip separates the phases.
+ * policy: AIGAR_POLICY_NONE keeps the current commands; RANDOM is
+ * aigar_policy_random(p_split, p_eject, seed);
+ * GREEDY is aigar_policy_greedy for every player.  With AIGAR_FLAG_EVENTS the
+ * event log holds the events of all n_steps of the call. */
+#define AIGAR_POLICY_NONE   0
+#define AIGAR_POLICY_RANDOM 1
+#define AIGAR_POLICY_GREEDY 2
+typedef struct aigar_run_params {
+  int32_t policy;        /* AIGAR_POLICY_*                                   */
+  int32_t greedy_split;  /* ENABLE_GREEDY_SPLIT (networkParameters.py:17)    */
+  double p_split;        /* RANDOM: split probability per bot-tick           */
+  double p_eject;        /* RANDOM: eject probability per bot-tick           */
+  uint64_t seed;         /* RANDOM: Philox salt                              */
+} aigar_run_params;
+int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p, void *obs_out, int dtype);
 
 /* Bot.getStateRepresentation() for every player (bot.py:272-497):
  * out[A*B][aigar_obs_len()] (dtype 0 = float64, 1 = float32); dead players get NaN.

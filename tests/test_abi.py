@@ -36,13 +36,14 @@ def test_library_exports_every_declared_symbol():
 
 def test_struct_layouts_match_header():
     # sizes of the ctypes mirrors vs a C compile of the header
-    src = '#include "%s"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%%zu %%zu %%zu %%zu\\n", ' \
+    src = '#include "%s"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%%zu %%zu %%zu %%zu %%zu\\n", ' \
           'sizeof(aigar_config), sizeof(aigar_state), offsetof(aigar_state, players_f), ' \
-          'sizeof(aigar_reward_params));return 0;}' % HEADER
+          'sizeof(aigar_reward_params), sizeof(aigar_run_params));return 0;}' % HEADER
     exe = "/tmp/aigar_hdr_check"
     subprocess.run(["gcc", "-x", "c", "-", "-o", exe], input=src.encode(), check=True)
-    cfg, st, off, rp = map(int, subprocess.check_output([exe]).split())
+    cfg, st, off, rp, run = map(int, subprocess.check_output([exe]).split())
     assert rp == C.sizeof(_abi.RewardParams)
+    assert run == C.sizeof(_abi.RunParams)
     assert cfg == C.sizeof(_abi.Config)
     assert st == C.sizeof(_abi.State)
     assert off == _abi.State.players_f.offset

@@ -1,0 +1,96 @@
+"""aigar_run: the whole env step (policy + Field.update + observation) replayed
+from one hipGraph must give exactly what the separate calls give -- same world,
+same observation rows -- and the graph must be re-captured when its parameters
+or its output buffer change."""
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import make_config
+import parity
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+_lib = pytest.importorskip("aigar_amd._lib")
+
+CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_SLF
+      | _abi.OBS_SELF_LF | _abi.OBS_ENEMY_SLF | _abi.OBS_ENEMY_LF)
+
+
+def _cfg(bots=96, arenas=1):
+    return make_config(n_arenas=arenas, bots=bots, virus=True, max_viruses=24, channels=CH, extras=0x1F)
+
+
+def _pair(cfg, seed):
+    a, b = _lib.Stepper(cfg), _lib.Stepper(cfg)
+    for s in (a, b):
+        s.set_stream(torch.cuda.current_stream().cuda_stream)
+        s.reset(seed)
+    return a, b
+
+
+@pytest.mark.parametrize("policy", ["random", "greedy"])
+def test_run_matches_separate_calls(policy):
+    cfg = _cfg()
+    fused, sep = _pair(cfg, 21)
+    oa = torch.zeros((fused.NP, fused.obs_len), dtype=torch.float64, device="cuda")
+    ob = torch.zeros_like(oa)
+    for t in range(30):
+        fused.run(1, policy, oa, p_split=0.05, p_eject=0.05, seed=3, greedy_split=True)
+        if policy == "random":
+            sep.policy_random(0.05, 0.05, 3)
+        else:
+            sep.policy_greedy(True)
+        sep.step(1)
+        sep.observe(ob)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0)), t
+    assert parity.diff_states(fused.get_state(), sep.get_state(), ftol=0.0) == []
+    fused.close()
+    sep.close()
+
+
+def test_run_multi_step_float32_and_recapture():
+    cfg = _cfg(bots=64, arenas=2)
+    fused, sep = _pair(cfg, 4)
+    o32 = torch.zeros((fused.NP, fused.obs_len), dtype=torch.float32, device="cuda")
+    r32 = torch.zeros_like(o32)
+    fused.run(5, "random", o32, p_split=0.1, p_eject=0.1, seed=8)  # 5 replays of one graph
+    for _ in range(5):
+        sep.policy_random(0.1, 0.1, 8)
+        sep.step(1)
+        sep.observe(r32)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(o32, nan=-7.0), torch.nan_to_num(r32, nan=-7.0))
+    # new parameters and no observation: a new graph, same world as the separate calls
+    fused.run(3, "random", None, p_split=0.0, p_eject=0.3, seed=9)
+    for _ in range(3):
+        sep.policy_random(0.0, 0.3, 9)
+        sep.step(1)
+    for a in range(2):
+        assert parity.diff_states(fused.get_state(a), sep.get_state(a), ftol=0.0) == []
+    # policy "none" keeps externally set commands
+    cmd = np.random.default_rng(1).uniform(0, 300, (fused.NP, 4))
+    cmd[:, 2:] = 0
+    fused.set_commands(cmd)
+    sep.set_commands(cmd)
+    fused.run(2, "none", o32)
+    sep.step(1)
+    sep.observe(r32)
+    sep.step(1)
+    sep.observe(r32)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(o32, nan=-7.0), torch.nan_to_num(r32, nan=-7.0))
+    fused.close()
+    sep.close()
+
+
+def test_run_rejects_host_buffers_and_bad_policy():
+    g = _lib.Stepper(_cfg(bots=8))
+    g.reset(1)
+    with pytest.raises(ValueError):
+        g.run(1, "random", np.zeros((g.NP, g.obs_len)))
+    with pytest.raises(KeyError):
+        g.run(1, "bogus")
+    g.close()
