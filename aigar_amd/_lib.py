@@ -229,7 +229,7 @@ class Stepper:
                                               C.byref(n)))
         return out
 
-    COUNTERS = ("vb_serial", "pv_serial", "pellet_serial", "blob_serial", "pp_serial_players", "-", "-", "ticks")
+    COUNTERS = ("vb_serial", "pv_serial", "food_serial", "-", "pp_serial_players", "-", "-", "ticks")
 
     def counters(self, arena=0):
         out = np.zeros(8, np.int64)

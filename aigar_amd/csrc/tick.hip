@@ -768,8 +768,15 @@ __device__ __forceinline__ int cgrid_bucket(const Dev &d, double x, double y) {
 __device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int parity) {
   return d.cgcnt + ((size_t)a * 2 + parity) * CG_STRIDE;
 }
-__global__ void __launch_bounds__(256) k_cgrid_count(Dev d) {
-  const int a = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x, per = kMaxCells * d.B;
+// block bodies; they run as extra blocks of the food-phase kernels (k_food_prep,
+// k_food_commit round 1): eating changes masses and radii, never positions, and
+// the player-cell grid is first read by playerPlayerOverlap
+__device__ __forceinline__ int cgrid_blocks(const Dev &d) {  // per arena, count and scatter alike
+  const int cc = cgrid_cols(d);
+  return (int)((std::max((long)kMaxCells * d.B, (long)cc * cc + 1) + 255) / 256);
+}
+__device__ void cgrid_count_block(const Dev &d, int a, int bx) {
+  const int i = bx * 256 + threadIdx.x, per = kMaxCells * d.B;
   const int cc = cgrid_cols(d), par = d.ctl[a].tick & 1;
   if (i <= cc * cc) cgrid_counts(d, a, par ^ 1)[i] = 0;  // next tick's counts
   const bool in = i < per;
@@ -786,11 +793,11 @@ __global__ void __launch_bounds__(256) k_cgrid_count(Dev d) {
   if (!ok) return;
   d.c_rank[(size_t)a * per + i] = atomicAdd(&cgrid_counts(d, a, par)[cgrid_bucket(d, x, y)], 1);
 }
-__global__ void __launch_bounds__(256) k_cgrid_scatter(Dev d) {
+__device__ void cgrid_scatter_block(const Dev &d, int a, int bx) {
   __shared__ int sc[CG_STRIDE];
   __shared__ int wsum[4];
-  const int a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i = blockIdx.x * 256 + tid, per = kMaxCells * d.B;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = bx * 256 + tid, per = kMaxCells * d.B;
   const int cc = cgrid_cols(d), n = cc * cc;  // buckets (start[n] = total)
   // this thread's cell first (independent of the scan): its loads overlap the counts'
   const bool in = i < per;
@@ -837,7 +844,7 @@ __global__ void __launch_bounds__(256) k_cgrid_scatter(Dev d) {
   }
   if (tid == 0) sc[n] = total;
   __syncthreads();
-  if (blockIdx.x == 0) {
+  if (bx == 0) {
     int *start = d.cstart + (size_t)a * (d.H + 1);
     for (int j = tid; j <= n; j += 256) start[j] = sc[j];
   }
@@ -1454,49 +1461,64 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
 }
 
 // ------------------------------------------------------------ T14/T15 food
-// foods: KIND 0 pellets (eat-phase buffer 1, records sorted by bucket), 1 blobs
-// Pellets of the eat phase: the current bucket-sorted buffer, indices [0, n0),
-// plus this tick's blob conversions (addPellet in updateBlobs), still in the
-// staging list, as indices [n0, n0 + nst) -- they join the sorted buffer at the
-// closing rebuild, so no rebuild runs before the eat phase.  Dead flags and
-// reservation words are indexed by the same j.
-template <int KIND>
+// playerPelletOverlap then playerBlobOverlap (field.py:200-222) as ONE
+// reservation pass.  The reference eats every pellet (all players, all cells)
+// before any blob, but a cell's blob turn depends only on its own mass after
+// its pellet turn and on the blobs lower-priority cells ate: no pellet turn of
+// another cell and no blob turn of any other cell touches either.  So the
+// sequential order "per cell (player order, list order): its pellets, then its
+// blobs" gives the same world, and one reservation pass with a combined
+// per-cell food list (pellets by creation sequence, then blobs by creation
+// sequence) resolves both phases.  Events keep their reference phase keys.
+//
+// Foods are coded j: pellets j in [0, n0) (the current bucket-sorted buffer)
+// and [n0, n0 + nst) (this tick's blob conversions, addPellet in updateBlobs,
+// still in the staging list -- they join the sorted buffer at the closing
+// rebuild, so no rebuild runs before the eat phase); blobs kBlobBit | slot.
+// Pellet dead flags and reservation words are indexed by a * Pcap + j.
+constexpr int kBlobBit = 1 << 30;
 struct Food {
   const Dev &d;
   int a, pb;  // pb: the eat-phase pellet buffer (ArenaCtl::peat)
   int n0, nst;
   __device__ Food(const Dev &dd, int aa)
-      : d(dd), a(aa), pb(KIND == 0 ? dd.ctl[aa].peat : 0), n0(KIND == 0 ? dd.ctl[aa].n_pel : 0),
-        nst(KIND == 0 ? dd.ctl[aa].n_pnew : 0) {}
-  __device__ size_t g(int j) const { return (size_t)a * (KIND == 0 ? d.Pcap : d.Ecap) + j; }
-  __device__ size_t gs(int j) const { return (size_t)a * d.Pcap + (j - n0); }  // staging slot
-  __device__ double x(int j) const { return KIND == 0 ? (j < n0 ? d.pel_x[pb][g(j)] : d.pn_x[gs(j)]) : d.b_x[g(j)]; }
-  __device__ double y(int j) const { return KIND == 0 ? (j < n0 ? d.pel_y[pb][g(j)] : d.pn_y[gs(j)]) : d.b_y[g(j)]; }
-  __device__ double m(int j) const { return KIND == 0 ? (j < n0 ? d.pel_m[pb][g(j)] : d.pn_m[gs(j)]) : d.b_m[g(j)]; }
-  __device__ double r(int j) const { return KIND == 0 ? radius_of(m(j)) : d.b_r[g(j)]; }
+      : d(dd), a(aa), pb(dd.ctl[aa].peat), n0(dd.ctl[aa].n_pel), nst(dd.ctl[aa].n_pnew) {}
+  __device__ static bool blob(int j) { return (j & kBlobBit) != 0; }
+  __device__ size_t g(int j) const { return (size_t)a * d.Pcap + j; }               // pellet j
+  __device__ size_t gs(int j) const { return (size_t)a * d.Pcap + (j - n0); }       // staged pellet j
+  __device__ size_t gb(int j) const { return (size_t)a * d.Ecap + (j & ~kBlobBit); }  // blob
+  __device__ double x(int j) const { return blob(j) ? d.b_x[gb(j)] : (j < n0 ? d.pel_x[pb][g(j)] : d.pn_x[gs(j)]); }
+  __device__ double y(int j) const { return blob(j) ? d.b_y[gb(j)] : (j < n0 ? d.pel_y[pb][g(j)] : d.pn_y[gs(j)]); }
+  __device__ double m(int j) const { return blob(j) ? d.b_m[gb(j)] : (j < n0 ? d.pel_m[pb][g(j)] : d.pn_m[gs(j)]); }
+  __device__ double r(int j) const { return blob(j) ? d.b_r[gb(j)] : radius_of(m(j)); }
   __device__ int64_t seq(int j) const {
-    return KIND == 0 ? (j < n0 ? d.pel_seq[pb][g(j)] : d.pn_seq[gs(j)]) : d.b_seq[g(j)];
+    return blob(j) ? d.b_seq[gb(j)] : (j < n0 ? d.pel_seq[pb][g(j)] : d.pn_seq[gs(j)]);
   }
-  // the staged conversions as extra candidates of a grid walk (f as for wave_grid_for)
-  template <class Fn>
-  __device__ void for_staged(Fn f) const {
-    if (KIND != 0) return;
-    const int lane = threadIdx.x & 63;
-    for (int t0 = 0; t0 < nst; t0 += 64) f(t0 + lane < nst, n0 + t0 + lane);
-  }
-  __device__ bool alive(int j) const { return KIND == 0 ? !d.pel_dead[g(j)] : (d.b_flags[g(j)] & F_ALIVE); }
-  __device__ int64_t ej(int j) const { return KIND == 0 ? -2 : d.b_ej[g(j)]; }
+  __device__ bool alive(int j) const { return blob(j) ? (d.b_flags[gb(j)] & F_ALIVE) != 0 : !d.pel_dead[g(j)]; }
+  __device__ int64_t ej(int j) const { return blob(j) ? d.b_ej[gb(j)] : -2; }
   __device__ void kill(int j) const {
-    if (KIND == 0) d.pel_dead[g(j)] = 1;
-    else {
-      d.b_flags[g(j)] = 0;
+    if (!blob(j)) {
+      d.pel_dead[g(j)] = 1;
+    } else {
+      d.b_flags[gb(j)] = 0;
       atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
     }
   }
-  __device__ uint64_t *owner(int j) const { return (KIND == 0 ? d.pel_owner : d.b_owner) + g(j); }
-  __device__ const int *start() const { return (KIND == 0 ? d.pstart : d.bstart) + (size_t)a * (d.H + 1); }
-  __device__ const int *items() const { return KIND == 0 ? nullptr : d.bitems + (size_t)a * d.Ecap; }
-  __device__ int shift() const { return KIND == 0 ? 0 : d.cshift; }  // blob grid is coarsened
+  __device__ uint64_t *owner(int j) const { return blob(j) ? d.b_owner + gb(j) : d.pel_owner + g(j); }
+  __device__ bool any_blobs() const { return d.ctl[a].n_blob > 0; }
+  // every pellet / blob whose footprint may touch q: f(valid, j) on all lanes (wave-uniform calls)
+  template <class Fn>
+  __device__ void walk_pellets(Rect q, Fn f) const {
+    wave_grid_for(d.pstart + (size_t)a * (d.H + 1), nullptr, d.cols, q, 1, f, 0, n0, nst);  // (+ staged)
+  }
+  template <class Fn>
+  __device__ void walk_blobs(Rect q, Fn f) const {
+    if (any_blobs())
+      wave_grid_for(d.bstart + (size_t)a * (d.H + 1), d.bitems + (size_t)a * d.Ecap, d.cols, q, 1,
+                    [&](bool valid, int j) { f(valid, valid ? (j | kBlobBit) : -1); }, d.cshift);
+  }
+  // order of a cell's food list: pellets by creation sequence, then blobs
+  __device__ static int64_t order_key(int j, int64_t sq) { return sq | (blob(j) ? (1ll << 62) : 0); }
 };
 // reservation key: higher round wins, within a round the lower priority wins.
 // Rounds are global per arena and only grow (ArenaCtl::food_round), so stale
@@ -1518,15 +1540,19 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// For every cell, the foods it could possibly eat this phase (R set, sorted by
-// creation sequence) and the round-1 reservation.  One wavefront per player:
-// lanes scan the candidate buckets in parallel, ballot-compact into LDS, rank
-// by sequence.  Cells with more than PREP_CAND candidates or FCAP foods in
-// reach reserve everything they may touch with a key that dominates all rounds
-// and are resolved by the serial pass.
+// For every cell, the foods it could possibly eat this phase (R set, pellets
+// then blobs, each by creation sequence) and the round-1 reservation.  One
+// wavefront per player: lanes scan the candidate buckets in parallel,
+// ballot-compact into LDS, rank by (kind, sequence).  Cells with more than
+// PREP_CAND candidates or FCAP foods in reach reserve everything they may touch
+// with a key that dominates all rounds and are resolved by the serial pass.
 constexpr int PREP_CAND = 128;
-template <int KIND>
 __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
+  const int nprep = (d.NP + 3) / 4;
+  if ((int)blockIdx.x >= nprep) {  // extra blocks: player-cell grid counts
+    const int e = blockIdx.x - nprep, nb = cgrid_blocks(d);
+    return cgrid_count_block(d, e / nb, e % nb);
+  }
   __shared__ int64_t s_seq[4][PREP_CAND];
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
   __shared__ int s_idx[4][PREP_CAND];
@@ -1536,12 +1562,8 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
   if (gp < d.NP && gp % d.B == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP || !d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
-  if (KIND == 1 && d.ctl[a].n_blob == 0) return;  // no blobs: nothing to reserve (commit skips too)
-  Food<KIND> F(d, a);
+  Food F(d, a);
   const uint32_t base = d.ctl[a].food_round;
-  const int cols = d.cols;
-  const int *st = F.start();
-  const int *items = F.items();
   int n = d.p_ncells[gp];
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
@@ -1554,7 +1576,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
     auto visit = [&](bool valid, int j) {
       bool keep = false;
       double fx = 0, fy = 0, fm = 0;
-      if (valid && F.alive(j) && F.ej(j) != cseq) {
+      if (valid && F.alive(j) && F.ej(j) != cseq) {  // a blob's own ejecter cell skips it (field.py:219)
         fx = F.x(j);
         fy = F.y(j);
         fm = F.m(j);
@@ -1565,7 +1587,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
       if (keep) {
         lsum += fm;
         if (slot < PREP_CAND) {
-          s_seq[w][slot] = F.seq(j);
+          s_seq[w][slot] = Food::order_key(j, F.seq(j));
           s_x[w][slot] = fx;
           s_y[w][slot] = fy;
           s_m[w][slot] = fm;
@@ -1574,7 +1596,36 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
       }
       cnt += __popcll(bal);
     };
-    wave_grid_for(st, items, cols, q, 1, visit, F.shift(), F.n0, F.nst);  // (+ staged conversions)
+    F.walk_pellets(q, visit);
+    // The blob turn's candidates are the blobs hashed in the buckets of the
+    // cell's box AFTER its pellet turn (field.py:215-222): walk the box of the
+    // largest radius the pellets can give (the eat loop applies the exact box).
+    const double Rp = fmax(r, radius_of(py_min(kMaxMass, (m + wave_sum(lsum)) * (1 + 1e-9))) * (1 + 1e-9));
+    const Rect qb = footprint(x, y, Rp, d.size);
+    auto visit_b = [&](bool valid, int j) {  // as visit, against the blob-turn box bound
+      bool keep = false;
+      double fx = 0, fy = 0, fm = 0;
+      if (valid && F.alive(j) && F.ej(j) != cseq) {  // a blob's own ejecter cell skips it (field.py:219)
+        fx = F.x(j);
+        fy = F.y(j);
+        fm = F.m(j);
+        keep = rect_hit(footprint(fx, fy, F.r(j), d.size), qb);
+      }
+      unsigned long long bal = __ballot(keep);
+      int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
+      if (keep) {
+        lsum += fm;
+        if (slot < PREP_CAND) {
+          s_seq[w][slot] = Food::order_key(j, F.seq(j));
+          s_x[w][slot] = fx;
+          s_y[w][slot] = fy;
+          s_m[w][slot] = fm;
+          s_idx[w][slot] = j;
+        }
+      }
+      cnt += __popcll(bal);
+    };
+    F.walk_blobs(qb, visit_b);
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
     double sum = wave_sum(lsum);
@@ -1610,17 +1661,12 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
           set_err(d, a, ERR_WORK_CAP);
         }
       }
-      const Span g = grid_span(q, 1, cols, F.shift());
-      for (int by = g.by0; by <= g.by1; by++) {
-        int lo = st[by * g.stride + g.bx0], hi = st[by * g.stride + g.bx1 + 1];
-        for (int t = lo + lane; t < hi; t += 64) {
-          int j = items ? items[t] : t;
-          if (F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q))
-            atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
-        }
-      }
-      F.for_staged([&](bool valid, int j) {
+      F.walk_pellets(q, [&](bool valid, int j) {
         if (valid && F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q))
+          atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
+      });
+      F.walk_blobs(qb, [&](bool valid, int j) {
+        if (valid && F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), qb))
           atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
       });
       continue;
@@ -1644,41 +1690,54 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
     wave_sync_lds();
   }
 }
-template <int KIND>
-__device__ void food_eat_loop(const Dev &d, const Food<KIND> &F, int a, size_t ci, uint32_t prio, const int *lst,
+// one eaten food: the event (in its reference phase), kill, growth
+// (eatCell -> adjustCellSize -> grow, field.py:327-344)
+__device__ __forceinline__ void food_eat(const Dev &d, const Food &F, int a, int j, uint32_t prio, int t,
+                                         int64_t cseq, int64_t fseq, double fm, double &m, double &r, int &eaten) {
+  const bool bl = Food::blob(j);
+  ev_push(d, a, bl ? PH_BLOB : PH_PELLET, ((uint64_t)prio << 16) | (uint64_t)t, bl ? 7 : 6, cseq, fseq);
+  m = grow_mass(m, fm);
+  r = radius_of(m);
+  F.kill(j);
+  eaten += bl ? 0 : 1;
+}
+__device__ bool food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, uint32_t prio, const int *lst,
                               int cnt) {
   double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
   int64_t cseq = d.c_seq[ci];
   int eaten = 0;
+  bool blobs = false, ate = false;
+  Rect qb{};
   for (int t = 0; t < cnt; t++) {
     int j = lst[t];
+    if (Food::blob(j) && !blobs) {  // the blob turn: candidates from the box after the pellet turn
+      blobs = true;
+      qb = footprint(x, y, r, d.size);
+    }
     if (!F.alive(j)) continue;
-    double fm = F.m(j);
-    if (!(overlap(x, y, m, r, F.x(j), F.y(j), fm, F.r(j)) && can_eat(m, fm))) continue;
-    ev_push(d, a, KIND == 0 ? PH_PELLET : PH_BLOB, ((uint64_t)prio << 16) | (uint64_t)t, KIND == 0 ? 6 : 7, cseq,
-            F.seq(j));
-    m = grow_mass(m, fm);  // eatCell -> adjustCellSize -> grow (field.py:337-344)
-    r = radius_of(m);
-    F.kill(j);
-    eaten++;
+    double fm = F.m(j), fx = F.x(j), fy = F.y(j), fr = F.r(j);
+    if (blobs && !rect_hit(footprint(fx, fy, fr, d.size), qb)) continue;
+    if (!(overlap(x, y, m, r, fx, fy, fm, fr) && can_eat(m, fm))) continue;
+    food_eat(d, F, a, j, prio, t, cseq, F.seq(j), fm, m, r, eaten);
+    ate = true;
   }
   d.c_m[ci] = m;
   d.c_r[ci] = r;
-  if (KIND == 0 && eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
+  if (eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
+  return ate;
 }
-template <int KIND>
-__global__ void k_food_commit(Dev d, int round, int last) {
-  int gp = GTID;
-  if (gp >= d.NP) return;
+// one player's cells in reservation round `round`; returns the largest radius
+// of its cells that ate (0: none) -- the player-cell grid's radius bound
+__device__ double food_commit_player(const Dev &d, int gp, int round, int last) {
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   ArenaCtl &c = d.ctl[a];
   // round r reads how many cells failed round r-1 (nothing left: skip), counts
   // its own failures, and clears the counter round r+1 will use
-  if (round > 1 && c.food_undone[(round - 1) % 3] == 0) return;
+  if (round > 1 && c.food_undone[(round - 1) % 3] == 0) return 0;
   if (p == 0) c.food_undone[(round + 1) % 3] = 0;
-  if (!d.p_alive[gp]) return;
-  if (KIND == 1 && c.n_blob == 0) return;
-  Food<KIND> F(d, a);
+  if (!d.p_alive[gp]) return 0;
+  double rgrow = 0;
+  Food F(d, a);
   int n = d.p_ncells[gp];
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
@@ -1693,7 +1752,7 @@ __global__ void k_food_commit(Dev d, int round, int last) {
       for (int t = 0; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
     }
     if (own) {
-      food_eat_loop<KIND>(d, F, a, ci, prio, lst, cnt);
+      if (food_eat_loop(d, F, a, ci, prio, lst, cnt)) rgrow = fmax(rgrow, d.c_r[ci]);
       d.f_done[ci] = 1;
     } else if (!last) {
       // reserve for the next round right away.  Safe without a separate pass: a
@@ -1714,13 +1773,23 @@ __global__ void k_food_commit(Dev d, int round, int last) {
       }
     }
   }
+  return rgrow;
+}
+__global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last) {
+  const int ncommit = (d.NP + 255) / 256;
+  if ((int)blockIdx.x >= ncommit) {  // extra blocks (round 1): player-cell grid scatter
+    const int e = blockIdx.x - ncommit, nb = cgrid_blocks(d);
+    return cgrid_scatter_block(d, e / nb, e % nb);
+  }
+  const int gp = GTID;
+  const double rg = gp < d.NP ? food_commit_player(d, gp, round, last) : 0.0;
+  wave_atomic_max_pos(&d.ctl[min(gp, d.NP - 1) / d.B].rmax_cell, rg);
 }
 // Cells the reservation rounds could not settle, in priority order (player,
 // list position), one wavefront per arena.  The sequential eat loop runs on
 // all lanes uniformly; each cell's candidates are gathered lane-parallel with
 // their state into LDS (within one cell's turn only that cell changes them).
 constexpr int FS_CAP = 512;
-template <int KIND>
 __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
   __shared__ int64_t s_key[FS_CAP];
   __shared__ int s_val[FS_CAP], s_srt[FS_CAP];
@@ -1731,11 +1800,11 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
   wave_fence();
   if (lane == 0) {
     c.n_pend = 0;
-    c.stat[2 + KIND] += nw;
+    c.stat[2] += nw;
     c.food_round += rounds + 2;  // next phase's keys dominate every key written in this one
   }
   if (nw == 0) return;
-  Food<KIND> F(d, a);
+  Food F(d, a);
   int *w = d.work + (size_t)a * d.Wcap;
   int *wp = d.work2 + (size_t)a * d.Wcap;
   if (nw <= FS_CAP) {  // priority order: rank sort in LDS (priorities are unique)
@@ -1769,6 +1838,8 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
     const double x = d.c_x[ci], y = d.c_y[ci];
     double m = d.c_m[ci], r = d.c_r[ci];
     const int64_t cseq = d.c_seq[ci];
+    int eaten = 0, t_base = 0;
+    for (int kind = 0; kind < 2; kind++) {  // pellet turn, then blob turn (box after the pellets)
     const Rect q = footprint(x, y, r, d.size);
     int nc = 0;
     auto gather = [&](bool valid, int j) {
@@ -1778,13 +1849,13 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
         fx = F.x(j);
         fy = F.y(j);
         fm = F.m(j);
-        fr = KIND == 0 ? radius_of(fm) : F.r(j);
+        fr = F.r(j);
         keep = rect_hit(footprint(fx, fy, fr, d.size), q);
       }
       unsigned long long bal = __ballot(keep);
       int slot = nc + __popcll(bal & lt);
       if (keep && slot < FS_CAP) {
-        s_key[slot] = F.seq(j);
+        s_key[slot] = Food::order_key(j, F.seq(j));
         s_val[slot] = j;
         s_x[slot] = fx;
         s_y[slot] = fy;
@@ -1793,38 +1864,42 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
       }
       nc += __popcll(bal);
     };
-    wave_grid_for(F.start(), F.items(), d.cols, q, 1, gather, F.shift(), F.n0, F.nst);  // (+ staged conversions)
+    if (kind == 0) F.walk_pellets(q, gather);
+    else F.walk_blobs(q, gather);
     if (nc > FS_CAP) {
       set_err(d, a, ERR_CAND_CAP);
       nc = FS_CAP;
     }
     wave_fence();
-    for (int k = lane; k < nc; k += 64) {  // candidate order: creation sequence
+    for (int k = lane; k < nc; k += 64) {  // candidate order: pellets, then blobs, each by creation sequence
       int64_t key = s_key[k];
       int rk = 0;
       for (int y = 0; y < nc; y++) rk += s_key[y] < key;
       s_srt[rk] = k;
     }
     wave_fence();
-    int eaten = 0;
     for (int t = 0; t < nc; t++) {  // food_eat_loop, on the turn-start snapshot
       const int k = s_srt[t];
       const double fm = s_m[k];
       if (!(overlap(x, y, m, r, s_x[k], s_y[k], fm, s_r[k]) && can_eat(m, fm))) continue;
+      const int j = s_val[k];
+      const int64_t fseq = s_key[k] & ~(1ll << 62);
       if (lane == 0) {
-        ev_push(d, a, KIND == 0 ? PH_PELLET : PH_BLOB, ((uint64_t)prio << 16) | (uint64_t)t, KIND == 0 ? 6 : 7, cseq,
-                s_key[k]);
-        F.kill(s_val[k]);
+        food_eat(d, F, a, j, prio, t_base + t, cseq, fseq, fm, m, r, eaten);
+      } else {
+        m = grow_mass(m, fm);
+        r = radius_of(m);
       }
-      m = grow_mass(m, fm);  // eatCell -> adjustCellSize -> grow (field.py:337-344)
-      r = radius_of(m);
-      eaten++;
+    }
+    t_base += nc;
+    wave_fence();  // this sub-turn's kills are read by the next gather
     }
     if (lane == 0) {
       d.c_m[ci] = m;
       d.c_r[ci] = r;
       d.f_done[ci] = 1;
-      if (KIND == 0 && eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
+      if (eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
+      atomic_max_pos(&c.rmax_cell, r);  // (radii only grow while eating)
     }
     wave_fence();  // kills and the new mass are read by the next cell's gather
   }
@@ -2418,14 +2493,19 @@ static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start, int f
   hipLaunchKernelGGL(k_grid_scatter<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
 }
 
-template <int KIND>
+// playerPelletOverlap + playerBlobOverlap: prep, reservation rounds, serial rest;
+// the player-cell grid (counts, scatter) rides along as extra blocks of the
+// prep and of the first round
 static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
-  int g = nblk(d.NP, 256);
-  hipLaunchKernelGGL(k_food_prep<KIND>, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d, rounds);
+  const int g = nblk(d.NP, 256);
+  const long per = (long)kMaxCells * d.B;
+  const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
+  const int ncg = nblk(std::max(per, (long)cc * cc + 1), 256) * d.A;
+  hipLaunchKernelGGL(k_food_prep, dim3(nblk(d.NP, 4) + ncg), dim3(256), 0, s, d, rounds);
   for (int r = 1; r <= rounds; r++) {
-    hipLaunchKernelGGL(k_food_commit<KIND>, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
+    hipLaunchKernelGGL(k_food_commit, dim3(g + (r == 1 ? ncg : 0)), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
   }
-  hipLaunchKernelGGL(k_food_serial<KIND>, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
+  hipLaunchKernelGGL(k_food_serial, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
 }
 
 void launch_player_fov(const Dev &d, hipStream_t s);
@@ -2447,14 +2527,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
     hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
   }
-  {  // player-cell grid (coarse): counts + scatter with an in-block scan
-    const long per = (long)kMaxCells * d.B;
-    const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
-    hipLaunchKernelGGL(k_cgrid_count, dim3(nblk(std::max(per, (long)cc * cc + 1), 256), d.A), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_cgrid_scatter, dim3(nblk(per, 256), d.A), dim3(256), 0, s, d);
-  }
-  launch_food<0>(d, s, rounds, scr);
-  launch_food<1>(d, s, 1, scr);  // blob conflicts are rare: one reservation round, the rest serial
+  launch_food(d, s, rounds, scr);
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);  // + end-of-tick virus grid

@@ -47,8 +47,9 @@ WORKLOADS = {
 }
 
 
-def make_cfg(name, device=0, flags=0):
-    bots, field, pellets, virus, _, _, ch, ex, arenas = WORKLOADS[name]
+def make_cfg(name, device=0, flags=0, arenas=None):
+    bots, field, pellets, virus, _, _, ch, ex, arenas0 = WORKLOADS[name]
+    arenas = arenas0 if arenas is None else arenas
     c = _abi.Config()
     c.n_arenas, c.bots_per_arena, c.field_size = arenas, bots, field
     c.virus_enabled = int(virus)
@@ -141,6 +142,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--arenas", type=int, default=None,
+                    help="independent arenas per GPU (default: the workload's own; >1 = batched-env scale sweep)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=1234)
@@ -159,8 +162,10 @@ def main():
 
     name = args.workload
     bots, field, pellets, virus, ps, pe, ch, ex, arenas = WORKLOADS[name]
+    if args.arenas:
+        arenas = args.arenas
     bots *= arenas  # players stepped per GPU
-    stp = _lib.Stepper(make_cfg(name, device=local))
+    stp = _lib.Stepper(make_cfg(name, device=local, arenas=arenas))
     stream = torch.cuda.current_stream()
     stp.set_stream(stream.cuda_stream)
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")

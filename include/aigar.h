@@ -238,7 +238,7 @@ int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *laun
 
 /* Diagnostics: per-arena work counters accumulated since reset/load_state --
  * out[0..n) of: serial work-list entries of virusBlobOverlap, playerVirusOverlap,
- * pellet eating, blob eating, playerPlayerOverlap (players), -, -, ticks.  n <= 8. */
+ * pellet + blob eating (cells), -, playerPlayerOverlap (players), -, -, ticks.  n <= 8. */
 int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n);
 
 /* Diagnostics: evaluate the device's correctly rounded pow (aigar_math.h) on
