@@ -127,5 +127,25 @@ __device__ inline void store_player_fov(const Dev &d, int gp) {
   d.p_fs[gp] = f.fs;
   d.p_mass[gp] = f.mass;
 }
+// one thread of the end-of-tick FOV cache pass (every thread of the wave calls
+// it): getFovPos / getFovSize / getTotalMass (player.py:129,156-167) for the
+// observation and the policies, the largest cell radius for their grid walks,
+// and a fresh overflow-pool epoch for an observe replayed from a graph (epoch
+// argument 0; host-issued observes pass epochs below 2^31, these sit above)
+__device__ inline void fov_cache_thread(const Dev &d, int gp) {
+  const bool live = gp < d.NP && d.p_alive[gp];
+  double rb = 0;
+  const int a = gp < d.NP ? gp / d.B : 0;
+  if (live) {
+    const Fov f = player_fov(d, gp);
+    d.p_fx[gp] = f.fx;
+    d.p_fy[gp] = f.fy;
+    d.p_fs[gp] = f.fs;
+    d.p_mass[gp] = f.mass;
+    rb = f.rmax;
+  }
+  wave_atomic_max_pos(&d.ctl[a].rmax_cell, rb);  // (per-lane atomics when a wave spans arenas)
+  if (gp == 0) *d.ob_epoch = 0x80000000u | ((*d.ob_epoch + 1) & 0x7FFFFFFFu);
+}
 
 }  // namespace aigar

@@ -862,24 +862,7 @@ __global__ void k_set_commands(Dev d, const double *cmd) {
 
 // FOV cache of every live player, and the arena's largest cell radius (bounds
 // the cell-grid expansion of the observation and the next greedy moves)
-__global__ void k_player_fov(Dev d) {
-  const int gp = GTID;
-  const bool live = gp < d.NP && d.p_alive[gp];
-  double rb = 0;
-  int a = gp < d.NP ? gp / d.B : 0;
-  if (live) {
-    const Fov f = player_fov(d, gp);
-    d.p_fx[gp] = f.fx;
-    d.p_fy[gp] = f.fy;
-    d.p_fs[gp] = f.fs;
-    d.p_mass[gp] = f.mass;
-    rb = f.rmax;
-  }
-  wave_atomic_max_pos(&d.ctl[a].rmax_cell, rb);  // (per-lane atomics when a wave spans arenas)
-  // a fresh overflow-pool epoch for an observe replayed from a graph (epoch
-  // argument 0); host-issued observes pass epochs below 2^31, these sit above
-  if (gp == 0) *d.ob_epoch = 0x80000000u | ((*d.ob_epoch + 1) & 0x7FFFFFFFu);
-}
+__global__ void __launch_bounds__(256) k_player_fov(Dev d) { fov_cache_thread(d, GTID); }
 void launch_player_fov(const Dev &d, hipStream_t s) {
   hipLaunchKernelGGL(k_player_fov, dim3((d.NP + 255) / 256), dim3(256), 0, s, d);
 }

@@ -1092,7 +1092,12 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
   d.pel_seq[dst][o] = s;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
-__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode) {
+// fov_blocks > 0 (the tick's closing rebuild): the last fov_blocks blocks
+// refresh the FOV cache instead -- the player state is final by then, and the
+// pellet records the scatter moves are not part of it
+__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode, int fov_blocks) {
+  const int nsc = gridDim.x - fov_blocks;
+  if ((int)blockIdx.x >= nsc) return fov_cache_thread(d, (blockIdx.x - nsc) * 256 + threadIdx.x);
   pgrid_scatter_one(d, GTID, mode);
 }
 // ------------------------------------------------------------ T10 merge
@@ -1547,8 +1552,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 // PREP_CAND candidates or FCAP foods in reach reserve everything they may touch
 // with a key that dominates all rounds and are resolved by the serial pass.
 constexpr int PREP_CAND = 128;
+constexpr int PREP_WAVES = 1;  // wavefronts per player (wave h takes cells h, h + PREP_WAVES, ...; 2 measured slower)
 __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
-  const int nprep = (d.NP + 3) / 4;
+  const int nprep = (d.NP * PREP_WAVES + 3) / 4;
   if ((int)blockIdx.x >= nprep) {  // extra blocks: player-cell grid counts
     const int e = blockIdx.x - nprep, nb = cgrid_blocks(d);
     return cgrid_count_block(d, e / nb, e % nb);
@@ -1558,14 +1564,14 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
   __shared__ int s_idx[4][PREP_CAND];
   __shared__ uint8_t s_sel[4][PREP_CAND];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int gp = blockIdx.x * 4 + w;
-  if (gp < d.NP && gp % d.B == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
+  const int wi = blockIdx.x * 4 + w, gp = wi / PREP_WAVES, h = wi - gp * PREP_WAVES;
+  if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP || !d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   Food F(d, a);
   const uint32_t base = d.ctl[a].food_round;
   int n = d.p_ncells[gp];
-  for (int k = 0; k < n; k++) {
+  for (int k = h; k < n; k += PREP_WAVES) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
@@ -2481,7 +2487,8 @@ void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
   if (mode != PR_CLOSE) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, mode);
   hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt, mode,
                      mode == PR_CLOSE ? 1 : 0, 0);
-  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256)), dim3(256), 0, s, d, mode);
+  const int fovb = mode == PR_CLOSE ? nblk(d.NP, 256) : 0;  // closing rebuild: + the FOV cache
+  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256) + fovb), dim3(256), 0, s, d, mode, fovb);
 }
 
 template <int KIND>
@@ -2501,7 +2508,7 @@ static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
   const long per = (long)kMaxCells * d.B;
   const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
   const int ncg = nblk(std::max(per, (long)cc * cc + 1), 256) * d.A;
-  hipLaunchKernelGGL(k_food_prep, dim3(nblk(d.NP, 4) + ncg), dim3(256), 0, s, d, rounds);
+  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4) + ncg), dim3(256), 0, s, d, rounds);
   for (int r = 1; r <= rounds; r++) {
     hipLaunchKernelGGL(k_food_commit, dim3(g + (r == 1 ? ncg : 0)), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
   }
@@ -2534,11 +2541,12 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   const long n_spawn = (long)d.NP + (long)d.A * d.Pcap + (d.virus_enabled ? (long)d.A * d.Vcap : 0) +
                        (long)d.A * d.H;
   hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d);
-  // P1 survivors U spawns -> P0, FOV cache, epilogue closes the tick
-  // closing pellet rebuild, then the FOV cache (player state is final).  The FOV
-  // is its own launch: fused into the scatter it stretched that kernel ~5x.
-  launch_pellet_rebuild(d, s, PR_CLOSE);  // eat-phase survivors U spawns -> new current buffer
-  launch_player_fov(d, s);
+  // closing pellet rebuild (eat-phase survivors U spawns -> the new current
+  // buffer; the scan's epilogue closes the tick); the FOV cache runs as extra
+  // blocks of its scatter (player state is final by then).  Fused into the
+  // scatter's own threads it stretched that kernel ~5x; as separate blocks it
+  // only adds them to the grid.
+  launch_pellet_rebuild(d, s, PR_CLOSE);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty
