@@ -136,6 +136,30 @@ def cpu_baseline(name, budget_s=12.0, seed=1, policy="random"):
                       "steps, oracle/oracle.c single thread, %.1f s" % (name.upper(), n, policy, bots, dt)}
 
 
+def batched(name, arenas, policy, ps, pe, seed, device, steps=20, warmup=5):
+    """The same per-arena workload, `arenas` independent arenas stepped by the
+    same launches (batched-env mode, SURVEY.md §8e C5 pattern): what one MI355X
+    sustains when it is given enough work to fill it.  Reported beside `value`."""
+    import torch
+    from aigar_amd import _lib
+    bots = WORKLOADS[name][0] * arenas
+    stp = _lib.Stepper(make_cfg(name, device=device, arenas=arenas))
+    stp.set_stream(torch.cuda.current_stream().cuda_stream)
+    obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
+    stp.reset(seed + 1)
+    run = lambda n: stp.run(n, policy, obs, p_split=ps, p_eject=pe, seed=seed, greedy_split=True)
+    run(warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stp.sync()
+    stp.close()
+    return {"arenas": arenas, "bots": bots, "value": bots * steps / dt, "unit": "env-steps/s",
+            "ms_per_step": dt / steps * 1e3, "steps": steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,6 +168,9 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--arenas", type=int, default=None,
                     help="independent arenas per GPU (default: the workload's own; >1 = batched-env scale sweep)")
+    ap.add_argument("--batched-arenas", type=int, default=16,
+                    help="also time this many independent arenas of the same workload stepped together on "
+                         "the GPU (reported under 'batched', never as 'value'); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=1234)
@@ -253,6 +280,8 @@ def main():
                   "serial_work_per_tick": {k: round(v / max(1, work["ticks"]), 3) for k, v in work.items()
                                            if k != "ticks"}},
     }
+    if rank == 0 and world == 1 and args.batched_arenas > 1 and not args.arenas:
+        out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget, policy=args.policy)
     if rank == 0:
