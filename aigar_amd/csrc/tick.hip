@@ -1,26 +1,27 @@
 // tick.hip -- Field.update() (field.py:85-92) as a sequence of gfx950 kernels.
 //
-// Phase map (kernel <- reference):
-//   k_update_viruses          updateViruses            field.py:94-97
-//   k_update_blobs            updateBlobs              field.py:99-110
-//   k_update_players          updatePlayers + Player.update + performEjections
-//                             + handlePlayerCollisions field.py:112-181, player.py:30-72
-//   k_scan_players/finalize   creation-sequence numbers (canonical order) + blob append
-//   grid builds               updateHashTables         field.py:121-132 (centre-bucket
-//                             counting sort; membership is tested exactly per query)
-//   k_merge                   mergePlayerCells         field.py:183-198
-//   k_vb_*                    virusBlobOverlap         field.py:246-253, 316-325
-//   k_pv_*                    playerVirusOverlap       field.py:225-231, 333-370
-//   k_food_*  (pellets/blobs) playerPelletOverlap / playerBlobOverlap field.py:207-222
-//                             parallel "deterministic reservations": each cell reserves
-//                             the foods it could ever eat; a cell commits once it owns
-//                             them all (=> every earlier conflicting cell has committed);
-//                             leftovers run serially in priority order.
-//   k_pp_*                    playerPlayerOverlap      field.py:233-244
-//                             parallel activity test, then one thread per arena walks
+// Phase map (kernel <- reference), in launch order:
+//   k_tick_begin              updateViruses + updateBlobs + per-cell part of Player.update
+//                             field.py:94-110, player.py:39-44
+//   k_players                 rest of updatePlayers (split, eject, move, push-apart) +
+//                             creation-sequence numbers (canonical order) + blob append
+//                             field.py:112-181, player.py:30-72
+//   k_grid_small              updateHashTables for blobs and viruses (field.py:121-132;
+//                             centre-bucket counting sort, membership tested exactly per query)
+//   k_merge_vb                mergePlayerCells + virus<-blob activity  field.py:183-198
+//   k_vb_serial               virusBlobOverlap         field.py:246-253, 316-325
+//   k_pv_active/serial        playerVirusOverlap       field.py:225-231, 333-370
+//   k_food_prep/commit/serial playerPelletOverlap + playerBlobOverlap field.py:207-222 as one
+//                             "deterministic reservations" pass: each cell reserves the foods
+//                             it could ever eat; a cell commits once it owns them all (=> every
+//                             earlier conflicting cell has committed); leftovers run serially
+//                             in priority order.  Extra blocks build the player-cell grid.
+//   k_pp_active/serial        playerPlayerOverlap      field.py:233-244
+//                             parallel activity test, then one wavefront per arena walks
 //                             the active players in order (live-list semantics incl.
 //                             skip-after-removal), re-activating neighbours on growth.
-//   k_spawn_*                 spawnStuff               field.py:256-313
+//   k_spawn_plan/all          spawnStuff               field.py:256-313
+//   k_scan_lb, k_pgrid_scatter closing pellet rebuild; extra blocks refresh the FOV cache
 #include <hip/hip_runtime.h>
 
 #include "aigar_dev.h"
@@ -275,10 +276,6 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
 
 // updateViruses + updateBlobs + the per-cell part of updatePlayers in one
 // launch: thread ranges [cell slots | viruses | blobs] (independent, field.py:94-119)
-__global__ void __launch_bounds__(256) k_update_players(Dev d) {
-  int gp = GTID;
-  if (gp < d.NP) update_player(d, gp);
-}
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d) {
   int gi = GTID;
   if (gi < kMaxCells * d.NP) {
@@ -352,66 +349,6 @@ __device__ int block_scan_excl(const int *in, int *out, int n, int *sh) {
   }
   __syncthreads();
   return total;
-}
-
-// ------------------------------------------------------------ T5/T6
-__global__ void __launch_bounds__(1024) k_scan_players(Dev d) {
-  __shared__ int sh[1024];
-  int a = blockIdx.x;
-  const int B = d.B, base = a * B;
-  // p_newc + p_newb -> seq offsets; p_newb -> blob offsets (use p_seqoff as temp for the sum)
-  for (int p = threadIdx.x; p < B; p += blockDim.x) d.p_seqoff[base + p] = d.p_newc[base + p] + d.p_newb[base + p];
-  __syncthreads();
-  int tot = block_scan_excl(d.p_seqoff + base, d.p_seqoff + base, B, sh);
-  int totb = block_scan_excl(d.p_newb + base, d.p_bloboff + base, B, sh);
-  if (threadIdx.x == 0) {
-    ArenaCtl &c = d.ctl[a];
-    c.seq_base_upd = c.seq_next;
-    c.seq_next += tot;
-    c.n_blob_base = c.n_blob;
-    if (c.n_blob + totb > d.Ecap) {
-      c.err |= ERR_BLOB_CAP;
-      c.n_blob = d.Ecap;
-    } else {
-      c.n_blob += totb;
-    }
-  }
-}
-
-__global__ void k_finalize_players(Dev d) {
-  int gp = GTID;
-  if (gp < d.NP && gp % d.B == 0) {  // grid radius bounds restart (re-maxed by every grid build)
-    d.ctl[gp / d.B].rmax_cell = 0;
-    d.ctl[gp / d.B].rmax_virus = 0;
-  }
-  if (gp >= d.NP || !d.p_alive[gp]) return;
-  const int NP = d.NP, a = gp / d.B;
-  const ArenaCtl &c = d.ctl[a];
-  int n = d.p_ncells[gp], nn = d.p_newc[gp], nb = d.p_newb[gp];
-  int64_t s0 = c.seq_base_upd + d.p_seqoff[gp];
-  for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    if (k >= n - nn) d.c_seq[ci] = s0 + (k - (n - nn));
-    d.c_flags[ci] = (d.c_flags[ci] & ~F_NEW) | F_INHASH;  // updateHashTables inserts every cell
-  }
-  for (int j = 0; j < nb; j++) {
-    int bi = c.n_blob_base + d.p_bloboff[gp] + j;
-    if (bi >= d.Ecap) return;  // ERR_BLOB_CAP already set
-    size_t g = (size_t)a * d.Ecap + bi, si = (size_t)j * NP + gp;
-    const double bm = kEjectMass * 0.8;
-    d.b_x[g] = d.sb_x[si];
-    d.b_y[g] = d.sb_y[si];
-    d.b_m[g] = bm;
-    d.b_r[g] = radius_of(bm);
-    d.b_vx[g] = 0;
-    d.b_vy[g] = 0;
-    d.b_svx[g] = d.sb_svx[si];
-    d.b_svy[g] = d.sb_svy[si];
-    d.b_svc[g] = 15;
-    d.b_seq[g] = s0 + nn + j;
-    d.b_ej[g] = d.c_seq[(size_t)d.sb_slot[si] * NP + gp];
-    d.b_flags[g] = F_ALIVE;
-  }
 }
 
 // updatePlayers' per-player part + the creation-sequence numbering + the blob
@@ -577,94 +514,6 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
 
 // ------------------------------------------------------------ grids
 
-// generic counting sort by centre bucket. kind: 0 cells (pool), 1 blobs, 2 viruses
-template <int KIND>
-__global__ void k_grid_count(Dev d, int fix) {
-  int gi = GTID;
-  int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
-  bool in = gi < d.A * per;
-  int a = in ? gi / per : 0, i = in ? gi - a * per : 0;
-  double x = 0, y = 0, r = 0;
-  bool ok = false;
-  int *rank, *cnt;
-  if (KIND == 0) {
-    int slot = i / d.B, p = i - slot * d.B;
-    size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-    ok = in && (d.c_flags[g] & F_ALIVE);
-    if (ok) {
-      x = d.c_x[g];
-      y = d.c_y[g];
-      r = d.c_r[g];
-    }
-    rank = d.c_rank;
-    cnt = d.ccnt;
-  } else if (KIND == 1) {
-    size_t g = (size_t)a * d.Ecap + i;
-    ok = in && i < d.ctl[a].n_blob && (d.b_flags[g] & F_ALIVE);
-    if (ok) {
-      x = d.b_x[g];
-      y = d.b_y[g];
-    }
-    rank = d.b_rank;
-    cnt = d.bcnt;
-  } else {
-    size_t g = (size_t)a * d.Vcap + i;
-    ok = in && i < d.ctl[a].n_vir && (d.v_flags[g] & F_ALIVE);
-    if (ok) {
-      x = d.v_x[g];
-      y = d.v_y[g];
-      r = d.v_r[g];
-    }
-    rank = d.v_rank;
-    cnt = d.vcnt;
-  }
-  if (KIND == 0) wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? r : 0.0);
-  if (KIND == 2) wave_atomic_max_pos(&d.ctl[a].rmax_virus, ok ? r : 0.0);
-  if (!ok) return;
-  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-  rank[(size_t)a * per + i] = atomicAdd(&cnt[(size_t)a * (d.H + 1) + b], 1);
-}
-template <int KIND>
-__global__ void k_grid_scatter(Dev d) {
-  int gi = GTID;
-  int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
-  if (gi >= d.A * per) return;
-  int a = gi / per, i = gi - a * per;
-  double x, y;
-  int *rank, *start, *items;
-  int val;
-  if (KIND == 0) {
-    int slot = i / d.B, p = i - slot * d.B;
-    size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-    if (!(d.c_flags[g] & F_ALIVE)) return;
-    x = d.c_x[g];
-    y = d.c_y[g];
-    rank = d.c_rank;
-    start = d.cstart;
-    items = d.citems;
-    val = (int)g;
-  } else if (KIND == 1) {
-    size_t g = (size_t)a * d.Ecap + i;
-    if (i >= d.ctl[a].n_blob || !(d.b_flags[g] & F_ALIVE)) return;
-    x = d.b_x[g];
-    y = d.b_y[g];
-    rank = d.b_rank;
-    start = d.bstart;
-    items = d.bitems;
-    val = i;
-  } else {
-    size_t g = (size_t)a * d.Vcap + i;
-    if (i >= d.ctl[a].n_vir || !(d.v_flags[g] & F_ALIVE)) return;
-    x = d.v_x[g];
-    y = d.v_y[g];
-    rank = d.v_rank;
-    start = d.vstart;
-    items = d.vitems;
-    val = i;
-  }
-  int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-  items[(size_t)a * per + start[(size_t)a * (d.H + 1) + b] + rank[(size_t)a * per + i]] = val;
-}
 // block-wide exclusive scan of one int per thread (1024 threads); returns the
 // exclusive prefix and writes the block total to *total (shared)
 __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
@@ -2491,14 +2340,6 @@ void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
   hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256) + fovb), dim3(256), 0, s, d, mode, fovb);
 }
 
-template <int KIND>
-static void launch_grid(const Dev &d, hipStream_t s, int *cnt, int *start, int fix = 0) {
-  int per = KIND == 0 ? kMaxCells * d.B : (KIND == 1 ? d.Ecap : d.Vcap);
-  long n = (long)d.A * per;
-  hipLaunchKernelGGL(k_grid_count<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d, fix);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, cnt, start, nullptr, 0, 0, 1);
-  hipLaunchKernelGGL(k_grid_scatter<KIND>, dim3(nblk(n, 256)), dim3(256), 0, s, d);
-}
 
 // playerPelletOverlap + playerBlobOverlap: prep, reservation rounds, serial rest;
 // the player-cell grid (counts, scatter) rides along as extra blocks of the
