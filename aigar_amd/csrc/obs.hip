@@ -132,17 +132,40 @@ __device__ __forceinline__ int obs_claim(const Dev &d, uint32_t epoch, int n) {
 // latency instead of chaining it.  f is called by every lane (it may ballot).
 // pre() runs once, after the row-range loads are issued and before they are
 // used (the caller's own-cell appends overlap that latency).
+// The hash query's centre-bucket span, cut to the centre buckets an object of
+// radius <= R can occupy and still pass isInFov (cell.py:169-177): its centre
+// lies within R of the FOV box (+1 unit against rounding at the box edge).
+// Exact -- every candidate is still tested -- and it drops the ring of buckets
+// the hash expansion adds whenever the FOV edge sits away from a bucket edge.
+__device__ __forceinline__ Span clip_to_fov(Span s, double fx, double fy, double h, double R, int cols, int shift) {
+  const double m = h + R + 1.0;
+  const int x0 = max(0, (int)floor((fx - m) / kBucket)) >> shift, x1 = min(cols - 1, (int)floor((fx + m) / kBucket));
+  const int y0 = max(0, (int)floor((fy - m) / kBucket)) >> shift, y1 = min(cols - 1, (int)floor((fy + m) / kBucket));
+  s.bx0 = max(s.bx0, x0);
+  s.bx1 = min(s.bx1, x1 < 0 ? -1 : x1 >> shift);
+  s.by0 = max(s.by0, y0);
+  s.by1 = min(s.by1, y1 < 0 ? -1 : y1 >> shift);
+  return s;
+}
+__device__ __forceinline__ int span_rows(const Span &s) { return (s.bx1 >= s.bx0 && s.by1 >= s.by0) ? s.by1 - s.by0 + 1 : 0; }
+
 template <class P, class F>
-__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, bool want_p, bool want_v, P pre, F f) {
+__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, double fx, double fy, double fs, bool want_p,
+                                              bool want_v, P pre, F f) {
   const int lane = threadIdx.x & 63;
   const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
   const ArenaCtl &ctl = d.ctl[a];
-  const int Ec = (int)ceil((fmax(ctl.rmax_cell, radius_of(kStartMass)) + 1.0) / kBucket) + 1;
-  const int Ev = (int)ceil((fmax(ctl.rmax_virus, radius_of(kVirusBase)) + 1.0) / kBucket) + 1;
-  const Span sp = grid_span(Q, 1, d.cols, 0), sc = grid_span(Q, Ec, d.cols, d.cshift_c), sv = grid_span(Q, Ev, d.cols, d.cshift);
-  const int np_rows = (qok && want_p) ? sp.by1 - sp.by0 + 1 : 0;
-  const int nc_rows = qok ? sc.by1 - sc.by0 + 1 : 0;
-  const int nv_rows = (qok && want_v) ? sv.by1 - sv.by0 + 1 : 0;
+  const double rc = fmax(ctl.rmax_cell, radius_of(kStartMass)), rv = fmax(ctl.rmax_virus, radius_of(kVirusBase));
+  const int Ec = (int)ceil((rc + 1.0) / kBucket) + 1;
+  const int Ev = (int)ceil((rv + 1.0) / kBucket) + 1;
+  const double h = fs / 2;
+  // pellets weigh 1-3, or 14.4 when converted from a blob: radius < 2.2
+  const Span sp = clip_to_fov(grid_span(Q, 1, d.cols, 0), fx, fy, h, 2.2, d.cols, 0);
+  const Span sc = clip_to_fov(grid_span(Q, Ec, d.cols, d.cshift_c), fx, fy, h, rc, d.cols, d.cshift_c);
+  const Span sv = clip_to_fov(grid_span(Q, Ev, d.cols, d.cshift), fx, fy, h, rv, d.cols, d.cshift);
+  const int np_rows = (qok && want_p) ? span_rows(sp) : 0;
+  const int nc_rows = qok ? span_rows(sc) : 0;
+  const int nv_rows = (qok && want_v) ? span_rows(sv) : 0;
   const int nrows = np_rows + nc_rows + nv_rows;
   const size_t H1 = (size_t)a * (d.H + 1);
   const int *pst = d.pstart + H1, *cst = d.cstart + H1, *vst = d.vstart + H1;
@@ -294,7 +317,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       }
       list_append(c, CLx, capC, nc);
     };
-    wave_fov_walk(d, a, Q, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, own_cells, [&](bool valid, int kd, size_t g) {
+    wave_fov_walk(d, a, Q, fx, fy, fs, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, own_cells, [&](bool valid, int kd, size_t g) {
       const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
       const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
       const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
@@ -687,7 +710,7 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   double best = -1;
   uint64_t bord = ~0ull;
   double tx = 0, ty = 0;
-  wave_fov_walk(d, a, Q, true, d.virus_enabled, [] {}, [&](bool valid, int kd, size_t g) {
+  wave_fov_walk(d, a, Q, fx, fy, fs, true, d.virus_enabled, [] {}, [&](bool valid, int kd, size_t g) {
     if (!valid) return;
     const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
     const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
