@@ -182,9 +182,14 @@ def main():
     import torch
     rank, world, local = replicas.world_from_env()
     dist = None
+    # AIGAR_DIST_BACKEND=gloo rehearses the N-rank path with several ranks
+    # sharing the GPUs there are (ranks wrap around the visible devices)
+    backend = os.environ.get("AIGAR_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:  # one process per GPU, independent replicas (weak scaling)
-        dist = replicas.init("nccl")
+        dist = replicas.init(backend)
     from aigar_amd import _lib  # raises if libaigar_hip.so is missing: no fallback
 
     name = args.workload
@@ -222,7 +227,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     stp.sync()  # raises on any device-side capacity error
-    elapsed = replicas.max_over_ranks(dist, elapsed, device="cuda")
+    elapsed = replicas.max_over_ranks(dist, elapsed, device="cuda" if backend == "nccl" else None)
     # per-phase breakdown and the roofline kernel's duration: the next
     # min(steps, 50) steps issued as separate calls, HIP events on the stepper's stream
     stp.profile(True)
@@ -282,7 +287,7 @@ def main():
     }
     if rank == 0 and world == 1 and args.batched_arenas > 1 and not args.arenas:
         out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (N = 1 only)
         out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget, policy=args.policy)
     if rank == 0:
         print(json.dumps(out), flush=True)
