@@ -77,6 +77,7 @@ def load(build_if_missing=False):
         "aigar_rewards": [vp, vp, C.POINTER(_abi.RewardParams), i32, i32],
         "aigar_set_split_likelihood": [vp, i32, C.POINTER(C.c_int32)],
         "aigar_run": [vp, i32, C.POINTER(_abi.RunParams), vp, i32],
+        "aigar_env_step": [vp, vp, i32, i32, i32, C.POINTER(_abi.RewardParams), vp, vp, i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -190,6 +191,24 @@ class Stepper:
             p = C.c_void_p(out.data_ptr())
         self._chk(self.L.aigar_run(self.h, int(n), C.byref(prm), p, dt))
         return out
+
+    def env_step(self, act, reward, obs, enable_split=True, skip=0, params=None):
+        """One learner decision on device tensors (aigar_env_step): act [NP, 2..4] float64,
+        reward [NP] float64 (summed over the skip + 1 ticks), obs [NP, obs_len]; one graph replay."""
+        for t in (act, reward, obs):
+            if not getattr(t, "is_cuda", False) or not t.is_contiguous():
+                raise ValueError("env_step takes contiguous device tensors")
+        if str(act.dtype) != "torch.float64" or str(reward.dtype) != "torch.float64":
+            raise ValueError("actions and rewards are float64")
+        if act.dim() != 2 or act.shape[0] != self.NP or not 2 <= act.shape[1] <= 4:
+            raise ValueError("actions must be [%d, 2..4]" % self.NP)
+        if tuple(obs.shape) != (self.NP, self.obs_len) or tuple(reward.shape) != (self.NP,):
+            raise ValueError("reward must be [%d], obs [%d, %d]" % (self.NP, self.NP, self.obs_len))
+        prm = params if isinstance(params, _abi.RewardParams) else _abi.RewardParams.from_parameters(params)
+        dt = 0 if str(obs.dtype) == "torch.float64" else 1
+        self._chk(self.L.aigar_env_step(self.h, C.c_void_p(act.data_ptr()), int(act.shape[1]), int(bool(enable_split)),
+                                        int(skip), C.byref(prm), C.c_void_p(reward.data_ptr()),
+                                        C.c_void_p(obs.data_ptr()), dt))
 
     def observe(self, out=None, dtype=np.float64):
         if out is None:

@@ -23,7 +23,8 @@ void launch_player_stats(const Dev &d, hipStream_t s, double *out);
 void launch_player_fov(const Dev &d, hipStream_t s);
 void launch_apply_actions(const Dev &d, hipStream_t s, const double *act, int n_act, int enable_split, int skipping,
                           int record);
-void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last);
+void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last,
+                    int mode);
 void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask);
 void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd);
 }  // namespace aigar
@@ -74,6 +75,15 @@ struct aigar_handle {
   aigar_run_params run_key{};
   void *run_out = nullptr;
   int run_dtype = -1;
+  // aigar_env_step: one learner decision (skip + 1 ticks) as a graph
+  hipGraphExec_t env_graph = nullptr;
+  struct EnvKey {
+    const double *act;
+    int n_act, enable_split, skip, dtype;
+    aigar_reward_params prm;
+    double *reward;
+    void *obs;
+  } env_key{};
 };
 
 extern "C" const char *aigar_last_error(void) { return g_err.c_str(); }
@@ -103,6 +113,7 @@ static int obs_len_of(const aigar_config &c) {
 static void free_all(aigar_handle *h) {
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
   if (h->run_graph) (void)hipGraphExecDestroy(h->run_graph);
+  if (h->env_graph) (void)hipGraphExecDestroy(h->env_graph);
   for (void *p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -426,6 +437,54 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
     Mark m(h, "run");
     if (h->run_graph) HIPCHK(hipGraphLaunch(h->run_graph, h->stream));
     else launch_env_step(h, h->stream, *p, obs_out, dtype);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// One learner decision for every player (bot.py:166-233 batched, the loop of
+// aigar.py:performModelSteps): the action through set_command_point, held for
+// skip + 1 ticks with split/eject dropped on the skipped ones, the rewards of
+// the window summed, then every bot's observation -- one graph replay.
+static void launch_env_decision(aigar_handle *h, hipStream_t s, const aigar_handle::EnvKey &k) {
+  for (int t = 0; t <= k.skip; t++) {
+    if (t > 0) launch_rewards(h->d, s, k.reward, k.prm, 0, t == 1 ? 1 : 2);  // updateRewards (bot.py:166-168)
+    launch_apply_actions(h->d, s, k.act, k.n_act, k.enable_split, t > 0, t == 0);
+    launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v);
+  }
+  launch_rewards(h->d, s, k.reward, k.prm, 1, k.skip == 0 ? 1 : 2);  // end of move_NN (bot.py:220-230)
+  launch_observe(h->d, s, k.obs, k.dtype, 0);
+}
+
+extern "C" int aigar_env_step(aigar_handle *h, const double *act, int n_act, int enable_split, int skip,
+                              const aigar_reward_params *p, double *reward_out, void *obs_out, int dtype) {
+  if (!h || !act || !p || !reward_out || !obs_out) return fail("null argument");
+  if (n_act < 2 || n_act > 4) return fail("env_step: n_act must be 2, 3 or 4");
+  if (skip < 0) return fail("env_step: skip < 0");
+  if (dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  aigar_handle::EnvKey k{};
+  k.act = act;
+  k.n_act = n_act;
+  k.enable_split = enable_split ? 1 : 0;
+  k.skip = skip;
+  k.dtype = dtype;
+  k.prm = *p;
+  k.reward = reward_out;
+  k.obs = obs_out;
+  if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log holds the window's ticks
+    hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  if (!h->use_graph) {
+    launch_env_decision(h, h->stream, k);
+  } else {
+    if (!h->env_graph || memcmp(&h->env_key, &k, sizeof k) != 0) {
+      if (h->env_graph) (void)hipGraphExecDestroy(h->env_graph);
+      h->env_graph = capture_graph(h, [&](hipStream_t cs) { launch_env_decision(h, cs, k); });
+      if (!h->env_graph) return fail("env_step: graph capture failed");
+      h->env_key = k;
+    }
+    Mark m(h, "env_step");
+    HIPCHK(hipGraphLaunch(h->env_graph, h->stream));
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -906,7 +965,7 @@ extern "C" int aigar_rewards(aigar_handle *h, double *out, const aigar_reward_pa
   if (!h || !out || !p) return fail("null argument");
   HIPCHK(hipSetDevice(h->cfg.device));
   double *dst = on_device ? out : h->d_stats;
-  launch_rewards(h->d, h->stream, dst, *p, update_last);
+  launch_rewards(h->d, h->stream, dst, *p, update_last, 0);
   HIPCHK(hipGetLastError());
   if (!on_device) {
     HIPCHK(hipMemcpyAsync(out, h->d_stats, sizeof(double) * h->d.NP, hipMemcpyDeviceToHost, h->stream));

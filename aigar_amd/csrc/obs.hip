@@ -835,7 +835,9 @@ void launch_apply_actions(const Dev &d, hipStream_t s, const double *act, int n_
 // Bot.getReward (bot.py:654-667) for every player; NaN where the reference
 // returns None (no lastMass yet).  update_last: the end of move_NN on a
 // decision frame (bot.py:229-230) -- lastMass <- total mass of live players.
-__global__ void k_rewards(Dev d, double *out, aigar_reward_params prm, int update_last) {
+// mode 0: out = r (NaN = None); 1: out = r, None -> 0; 2: out += r, None -> 0 (the
+// cumulative reward of a frame-skip window, bot.py:166-168,220-228)
+__global__ void k_rewards(Dev d, double *out, aigar_reward_params prm, int update_last, int mode) {
   int gp = GTID;
   if (gp >= d.NP) return;
   const bool alive = d.p_alive[gp];
@@ -849,11 +851,13 @@ __global__ void k_rewards(Dev d, double *out, aigar_reward_params prm, int updat
     double rw = alive ? mass - last : -1 * last * prm.death_factor + prm.death_term;
     r = rw * prm.reward_scale - prm.reward_term;
   }
-  out[gp] = r;
+  if (mode != 0 && isnan(r)) r = 0;
+  out[gp] = mode == 2 ? out[gp] + r : r;
   if (update_last && alive) d.o_last_mass[gp] = mass;
 }
-void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last) {
-  hipLaunchKernelGGL(k_rewards, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, out, p, update_last);
+void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last,
+                    int mode) {
+  hipLaunchKernelGGL(k_rewards, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, out, p, update_last, mode);
 }
 
 __global__ void k_player_stats(Dev d, double *out) {

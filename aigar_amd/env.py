@@ -47,6 +47,7 @@ class AgarVecEnv:
         self.reward_params = _abi.RewardParams.from_parameters(parameters)
         self.obs = torch.empty((self.NP, self.stepper.obs_len), dtype=torch.float64, device=self.dev)
         self._r = torch.empty(self.NP, dtype=torch.float64, device=self.dev)
+        self._act = {}  # n_act -> persistent action buffer (the decision graph is keyed by its address)
 
     def reset(self, seed=0):
         """Field.reset + NN bots' reset (lastMass = None, history grids cleared)."""
@@ -58,7 +59,21 @@ class AgarVecEnv:
         return self.obs
 
     def step(self, actions):
-        """actions: [n_players, 2..4] tensor/array in [0, 1] -> (obs, reward, alive)."""
+        """actions: [n_players, 2..4] tensor/array in [0, 1] -> (obs, reward, alive).
+        The whole decision (skip + 1 ticks, rewards, observation) is one graph replay."""
+        torch = self.torch
+        act = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions), device=self.dev)
+        n = int(act.shape[1])
+        buf = self._act.get(n)
+        if buf is None:
+            buf = self._act[n] = torch.empty((self.NP, n), dtype=torch.float64, device=self.dev)
+        buf.copy_(act)
+        self.stepper.env_step(buf, self._r, self.obs, self.enable_split, self.skip, self.reward_params)
+        alive = ~torch.isnan(self.obs[:, 0])
+        return self.obs, self._r.clone(), alive
+
+    def step_calls(self, actions):
+        """The same decision as separate calls (apply_actions / step / rewards / observe)."""
         torch = self.torch
         act = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions), device=self.dev)
         act = act.to(device=self.dev, dtype=torch.float64).contiguous()

@@ -182,6 +182,18 @@ typedef struct aigar_reward_params {
 } aigar_reward_params;
 int aigar_rewards(aigar_handle *h, double *out, const aigar_reward_params *p, int update_last, int on_device);
 
+/* One learner decision for every player -- the NN bots' move_NN / updateRewards
+ * / frame skipping (bot.py:166-233) batched, as aigar.py:performModelSteps
+ * drives them: act[A*B][n_act] (n_act 2..4, DEVICE pointer) goes through
+ * set_command_point (as aigar_apply_actions) and is held for skip + 1 ticks
+ * (FRAME_SKIP_RATE; split/eject dropped on the skipped ticks), reward_out[A*B]
+ * (DEVICE) gets the window's summed getReward (None counts 0; lastMass advances
+ * at the end), obs_out (DEVICE, as aigar_observe) every bot's observation.  The
+ * whole decision is one hipGraph replay (re-captured when a pointer or a
+ * parameter changes). */
+int aigar_env_step(aigar_handle *h, const double *act, int n_act, int enable_split, int skip,
+                   const aigar_reward_params *p, double *reward_out, void *obs_out, int dtype);
+
 /* n_ticks x Field.update() with the current commands (field.py:85-92). */
 int aigar_step(aigar_handle *h, int n_ticks);
 

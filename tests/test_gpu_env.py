@@ -87,3 +87,29 @@ def test_vec_env_runs_on_device_tensors():
         assert torch.equal(obs[live, 7 * 121 + 3:7 * 121 + 7], act[live])
         was_alive = alive
     env.close()
+
+
+def test_vec_env_decision_graph_matches_separate_calls():
+    """AgarVecEnv.step (one aigar_env_step graph replay per decision) == the same
+    decision issued as apply_actions / step / rewards / observe calls."""
+    import torch
+    from aigar_amd.env import AgarVecEnv
+    p = types.SimpleNamespace(VIRUS_SPAWN=True, ENABLE_SPLIT=True, PELLET_GRID=True, SELF_GRID=True, WALL_GRID=True,
+                              ENEMY_GRID=True, VIRUS_GRID=True, SELF_GRID_LF=True, ENEMY_GRID_LF=True,
+                              USE_FOVSIZE=True, USE_TOTALMASS=True, USE_LAST_ACTION=True, USE_LAST_FOVSIZE=True,
+                              GRID_SQUARES_PER_FOV=11, EXTRA_INPUT=True, FRAME_SKIP_RATE=7)
+    a, b = AgarVecEnv(48, p, field_size=300, max_viruses=8), AgarVecEnv(48, p, field_size=300, max_viruses=8)
+    oa, ob = a.reset(5), b.reset(5)
+    assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0))
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    for t in range(12):
+        act = torch.rand((48, 4 if t % 3 else 3), dtype=torch.float64, device="cuda", generator=gen)
+        oa, ra, la = a.step(act)
+        ob, rb, lb = b.step_calls(act)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0)), t
+        assert torch.equal(ra, rb), t
+        assert torch.equal(la, lb), t
+    assert parity.diff_states(a.stepper.get_state(), b.stepper.get_state(), ftol=0.0) == []
+    a.close()
+    b.close()
