@@ -22,8 +22,12 @@ Differences a caller can see:
  - canonical order: every set-derived list (FOV queries) is ordered by creation
    sequence instead of CPython object addresses;
  - randomness comes from the device's Philox stream (seeded by `seed`), not from
-   numpy's global MT19937 (colours are not modelled); Random bots still draw
-   from numpy like the reference;
+   numpy's global MT19937; Random bots still draw from numpy like the reference;
+ - colours (for a View: view.py:164-215) follow the reference's rules with
+   hashed instead of drawn values: a player's colour is three bytes with a sum
+   <= 600 (player.py:38-41), its cells and its ejected blobs take it
+   (cell.py:35, field.py:141), viruses are (0, 255, 0) (field.py:274) and
+   pellets three values in [50, 200) (cell.py:31), each keyed by the object;
  - Greedy bots move on the device, all in one launch per tick
    (`Model.takeBotActions`); their splitLikelihood comes from the Philox stream
    unless set with `Field.set_split_likelihood`.
@@ -76,6 +80,34 @@ def obs_masks(parameters):
     return ch, ex, int(getattr(parameters, "GRID_SQUARES_PER_FOV", 11))
 
 
+def _mix(v):
+    """splitmix64 finaliser: the hash behind the (deterministic) colours."""
+    v = (v + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    v = ((v ^ (v >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    v = ((v ^ (v >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return v ^ (v >> 31)
+
+
+def player_color(index, seed=0):
+    """Player.randomizeColor (player.py:38-41): (0..255)^3, redrawn while the sum exceeds 600."""
+    k = 0
+    while True:
+        h = _mix((int(seed) << 32) ^ (int(index) << 8) ^ k)
+        c = (h & 255, (h >> 8) & 255, (h >> 16) & 255)
+        if sum(c) <= 600:
+            return c
+        k += 1
+
+
+def pellet_color(seq, seed=0):
+    """cell.py:31: three numpy.random.randint(50, 200) draws (hashed from the creation sequence)."""
+    h = _mix((int(seed) << 40) ^ int(seq) ^ 0x5E11E7)
+    return (50 + h % 150, 50 + (h >> 16) % 150, 50 + (h >> 32) % 150)
+
+
+VIRUS_COLOR = (0, 255, 0)  # field.py:274
+
+
 def _footprint(x, y, r, size):
     """Bucket rectangle of spatialHashTable.getIdsForArea (int variant,
     spatialHashTable.py:70-83); arrays in, (x0, x1, y0, y1) out (x1 < x0: empty)."""
@@ -109,9 +141,9 @@ def _in_area(x, y, r, size, fov_pos, fov_size):
 class Cell:
     """Read-only view of one entity of a tick snapshot (cell.py:7-260)."""
     __slots__ = ("x", "y", "mass", "radius", "velocity", "splitVelocity", "splitVelocityCounter", "mergeTime",
-                 "player", "id", "kind", "alive", "pos")
+                 "player", "id", "kind", "alive", "pos", "color")
 
-    def __init__(self, kind, f, seq, svc, player=None, merge_time=0.0):
+    def __init__(self, kind, f, seq, svc, player=None, merge_time=0.0, color=(0, 0, 0)):
         self.kind = kind
         self.x, self.y, self.mass, self.radius = float(f[0]), float(f[1]), float(f[2]), float(f[3])
         self.pos = [self.x, self.y]
@@ -122,6 +154,7 @@ class Cell:
         self.player = player
         self.id = int(seq)
         self.alive = True
+        self.color = color
 
     def __repr__(self):
         return "Cell(%s #%d m=%.3f @ %.2f,%.2f)" % (self.kind, self.id, self.mass, self.x, self.y)
@@ -140,7 +173,7 @@ class Cell:
     def getSplitVelocity(self): return self.splitVelocity
     def getReducedSpeed(self): return 3.0 * math.pow(self.mass, -0.35)
     def getName(self): return self.player.getName() if self.player is not None else ""
-    def getColor(self): return (0, 0, 0)
+    def getColor(self): return self.color
 
     # predicates (cell.py:143-189)
     def isAlive(self): return self.alive
@@ -236,7 +269,10 @@ class Player:
     def getName(self): return self.name
     def getSelected(self): return self.selected
     def isExploring(self): return self.exploring
-    def getColor(self): return (0, 0, 0)
+
+    def getColor(self):  # player.py:174
+        seed = self.field.seed if self.field is not None else 0
+        return player_color(self.index, seed)
 
 
 class Field:
@@ -335,13 +371,19 @@ class Field:
         st = self._snapshot()
         per_player = [[] for _ in self.players]
         cells = []
+        owner_of = {}  # cell seq -> player index (an ejected blob takes its player's colour)
+        pcol = [p.getColor() for p in self.players]
         for f, i in zip(st["cells_f"], st["cells_i"]):
-            c = Cell("player", f[:8], i[2], i[1], self.players[int(i[0])], f[8])
+            c = Cell("player", f[:8], i[2], i[1], self.players[int(i[0])], f[8], pcol[int(i[0])])
             per_player[int(i[0])].append(c)
             cells.append(c)
-        pel = [Cell("pellet", f, s, 0) for f, s in zip(st["pellets_f"], st["pellets_seq"])]
-        blobs = [Cell("blob", f, i[1], i[0]) for f, i in zip(st["blobs_f"], st["blobs_i"])]
-        vir = [Cell("virus", f, i[1], i[0]) for f, i in zip(st["viruses_f"], st["viruses_i"])]
+            owner_of[int(i[2])] = int(i[0])
+        pel = [Cell("pellet", f, s, 0, color=pellet_color(s, self.seed))
+               for f, s in zip(st["pellets_f"], st["pellets_seq"])]
+        blobs = [Cell("blob", f, i[1], i[0], color=(pcol[owner_of[int(i[2])]] if int(i[2]) in owner_of
+                                                    else pellet_color(i[1], self.seed)))
+                 for f, i in zip(st["blobs_f"], st["blobs_i"])]
+        vir = [Cell("virus", f, i[1], i[0], color=VIRUS_COLOR) for f, i in zip(st["viruses_f"], st["viruses_i"])]
         v = {"per_player": per_player, "cells": cells, "pellets": pel, "blobs": blobs, "viruses": vir,
              "cell_hashed": np.asarray(st["cells_i"])[:, 3] != 0 if len(cells) else np.zeros(0, bool),
              "virus_hashed": np.asarray(st["viruses_i"])[:, 2] != 0 if len(vir) else np.zeros(0, bool)}

@@ -115,3 +115,17 @@ def test_cell_view_predicates():
     assert a.overlap(b) and b.overlap(a)
     assert a.canSplit() and a.canEject() and a.canMerge() and not a.justEjected()
     assert a.isInFov([10.0, 10.0], 20.0) and not a.isInFov([30.0, 30.0], 10.0)
+
+
+def test_colours_follow_the_reference_rules():
+    # Player.randomizeColor (player.py:38-41): bytes, sum <= 600; deterministic per (seed, player)
+    cols = [M.player_color(i, 3) for i in range(500)]
+    assert all(all(0 <= v <= 255 for v in c) and sum(c) <= 600 for c in cols)
+    assert cols == [M.player_color(i, 3) for i in range(500)]
+    assert len(set(cols)) > 450 and M.player_color(0, 3) != M.player_color(0, 4)
+    # pellets: three randint(50, 200) values (cell.py:31); viruses green (field.py:274)
+    pc = [M.pellet_color(s) for s in range(2000)]
+    assert all(all(50 <= v < 200 for v in c) for c in pc)
+    assert M.VIRUS_COLOR == (0, 255, 0)
+    p = M.Player("p")
+    assert p.getColor() == M.player_color(-1, 0) or sum(p.getColor()) <= 600
