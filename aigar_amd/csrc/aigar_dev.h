@@ -166,4 +166,12 @@ struct Dev {
 
 constexpr int FCAP = 32;  // stored candidate foods per cell (overflow -> serial)
 
+// the synthetic population's policy when it is evaluated inside the tick
+// (aigar_run, AIGAR_POLICY_RANDOM): probabilities and Philox salt
+struct RandomPolicy {
+  int on;
+  double ps, pe;
+  uint64_t salt;
+};
+
 }  // namespace aigar

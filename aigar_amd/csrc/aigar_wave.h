@@ -148,4 +148,23 @@ __device__ inline void fov_cache_thread(const Dev &d, int gp) {
   if (gp == 0) *d.ob_epoch = 0x80000000u | ((*d.ob_epoch + 1) & 0x7FFFFFFFu);
 }
 
+// The synthetic bot population's command for live player gp (bench / smoke
+// driver): an action in [0,1]^2 through set_command_point (bot.py:550-577),
+// split / eject with probabilities ps / pe; Philox-keyed by (player, tick, salt).
+struct Command {
+  double x, y;
+  int split, eject;
+};
+__device__ inline Command random_command(const Dev &d, int gp, const RandomPolicy &rp) {
+  const int a = gp / d.B;
+  const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
+  uint64_t u[4];
+  philox((uint64_t)gp, ST_POLICY, (uint64_t)d.ctl[a].tick, rp.salt, d.ctl[a].key0, d.ctl[a].key1, u);
+  const double a0 = u01(u[0]), a1 = u01(u[1]);
+  const int64_t x = (int64_t)fx, y = (int64_t)fy;
+  const int64_t left = x - (int64_t)(fs / 2), top = y - (int64_t)(fs / 2), size = (int64_t)fs;
+  return Command{(double)left + a0 * (double)size, (double)top + a1 * (double)size, u01(u[2]) < rp.ps,
+                 u01(u[3]) < rp.pe};
+}
+
 }  // namespace aigar

@@ -15,7 +15,8 @@
 #include "aigar_sem.h"
 
 namespace aigar {
-void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v);
+void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v,
+                 const RandomPolicy *rp = nullptr);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch);
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
@@ -409,9 +410,10 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
 // once as a single hipGraph and replayed n_steps times: no host round trip
 // between the policy, the tick's ~25 kernels and the observation.
 static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_params &p, void *out, int dtype) {
-  if (p.policy == AIGAR_POLICY_RANDOM) launch_policy(h->d, s, p.p_split, p.p_eject, p.seed);
-  else if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr);
-  launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v);
+  // the random population's policy runs inside the tick's first kernel (same draws as aigar_policy_random)
+  const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
+  if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr);
+  launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v, &rp);
   if (out) launch_observe(h->d, s, out, dtype, 0);  // epoch 0: the device-side epoch
 }
 

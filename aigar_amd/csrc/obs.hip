@@ -806,18 +806,11 @@ void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const u
 __global__ void k_policy_random(Dev d, double p_split, double p_eject, uint64_t salt) {
   int gp = GTID;
   if (gp >= d.NP || !d.p_alive[gp]) return;
-  int a = gp / d.B;
-  const Fov f{d.p_fx[gp], d.p_fy[gp], d.p_fs[gp], d.p_mass[gp], 0};
-  uint64_t u[4];
-  philox((uint64_t)gp, ST_POLICY, (uint64_t)d.ctl[a].tick, salt, d.ctl[a].key0, d.ctl[a].key1, u);
-  double a0 = u01(u[0]), a1 = u01(u[1]);
-  int64_t x = (int64_t)f.fx, y = (int64_t)f.fy;
-  int64_t left = x - (int64_t)(f.fs / 2), top = y - (int64_t)(f.fs / 2);
-  int64_t size = (int64_t)f.fs;
-  d.p_cmdx[gp] = (double)left + a0 * (double)size;
-  d.p_cmdy[gp] = (double)top + a1 * (double)size;
-  d.p_split[gp] = u01(u[2]) < p_split;
-  d.p_eject[gp] = u01(u[3]) < p_eject;
+  const Command c = random_command(d, gp, RandomPolicy{1, p_split, p_eject, salt});
+  d.p_cmdx[gp] = c.x;
+  d.p_cmdy[gp] = c.y;
+  d.p_split[gp] = c.split;
+  d.p_eject[gp] = c.eject;
 }
 
 // set_command_point (bot.py:550-577) for external actions act[NP][n_act]

@@ -113,12 +113,32 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
 // Player.decayMass + updateCellProperties for one cell (player.py:39-44,
 // cell.py:105-130,47-57): independent per cell, so one thread per pool slot --
 // the correctly rounded pow of the move speed no longer chains per player
-__device__ __forceinline__ void update_cell(const Dev &d, int gi) {
+// rp.on: the synthetic population's policy is evaluated here (every cell of a
+// player computes the same command; slot 0 stores it for k_players), which
+// saves the policy launch of aigar_run's step
+__device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPolicy &rp) {
   const int NP = d.NP;
   if (gi >= kMaxCells * NP) return;
   const int gp = gi % NP;
   const size_t ci = (size_t)gi;
-  if (!(d.c_flags[ci] & F_ALIVE) || !d.p_alive[gp]) return;
+  double cmdx, cmdy;
+  if (rp.on) {
+    if (!d.p_alive[gp]) return;  // makeMove: dead players keep their command
+    const Command c = random_command(d, gp, rp);
+    if (gi < NP) {  // slot 0 stores the player's command
+      d.p_cmdx[gp] = c.x;
+      d.p_cmdy[gp] = c.y;
+      d.p_split[gp] = c.split;
+      d.p_eject[gp] = c.eject;
+    }
+    if (!(d.c_flags[ci] & F_ALIVE)) return;
+    cmdx = c.x;
+    cmdy = c.y;
+  } else {
+    if (!(d.c_flags[ci] & F_ALIVE) || !d.p_alive[gp]) return;
+    cmdx = d.p_cmdx[gp];
+    cmdy = d.p_cmdy[gp];
+  }
   double m = d.c_m[ci], r = d.c_r[ci];
   if (m >= 4) {  // Cell.decayMass (cell.py:123-126)
     m = m * kDecay;
@@ -135,7 +155,7 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi) {
   double mt = d.c_mt[ci];
   if (mt > 0) d.c_mt[ci] = mt - 1;
   double vx, vy;
-  set_move_direction(d.c_x[ci], d.c_y[ci], m, r, d.p_cmdx[gp], d.p_cmdy[gp], vx, vy);
+  set_move_direction(d.c_x[ci], d.c_y[ci], m, r, cmdx, cmdy, vx, vy);
   d.c_vx[ci] = vx;
   d.c_vy[ci] = vy;
 }
@@ -276,10 +296,10 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
 
 // updateViruses + updateBlobs + the per-cell part of updatePlayers in one
 // launch: thread ranges [cell slots | viruses | blobs] (independent, field.py:94-119)
-__global__ void __launch_bounds__(256) k_tick_begin(Dev d) {
+__global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   int gi = GTID;
   if (gi < kMaxCells * d.NP) {
-    update_cell(d, gi);
+    update_cell(d, gi, rp);
     return;
   }
   gi -= kMaxCells * d.NP;
@@ -2361,11 +2381,11 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 // hipGraph by api.hip).  Forking independent phases onto a second stream was
 // measured slower on MI355X (cross-queue dependencies cost more than the
 // overlap gains at this kernel size), so the graph stays linear.
-void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v) {
+void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   Scratch scr{scr_k, scr_v};
   const int gP = nblk(d.NP, 256);
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
-  hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
