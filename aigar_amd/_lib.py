@@ -80,7 +80,11 @@ def load(build_if_missing=False):
         "aigar_env_step": [vp, vp, i32, i32, i32, C.POINTER(_abi.RewardParams), vp, vp, i32],
     }
     for name, args in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None and os.environ.get("AIGAR_SO"):  # an older diagnostics build: bind what it has
+            continue
+        if f is None:
+            raise RuntimeError("libaigar_hip.so lacks %s: rebuild it (python -m aigar_amd._build)" % name)
         f.argtypes = args
         f.restype = i32
     if L.aigar_abi_version() != _abi.ABI_VERSION:

@@ -411,7 +411,12 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
 // between the policy, the tick's ~25 kernels and the observation.
 static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_params &p, void *out, int dtype) {
   // the random population's policy runs inside the tick's first kernel (same draws as aigar_policy_random)
+#ifdef AIGAR_NO_POLICY_FOLD  // (diagnostics build: the policy as its own launch)
+  const RandomPolicy rp{0, 0, 0, 0};
+  if (p.policy == AIGAR_POLICY_RANDOM) launch_policy(h->d, s, p.p_split, p.p_eject, p.seed);
+#else
   const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
+#endif
   if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr);
   launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v, &rp);
   if (out) launch_observe(h->d, s, out, dtype, 0);  // epoch 0: the device-side epoch

@@ -161,8 +161,12 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
   const double h = fs / 2;
   // pellets weigh 1-3, or 14.4 when converted from a blob: radius < 2.2
   const Span sp = clip_to_fov(grid_span(Q, 1, d.cols, 0), fx, fy, h, 2.2, d.cols, 0);
+#ifdef AIGAR_OBS_CLIP_ALL
   const Span sc = clip_to_fov(grid_span(Q, Ec, d.cols, d.cshift_c), fx, fy, h, rc, d.cols, d.cshift_c);
   const Span sv = clip_to_fov(grid_span(Q, Ev, d.cols, d.cshift), fx, fy, h, rv, d.cols, d.cshift);
+#else  // (the coarse cell / virus grids gain little from the cut; it cost registers)
+  const Span sc = grid_span(Q, Ec, d.cols, d.cshift_c), sv = grid_span(Q, Ev, d.cols, d.cshift);
+#endif
   const int np_rows = (qok && want_p) ? span_rows(sp) : 0;
   const int nc_rows = qok ? span_rows(sc) : 0;
   const int nv_rows = (qok && want_v) ? span_rows(sv) : 0;
@@ -215,54 +219,32 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 #else  // 4 waves/SIMD: 4096 bots = 16 waves per CU, one residency round on 256 CUs
 #define OBS_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
-#ifndef AIGAR_OBS_BPB
-#define AIGAR_OBS_BPB 4
-#endif
-constexpr int OBS_BPB = AIGAR_OBS_BPB;  // bots (wavefronts) per block: fewer, larger blocks to dispatch
 template <typename OutT>
-__global__ void __launch_bounds__(64 * OBS_BPB) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch) {
-  // one LDS slice per wavefront (each wave is one bot; no block-level barrier)
+__global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch) {
   // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
   // masks in creation order (no indirection in the per-square sums)
-  union SX {
+  __shared__ union {
     int64_t seq;
     double m;
-  };
-  union PX {
+  } p_sx[OBS_PCAP];
+  __shared__ double p_m[OBS_PCAP];
+  __shared__ uint32_t p_mask[OBS_PCAP];
+  __shared__ union {
     int perm;
     uint32_t mask;
-  };
-  __shared__ SX p_sx_[OBS_BPB][OBS_PCAP];
-  __shared__ double p_m_[OBS_BPB][OBS_PCAP];
-  __shared__ uint32_t p_mask_[OBS_BPB][OBS_PCAP];
-  __shared__ PX p_px_[OBS_BPB][OBS_PCAP];
-  __shared__ double c_mass_[OBS_BPB][OBS_CCAP];
-  __shared__ uint32_t c_mask_[OBS_BPB][OBS_CCAP];
-  __shared__ uint8_t c_own_[OBS_BPB][OBS_CCAP];
-  __shared__ double v_rad_[OBS_BPB][OBS_VCAP], v_mass_[OBS_BPB][OBS_VCAP];
-  __shared__ int64_t v_seqs_[OBS_BPB][OBS_VCAP];
-  __shared__ uint32_t v_mask_[OBS_BPB][OBS_VCAP];
-  const int wv = threadIdx.x >> 6;
-  SX(&p_sx)[OBS_PCAP] = p_sx_[wv];
-  double(&p_m)[OBS_PCAP] = p_m_[wv];
-  uint32_t(&p_mask)[OBS_PCAP] = p_mask_[wv];
-  PX(&p_px)[OBS_PCAP] = p_px_[wv];
-  double(&c_mass)[OBS_CCAP] = c_mass_[wv];
-  uint32_t(&c_mask)[OBS_CCAP] = c_mask_[wv];
-  uint8_t(&c_own)[OBS_CCAP] = c_own_[wv];
-  double(&v_rad)[OBS_VCAP] = v_rad_[wv];
-  double(&v_mass)[OBS_VCAP] = v_mass_[wv];
-  int64_t(&v_seqs)[OBS_VCAP] = v_seqs_[wv];
-  uint32_t(&v_mask)[OBS_VCAP] = v_mask_[wv];
+  } p_px[OBS_PCAP];
+  __shared__ double c_mass[OBS_CCAP];
+  __shared__ uint32_t c_mask[OBS_CCAP];
+  __shared__ uint8_t c_own[OBS_CCAP];
+  __shared__ double v_rad[OBS_VCAP], v_mass[OBS_VCAP];
+  __shared__ int64_t v_seqs[OBS_VCAP];
+  __shared__ uint32_t v_mask[OBS_VCAP];
 
-  const int gp = blockIdx.x * OBS_BPB + wv, lane = threadIdx.x & 63;
-  const int NP = d.NP;
-  if (gp >= NP) return;  // (wave-uniform)
-  const int a = gp / d.B, G = d.G, GG = G * G, L = d.L;
+  const int gp = blockIdx.x, lane = threadIdx.x;
+  const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
   if (epoch == 0) epoch = *d.ob_epoch;  // graph replay (aigar_run): the tick's closing kernel set it
 #ifdef AIGAR_OBS_TIMING
-  __shared__ unsigned long long obs_ts_all[OBS_BPB][OBS_TS];
-  unsigned long long(&obs_ts_l)[OBS_TS] = obs_ts_all[wv];
+  __shared__ unsigned long long obs_ts_l[OBS_TS];
   if (lane == 0) obs_ts_l[5] = (unsigned long long)__smid();
 #endif
   OBS_STAMP(0);
@@ -909,9 +891,8 @@ void launch_player_fov(const Dev &d, hipStream_t s) {
   hipLaunchKernelGGL(k_player_fov, dim3((d.NP + 255) / 256), dim3(256), 0, s, d);
 }
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch) {
-  const dim3 grid((d.NP + OBS_BPB - 1) / OBS_BPB), block(64 * OBS_BPB);
-  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, grid, block, 0, s, d, (double *)out, epoch);
-  else hipLaunchKernelGGL(k_observe<float>, grid, block, 0, s, d, (float *)out, epoch);
+  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch);
+  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch);
 }
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt) {
   hipLaunchKernelGGL(k_policy_random, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, ps, pe, salt);
