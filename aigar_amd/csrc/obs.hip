@@ -150,12 +150,13 @@ __device__ __forceinline__ Span clip_to_fov(Span s, double fx, double fy, double
 __device__ __forceinline__ int span_rows(const Span &s) { return (s.bx1 >= s.bx0 && s.by1 >= s.by0) ? s.by1 - s.by0 + 1 : 0; }
 
 template <class P, class F>
-__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, double fx, double fy, double fs, bool want_p,
-                                              bool want_v, P pre, F f) {
+// rmax_c / rmax_v: the arena's largest cell / virus radius (ArenaCtl), read by
+// the caller together with its first loads
+__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, double fx, double fy, double fs,
+                                              double rmax_c, double rmax_v, bool want_p, bool want_v, P pre, F f) {
   const int lane = threadIdx.x & 63;
   const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
-  const ArenaCtl &ctl = d.ctl[a];
-  const double rc = fmax(ctl.rmax_cell, radius_of(kStartMass)), rv = fmax(ctl.rmax_virus, radius_of(kVirusBase));
+  const double rc = fmax(rmax_c, radius_of(kStartMass)), rv = fmax(rmax_v, radius_of(kVirusBase));
   const int Ec = (int)ceil((rc + 1.0) / kBucket) + 1;
   const int Ev = (int)ceil((rv + 1.0) / kBucket) + 1;
   const double h = fs / 2;
@@ -255,6 +256,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
   const int ncell = d.p_ncells[gp];
   const int oslot = lane < kMaxCells ? (int)d.p_list[lane * NP + gp] : 0;
+  const ArenaCtl &ctl = d.ctl[a];
+  const double rmax_c = ctl.rmax_cell, rmax_v = ctl.rmax_virus;  // (the walk's grid expansions)
+  const int pcur = ctl.pcur;                                      // current pellet buffer
   if (!alive) {  // getStateRepresentation returns None for dead players
     for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
     return;
@@ -280,7 +284,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     o += o < 0 ? NP : 0;
     return o >= NP ? o - NP : o;
   };
-  const ArenaCtl &ctl = d.ctl[a];
   // last-frame history grids: independent of the queries, fetched up front
   // (first two squares of each lane; larger grids read the rest in the loop)
   // (GG <= 128: the loop below then issues no load, so no wait on its own stores)
@@ -308,7 +311,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // are flattened with a prefix sum, and each step inspects 64 candidates of any
   // kind with a single round of loads (per-lane base pointers), so the three
   // queries share their memory latency instead of chaining it.
-  const int pcur = ctl.pcur;  // current pellet buffer
 
   auto walk = [&](ObjList &PLx, int capP, ObjList &CLx, int capC, ObjList &VLx, int capV, int &np, int &nc,
                   int &nv) __attribute__((always_inline)) {
@@ -321,7 +323,8 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       }
       list_append(c, CLx, capC, nc);
     };
-    wave_fov_walk(d, a, Q, fx, fy, fs, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, own_cells, [&](bool valid, int kd, size_t g) {
+    wave_fov_walk(d, a, Q, fx, fy, fs, rmax_c, rmax_v, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, own_cells,
+                  [&](bool valid, int kd, size_t g) {
       const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
       const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
       const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
@@ -714,7 +717,8 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   double best = -1;
   uint64_t bord = ~0ull;
   double tx = 0, ty = 0;
-  wave_fov_walk(d, a, Q, fx, fy, fs, true, d.virus_enabled, [] {}, [&](bool valid, int kd, size_t g) {
+  wave_fov_walk(d, a, Q, fx, fy, fs, ctl.rmax_cell, ctl.rmax_virus, true, d.virus_enabled, [] {},
+                [&](bool valid, int kd, size_t g) {
     if (!valid) return;
     const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
     const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
