@@ -1799,10 +1799,14 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     Rect q = footprint(x, y, r, d.size);
     bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int e) {
-      if (!(d.c_flags[e] & F_ALIVE) || (e % NP) == gp) return false;
+      // only the LOWER-index player of a pair is marked: its turn comes first
+      // and resolves the pair ("the one that can eat does", field.py:238-243).
+      // The higher-index side's turn could only see a changed pair, and every
+      // change re-activates it: a growth re-activates the cells overlapping the
+      // grown one; a cell skipped by the live-list quirk re-activates its partners.
+      if (!(d.c_flags[e] & F_ALIVE) || (int)(e % NP) <= gp) return false;
       if (!rect_hit(cell_rect(d, e), q)) return false;
-      // a pair where neither side can eat stays inert until one of them grows,
-      // and every growth re-activates the cells overlapping the grown one
+      // a pair where neither side can eat stays inert until one of them grows
       double me = d.c_m[e];
       return overlap(x, y, m, r, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(m, me) || can_eat(me, m));
     }, d.cshift_c);
@@ -1985,7 +1989,27 @@ __global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *sc
         active_st(d, g, 1);
         if (gpl - a * B > P && lane == 0) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
         wave_fence();
-        if (!pc_eats) break;
+        if (!pc_eats) {
+          // pc left the live list: the cell that moved into its place is skipped
+          // this turn (field.py:236 + player.py:97).  Its pairs with later
+          // players are then theirs to resolve: activate those partners.
+          if (i - 1 < d.p_ncells[gp]) {
+            const size_t sk = (size_t)d.p_list[(i - 1) * NP + gp] * NP + gp;
+            const double sx = d.c_x[sk], sy = d.c_y[sk], sm = d.c_m[sk], sr = d.c_r[sk];
+            wave_grid_for(st, it, d.cols, cell_rect(d, sk), expand_for(rmax), [&](bool valid, int e) {
+              if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gp) return;
+              const double me = d.c_m[e];
+              if (!(overlap(sx, sy, sm, sr, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(sm, me) || can_eat(me, sm))))
+                return;
+              int pe = (int)(e % NP) - a * B;
+              if (pe <= P) return;
+              active_st(d, (size_t)e, 1);
+              atomicOr(&pend[pe >> 5], 1u << (pe & 31));
+            }, d.cshift_c);
+            wave_fence();
+          }
+          break;
+        }
       }
     }
   }
