@@ -20,14 +20,18 @@ def commands(st):
     return np.c_[pf[:, 0], pf[:, 1], pi[:, 2], pi[:, 3]].astype(np.float64)
 
 
-@pytest.mark.parametrize("bots,virus,gsplit,seed", [(16, False, False, 1), (48, True, True, 2), (200, True, True, 3)])
-def test_greedy_population_matches_oracle(bots, virus, gsplit, seed):
-    cfg = make_config(bots=bots, virus=virus, max_viruses=30 if virus else -1.0,
+@pytest.mark.parametrize("bots,virus,gsplit,seed,field,ticks", [
+    (16, False, False, 1, 0, 120), (48, True, True, 2, 0, 120), (200, True, True, 3, 0, 120),
+    (64, True, True, 4, 250, 200),  # crowded: greedy bots hunt each other (playerPlayerOverlap turns, respawns)
+])
+def test_greedy_population_matches_oracle(bots, virus, gsplit, seed, field, ticks):
+    cfg = make_config(bots=bots, virus=virus, max_viruses=30 if virus else -1.0, field_size=field,
                       channels=_abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY, extras=0x3)
     g, o = _lib.Stepper(cfg), Oracle(cfg)
     g.reset(seed)
     o.reset(seed)
-    for t in range(120):
+    kinds = set()
+    for t in range(ticks):
         g.policy_greedy(gsplit)
         o.policy_greedy(gsplit)
         cg, co = commands(g.get_state()), commands(o.get_state())
@@ -35,9 +39,13 @@ def test_greedy_population_matches_oracle(bots, virus, gsplit, seed):
         assert not len(bad), "tick %d bot %d: gpu %s oracle %s" % (t, bad[0][0], cg[bad[0][0]], co[bad[0][0]])
         g.step(1)
         o.step(1)
-        assert np.array_equal(g.events(), o.events()), "events differ at tick %d" % t
+        ev = g.events()
+        assert np.array_equal(ev, o.events()), "events differ at tick %d" % t
+        kinds |= set(ev[:, 1].tolist())
     dif = parity.diff_states(g.get_state(), o.get_state())
     assert not dif, dif
+    if field:  # the crowded world must have exercised cell-eats-cell and deaths
+        assert {_abi.EV_CELL_EAT_CELL, _abi.EV_PLAYER_DEATH} <= kinds, kinds
     g.close()
     o.close()
 
