@@ -123,15 +123,16 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   const size_t ci = (size_t)gi;
   double cmdx, cmdy;
   if (rp.on) {
-    if (!d.p_alive[gp]) return;  // makeMove: dead players keep their command
-    const Command c = random_command(d, gp, rp);
+    const bool live = d.c_flags[ci] & F_ALIVE;
+    if ((!live && gi >= NP) || !d.p_alive[gp]) return;  // (dead players keep their command: makeMove)
+    const Command c = random_command(d, gp, rp);  // (the player's live cells and slot 0 only)
     if (gi < NP) {  // slot 0 stores the player's command
       d.p_cmdx[gp] = c.x;
       d.p_cmdy[gp] = c.y;
       d.p_split[gp] = c.split;
       d.p_eject[gp] = c.eject;
     }
-    if (!(d.c_flags[ci] & F_ALIVE)) return;
+    if (!live) return;
     cmdx = c.x;
     cmdy = c.y;
   } else {
