@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "aigar_math.h"
+#include "aigar_trig.h"
 
 #define AIGAR_D __device__ __forceinline__
 
@@ -91,10 +92,10 @@ AIGAR_D void set_move_direction(double x, double y, double m, double r, double c
   double xd = cpx - x, yd = cpy - y;
   double hyp = xd * xd + yd * yd, r2 = r * r;
   double mod = py_min(hyp, r2) / r2;
-  double ang = atan2(yd, xd);
+  double ang = aigar_math::trig_atan2(yd, xd);  // correctly rounded (aigar_trig.h)
   double sp = kMoveSpeed * aigar_math::pow_cr(m, -0.35);  // correctly rounded (see aigar_math.h)
-  double c = cos(ang);
-  double s = sin(ang);
+  double c, s;
+  aigar_math::trig_sincos(ang, s, c);
   vx = sp * mod * c;
   vy = sp * mod * s;
 }
@@ -102,10 +103,10 @@ AIGAR_D void set_move_direction(double x, double y, double m, double r, double c
 AIGAR_D void add_momentum(double x, double y, double cpx, double cpy, double w, double h, double orig_r,
                           double &svx, double &svy, int &svc) {
   double cx = py_max(0.0, py_min(w, cpx)), cy = py_max(0.0, py_min(h, cpy));
-  double ang = atan2(cy - y, cx - x);
+  double ang = aigar_math::trig_atan2(cy - y, cx - x);
   double sp = 2 + orig_r * 0.05;
-  double c = cos(ang);
-  double s = sin(ang);
+  double c, s;
+  aigar_math::trig_sincos(ang, s, c);
   svx = c * sp;
   svy = s * sp;
   svc = 15;

@@ -209,9 +209,9 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
       // Cell.split (cell.py:72-85)
       double x = cx[ci], y = cy[ci];
       double nm = cm[ci] / 2, nr = radius_of(nm);
-      double ang = atan2(cpy - y, cpx - x);
-      double ca = cos(ang);
-      double sa = sin(ang);
+      double ang = aigar_math::trig_atan2(cpy - y, cpx - x);
+      double ca, sa;
+      aigar_math::trig_sincos(ang, sa, ca);
       double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
       double svx, svy;
       int svc;
@@ -1120,9 +1120,9 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
         double ox = 2 * d.v_x[gv] - d.b_x[g], oy = 2 * d.v_y[gv] - d.b_y[g];
         size_t gn = (size_t)a * d.Vcap + c.n_vir;
         double x = d.v_x[gv], y = d.v_y[gv], nm = m / 2, nr = radius_of(nm);
-        double ang = atan2(oy - y, ox - x);
-        double ca = cos(ang);
-        double sa = sin(ang);
+        double ang = aigar_math::trig_atan2(oy - y, ox - x);
+        double ca, sa;
+        aigar_math::trig_sincos(ang, sa, ca);
         double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
         double svx, svy;
         int svc;
@@ -1306,8 +1306,8 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
           philox((uint64_t)seq, ST_ANGLE, 0, 0, c.key0, c.key1, u);
           int64_t deg = (int64_t)mulhi(u[0], 360);
           double ang = (double)deg * (kPi / 180.0);  // numpy.deg2rad
-          double ca = cos(ang);
-          double sa = sin(ang);
+          double ca, sa;
+          aigar_math::trig_sincos(ang, sa, ca);
           double xp = ca * pr * 12 + px, yp = sa * pr * 12 + py;
           double vx, vy, svx, svy;
           int svc;

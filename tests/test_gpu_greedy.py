@@ -22,7 +22,10 @@ def commands(st):
 
 @pytest.mark.parametrize("bots,virus,gsplit,seed,field,ticks", [
     (16, False, False, 1, 0, 120), (48, True, True, 2, 0, 120), (200, True, True, 3, 0, 120),
-    (64, True, True, 4, 250, 200),  # crowded: greedy bots hunt each other (playerPlayerOverlap turns, respawns)
+    # crowded: greedy bots hunt each other (playerPlayerOverlap turns, respawns); with correctly rounded device
+    # atan2/sin/cos (aigar_trig.h) the world stays within 1e-9 of the oracle for 600 ticks (OCML trig: 1e-5 is
+    # exceeded at tick ~277)
+    (64, True, True, 4, 250, 600), (64, True, True, 5, 250, 600),
 ])
 def test_greedy_population_matches_oracle(bots, virus, gsplit, seed, field, ticks):
     cfg = make_config(bots=bots, virus=virus, max_viruses=30 if virus else -1.0, field_size=field,
@@ -42,7 +45,7 @@ def test_greedy_population_matches_oracle(bots, virus, gsplit, seed, field, tick
         ev = g.events()
         assert np.array_equal(ev, o.events()), "events differ at tick %d" % t
         kinds |= set(ev[:, 1].tolist())
-    dif = parity.diff_states(g.get_state(), o.get_state())
+    dif = parity.diff_states(g.get_state(), o.get_state(), ftol=1e-9 if field else parity.FTOL)
     assert not dif, dif
     if field:  # the crowded world must have exercised cell-eats-cell and deaths
         assert {_abi.EV_CELL_EAT_CELL, _abi.EV_PLAYER_DEATH} <= kinds, kinds

@@ -28,3 +28,19 @@ def test_mod_pos_matches_python_float_mod(tmp_path):
     out = subprocess.run([exe, "300000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatches=0" in out.stdout, out.stdout
+
+
+def test_trig_is_correctly_rounded(tmp_path):
+    """aigar_trig.h sin_cr / cos_cr / atan2_cr == the quad-precision value
+    rounded to double on the stepper's input shapes (host build).  glibc, which
+    the reference runs, differs from that rounding on ~0.1% of them; OCML on
+    4-27% (tools/micro/trig_vs_glibc.hip)."""
+    exe = str(tmp_path / "check_trig")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I",
+                           os.path.join(ROOT, "aigar_amd", "csrc"), os.path.join(ROOT, "tools", "gen", "check_trig.cpp"),
+                           "-lquadmath", "-o", exe])
+    out = subprocess.run([exe, "100000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0 " in out.stdout, out.stdout
+    glibc = float(out.stdout.split("(")[1].split("%")[0])
+    assert glibc < 0.5, out.stdout
