@@ -61,6 +61,7 @@ def load(build_if_missing=False):
         "aigar_step": [vp, i32],
         "aigar_obs_len": [vp],
         "aigar_observe": [vp, vp, i32, i32],
+        "aigar_observe_pixels": [vp, vp, i32, u64, i32, i32],
         "aigar_set_actions": [vp, vp, vp, i32],
         "aigar_player_stats": [vp, vp, i32],
         "aigar_get_state": [vp, i32, C.POINTER(_abi.State)],
@@ -220,6 +221,17 @@ class Stepper:
         dt = 0 if (getattr(out, "dtype", None) in (np.float64,) or str(getattr(out, "dtype", "")) == "torch.float64") else 1
         p, dev = _ptr(out)
         self._chk(self.L.aigar_observe(self.h, p, dt, dev))
+        return out
+
+    def observe_pixels(self, side=42, color_seed=0, rgb=True, out=None):
+        """RGBGenerator.get_cnn_inputRGB for every player (rgbGenerator.py:95-110):
+        uint8 [NP, side, side, 3] when rgb, else float64/float32 grayscale [NP, side, side]."""
+        if out is None:
+            out = np.zeros((self.NP, side, side, 3), np.uint8) if rgb else np.zeros((self.NP, side, side), np.float64)
+        d = str(getattr(out, "dtype", ""))
+        dt = 2 if "uint8" in d else 0 if "float64" in d else 1
+        p, dev = _ptr(out)
+        self._chk(self.L.aigar_observe_pixels(self.h, p, int(side), int(color_seed), dt, dev))
         return out
 
     def set_actions(self, cur=None, prev=None):

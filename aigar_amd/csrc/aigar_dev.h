@@ -63,7 +63,7 @@ struct ArenaCtl {
 
 enum : uint32_t {
   ERR_PELLET_CAP = 1, ERR_BLOB_CAP = 2, ERR_VIRUS_CAP = 4, ERR_EVENT_CAP = 8, ERR_WORK_CAP = 16,
-  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128
+  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };

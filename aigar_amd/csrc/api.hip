@@ -19,6 +19,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
                  const RandomPolicy *rp = nullptr);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch);
+int launch_observe_pixels(const Dev &d, hipStream_t s, void *out, int dtype, int side, uint64_t seed);
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
 void launch_player_stats(const Dev &d, hipStream_t s, double *out);
 void launch_player_fov(const Dev &d, hipStream_t s);
@@ -61,6 +62,8 @@ struct aigar_handle {
   double *d_cmd = nullptr, *d_stats = nullptr;
   uint8_t *d_mask = nullptr;
   void *d_obs = nullptr;
+  void *d_pix = nullptr;  // host-destination staging for aigar_observe_pixels
+  size_t pix_bytes = 0;
   std::vector<void *> allocs;
   bool profile = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -117,6 +120,9 @@ static void free_all(aigar_handle *h) {
   if (h->env_graph) (void)hipGraphExecDestroy(h->env_graph);
   for (void *p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
+  if (h->d_pix) (void)hipFree(h->d_pix);
+  h->d_pix = nullptr;
+  h->pix_bytes = 0;
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto &m : h->marks) {
@@ -301,7 +307,7 @@ static int check_device_errors(aigar_handle *h) {
   for (int a = 0; a < h->d.A; a++)
     if (ctl[a].err)
       return fail("device error bits 0x%x in arena %d (1 pellet cap, 2 blob cap, 4 virus cap, 8 event cap, "
-                  "16 worklist cap, 32 observation cap, 64 candidate cap)",
+                  "16 worklist cap, 32 observation cap, 64 candidate cap, 128 slot, 256 pixel-frame object cap)",
                   ctl[a].err, a);
   return 0;
 }
@@ -512,6 +518,37 @@ extern "C" int aigar_observe(aigar_handle *h, void *out, int dtype, int on_devic
   if (!on_device) {
     size_t bytes = (size_t)h->d.NP * h->d.L * (dtype == 0 ? 8 : 4);
     HIPCHK(hipMemcpyAsync(out, h->d_obs, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return check_device_errors(h);
+  }
+  return 0;
+}
+
+extern "C" int aigar_observe_pixels(aigar_handle *h, void *out, int side, uint64_t color_seed, int dtype,
+                                    int on_device) {
+  if (!h || !out) return fail("null argument");
+  if (side < 1 || side > 84) return fail("pixel frame side must be in [1, 84], got %d", side);
+  if (dtype < 0 || dtype > 2) return fail("dtype must be 0 (float64 gray), 1 (float32 gray) or 2 (uint8 rgb)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t bytes = (size_t)h->d.NP * side * side * (dtype == 0 ? 8 : dtype == 1 ? 4 : 3);
+  void *dst = out;
+  if (!on_device) {
+    if (bytes > h->pix_bytes) {
+      if (h->d_pix) HIPCHK(hipFree(h->d_pix));
+      h->d_pix = nullptr;
+      h->pix_bytes = 0;
+      HIPCHK(hipMalloc(&h->d_pix, bytes));
+      h->pix_bytes = bytes;
+    }
+    dst = h->d_pix;
+  }
+  {
+    Mark m(h, "observe_pixels");
+    if (launch_observe_pixels(h->d, h->stream, dst, dtype, side, color_seed)) return fail("bad pixel launch");
+  }
+  HIPCHK(hipGetLastError());
+  if (!on_device) {
+    HIPCHK(hipMemcpyAsync(out, h->d_pix, bytes, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return check_device_errors(h);
   }

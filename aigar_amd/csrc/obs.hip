@@ -894,6 +894,23 @@ __global__ void __launch_bounds__(256) k_player_fov(Dev d) { fov_cache_thread(d,
 void launch_player_fov(const Dev &d, hipStream_t s) {
   hipLaunchKernelGGL(k_player_fov, dim3((d.NP + 255) / 256), dim3(256), 0, s, d);
 }
+// ---------------------------------------------------- pixel observation
+// RGBGenerator.get_cnn_inputRGB (rgbGenerator.py:95-110) for every player: a
+// white side x side frame, every pellet / blob / virus / player cell in the FOV
+// (drawAllCells, rgbGenerator.py:60-68) stable-sorted by mass and drawn in
+// that order, then numpy.average(weights=[0.298, 0.587, 0.114]) grayscale.
+// pygame's primitives follow the published SDL_gfx 2.0 algorithms (see
+// oracle/oracle.c pixels_one; pygame itself is absent, parity with it is
+// unpinned): rad >= 4 filledCircle + aacircle rim (black for viruses), else
+// pygame.draw.circle as filledEllipse spans.
+// One 64-lane block per player, the frame in LDS (packed 0x00RRGGBB): the FOV
+// objects are gathered by the observation walk (+ the arena's blob slots),
+// culled to those that touch the frame, bitonic-sorted by (mass, kind, seq),
+// then drawn one by one: lane 0 runs the span recurrence into a half-width
+// table, all lanes fill the spans, lane 0 runs the anti-aliased rim (its
+// blends are order-dependent).
+#include "pixels.inc"
+
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch) {
   if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch);
   else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch);

@@ -224,6 +224,15 @@ int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p, void *obs
  * Updates each bot's last-frame history grids like the reference does. */
 int aigar_obs_len(aigar_handle *h);
 int aigar_observe(aigar_handle *h, void *out, int dtype, int on_device);
+/* RGBGenerator.get_cnn_inputRGB (rgbGenerator.py:95-110) for every player: a
+ * side x side frame (side <= 84; CNN_INPUT_DIM_* of networkParameters.py) of
+ * the player's FOV, objects drawn in stable mass order with SDL_gfx circle
+ * primitives.  dtype 2: uint8 RGB out[A*B][side][side][3] in pygame surfarray
+ * order [x][y][rgb]; 0 / 1: float64 / float32 grayscale out[A*B][side][side]
+ * (numpy.average with weights 0.298, 0.587, 0.114).  color_seed picks the
+ * per-player / per-pellet colours (the reference draws them from numpy RNG,
+ * cell.py:31, player.py:39).  Dead players get zeros (uint8) / NaN (gray). */
+int aigar_observe_pixels(aigar_handle *h, void *out, int side, uint64_t color_seed, int dtype, int on_device);
 /* bot.currentAction / bot.lastAction used by the action extras: [A*B][4] each (may be NULL). */
 int aigar_set_actions(aigar_handle *h, const double *cur, const double *prev, int on_device);
 

@@ -1183,7 +1183,232 @@ static void observe_one(Oracle *O, Arena *A, int p, double *out) {
   free(gP); free(gW); free(gE); free(gS); free(gV);
 }
 
+/* ------------------------------------------------ pixel observation ---- */
+/* RGBGenerator.get_cnn_inputRGB (rgbGenerator.py:95-110): white frame, every
+ * pellet / blob / virus / player cell in the FOV (rgbGenerator.py:60-68),
+ * stable-sorted by mass, drawn with pygame's primitives.  pygame (1.9.4,
+ * src/pip.txt) is not in this image, so the primitives are restated from the
+ * published SDL_gfx 2.0 algorithms: filledCircleColor (midpoint spans),
+ * aacircleColor = aaellipseColor (Wu-style weighted rim) with
+ * pixelColorWeight blending, and pygame.draw.circle (width 0) as
+ * filledEllipseColor spans.  Parity with pygame itself is UNPINNED.
+ * Frame: RGB bytes, surfarray order [x][y][3]. */
+typedef struct { uint8_t *px; int L; } Frame; /* px[(y * L + x) * 3 + c] */
+static void fr_put(Frame *f, int x, int y, const uint8_t *c) {
+  if (x < 0 || y < 0 || x >= f->L || y >= f->L) return; /* clip rect = surface */
+  uint8_t *p = f->px + ((size_t)y * f->L + x) * 3;
+  p[0] = c[0]; p[1] = c[1]; p[2] = c[2];
+}
+static void fr_hline(Frame *f, int x1, int x2, int y, const uint8_t *c) { /* hlineColor, opaque */
+  if (x1 > x2) { int t = x1; x1 = x2; x2 = t; }
+  for (int x = x1; x <= x2; x++) fr_put(f, x, y, c);
+}
+/* pixelColorWeight: alpha = (255 * weight) >> 8, then the 32-bpp blend
+ * d + ((s - d) * alpha >> 8) per channel (alpha 255: plain store) */
+static void fr_weight(Frame *f, int x, int y, const uint8_t *c, int weight) {
+  int alpha = (255 * weight) >> 8;
+  if (x < 0 || y < 0 || x >= f->L || y >= f->L) return;
+  uint8_t *p = f->px + ((size_t)y * f->L + x) * 3;
+  for (int k = 0; k < 3; k++) {
+    int d = p[k];
+    p[k] = (uint8_t)(alpha == 255 ? c[k] : d + (((c[k] - d) * alpha) >> 8));
+  }
+}
+static void sdl_filled_circle(Frame *f, int x, int y, int rad, const uint8_t *c) { /* filledCircleColor */
+  if (rad == 0) { fr_put(f, x, y, c); return; }
+  int cx = 0, cy = rad, ocx = -1, ocy = -1, df = 1 - rad, d_e = 3, d_se = -2 * rad + 5;
+  do {
+    if (ocy != cy) {
+      if (cy > 0) { fr_hline(f, x - cx, x + cx, y + cy, c); fr_hline(f, x - cx, x + cx, y - cy, c); }
+      else fr_hline(f, x - cx, x + cx, y, c);
+      ocy = cy;
+    }
+    if (ocx != cx) {
+      if (cx != cy) {
+        if (cx > 0) { fr_hline(f, x - cy, x + cy, y - cx, c); fr_hline(f, x - cy, x + cy, y + cx, c); }
+        else fr_hline(f, x - cy, x + cy, y, c);
+      }
+      ocx = cx;
+    }
+    if (df < 0) { df += d_e; d_e += 2; d_se += 2; }
+    else { df += d_se; d_e += 2; d_se += 4; cy--; }
+    cx++;
+  } while (cx <= cy);
+}
+static void sdl_filled_ellipse(Frame *f, int x, int y, int rx, int ry, const uint8_t *c) { /* filledEllipseColor */
+  if (rx == 0) { for (int yy = y - ry; yy <= y + ry; yy++) fr_put(f, x, yy, c); return; }
+  if (ry == 0) { fr_hline(f, x - rx, x + rx, y, c); return; }
+  int oh = 0xFFFF, oi = 0xFFFF, oj = 0xFFFF, ok = 0xFFFF, ix, iy, h, i, j, k;
+  if (rx > ry) {
+    ix = 0; iy = rx * 64;
+    do {
+      h = (ix + 32) >> 6; i = (iy + 32) >> 6; j = (h * ry) / rx; k = (i * ry) / rx;
+      if (ok != k && oj != k) {
+        if (k > 0) { fr_hline(f, x - h, x + h, y + k, c); fr_hline(f, x - h, x + h, y - k, c); }
+        else fr_hline(f, x - h, x + h, y, c);
+        ok = k;
+      }
+      if (oj != j && ok != j && k != j) {
+        if (j > 0) { fr_hline(f, x - i, x + i, y + j, c); fr_hline(f, x - i, x + i, y - j, c); }
+        else fr_hline(f, x - i, x + i, y, c);
+        oj = j;
+      }
+      ix = ix + iy / rx; iy = iy - ix / rx;
+    } while (i > h);
+  } else {
+    ix = 0; iy = ry * 64;
+    do {
+      h = (ix + 32) >> 6; i = (iy + 32) >> 6; j = (h * rx) / ry; k = (i * rx) / ry;
+      if (oi != i && oh != i) {
+        if (i > 0) { fr_hline(f, x - j, x + j, y + i, c); fr_hline(f, x - j, x + j, y - i, c); }
+        else fr_hline(f, x - j, x + j, y, c);
+        oi = i;
+      }
+      if (oh != h && oi != h && i != h) {
+        if (h > 0) { fr_hline(f, x - k, x + k, y + h, c); fr_hline(f, x - k, x + k, y - h, c); }
+        else fr_hline(f, x - k, x + k, y, c);
+        oh = h;
+      }
+      ix = ix + iy / ry; iy = iy - ix / ry;
+    } while (i > h);
+  }
+}
+static void sdl_aa_ellipse(Frame *f, int xc, int yc, int rx, int ry, const uint8_t *c) { /* aaellipseColor */
+  int a2 = rx * rx, b2 = ry * ry, ds = 2 * a2, dt = 2 * b2, xc2 = 2 * xc, yc2 = 2 * yc;
+  double sab = sqrt((double)(a2 + b2));
+  int od = (int)lrint(sab * 0.01) + 1;
+  int dxt = (int)lrint((double)a2 / sab) + od;
+  int t = 0, s = -2 * a2 * ry, d = 0, x = xc, y = yc - ry, xs, ys, xx, yy;
+  fr_put(f, x, y, c); fr_put(f, xc2 - x, y, c); fr_put(f, x, yc2 - y, c); fr_put(f, xc2 - x, yc2 - y, c);
+  for (int i = 1; i <= dxt; i++) {
+    x--;
+    d += t - b2;
+    if (d >= 0) ys = y - 1;
+    else if ((d - s - a2) > 0) {
+      if ((2 * d - s - a2) >= 0) ys = y + 1;
+      else { ys = y; y++; d -= s + a2; s += ds; }
+    } else { y++; ys = y + 1; d -= s + a2; s += ds; }
+    t -= dt;
+    float cp = s != 0 ? (float)abs(d) / (float)abs(s) : 1.0f;
+    if (cp > 1.0f) cp = 1.0f;
+    int weight = (uint8_t)(cp * 255), iweight = 255 - weight;
+    xx = xc2 - x;
+    fr_weight(f, x, y, c, iweight); fr_weight(f, xx, y, c, iweight);
+    fr_weight(f, x, ys, c, weight); fr_weight(f, xx, ys, c, weight);
+    yy = yc2 - y;
+    fr_weight(f, x, yy, c, iweight); fr_weight(f, xx, yy, c, iweight);
+    yy = yc2 - ys;
+    fr_weight(f, x, yy, c, weight); fr_weight(f, xx, yy, c, weight);
+  }
+  int dyt = (int)lrint((double)b2 / sab) + od;
+  for (int i = 1; i <= dyt; i++) {
+    y++;
+    d -= s + a2;
+    if (d <= 0) xs = x + 1;
+    else if ((d + t - b2) < 0) {
+      if ((2 * d + t - b2) <= 0) xs = x - 1;
+      else { xs = x; x--; d += t - b2; t -= dt; }
+    } else { x--; xs = x - 1; d += t - b2; t -= dt; }
+    s += ds;
+    float cp = t != 0 ? (float)abs(d) / (float)abs(t) : 1.0f;
+    if (cp > 1.0f) cp = 1.0f;
+    int weight = (uint8_t)(cp * 255), iweight = 255 - weight;
+    xx = xc2 - x; yy = yc2 - y;
+    fr_weight(f, x, y, c, iweight); fr_weight(f, xx, y, c, iweight);
+    fr_weight(f, x, yy, c, iweight); fr_weight(f, xx, yy, c, iweight);
+    xx = xc2 - xs;
+    fr_weight(f, xs, y, c, weight); fr_weight(f, xx, y, c, weight);
+    fr_weight(f, xs, yy, c, weight); fr_weight(f, xx, yy, c, weight);
+  }
+}
+
+/* colours: the facade's deterministic stand-ins for the reference's random
+ * draws (aigar_amd/model.py player_color / pellet_color; splitmix64 finaliser) */
+static uint64_t mix64(uint64_t v) {
+  v += 0x9E3779B97F4A7C15ull;
+  v = (v ^ (v >> 30)) * 0xBF58476D1CE4E5B9ull;
+  v = (v ^ (v >> 27)) * 0x94D049BB133111EBull;
+  return v ^ (v >> 31);
+}
+static void player_rgb(int index, uint64_t seed, uint8_t *c) { /* Player.randomizeColor (player.py:38-41) */
+  for (uint64_t k = 0;; k++) {
+    uint64_t h = mix64((seed << 32) ^ ((uint64_t)index << 8) ^ k);
+    c[0] = h & 255; c[1] = (h >> 8) & 255; c[2] = (h >> 16) & 255;
+    if (c[0] + c[1] + c[2] <= 600) return;
+  }
+}
+static void pellet_rgb(int64_t seq, uint64_t seed, uint8_t *c) { /* cell.py:31 (also blobs: Cell(..., None)) */
+  uint64_t h = mix64((seed << 40) ^ (uint64_t)seq ^ 0x5E11E7ull);
+  c[0] = 50 + h % 150; c[1] = 50 + (h >> 16) % 150; c[2] = 50 + (h >> 32) % 150;
+}
+
+typedef struct { const Cell *c; int kind; } PixObj; /* kind: 0 pellet, 1 blob, 2 virus, 3 player cell */
+static int cmp_pix(const void *pa, const void *pb) {
+  const PixObj *a = (const PixObj *)pa, *b = (const PixObj *)pb;
+  /* list.sort(key=mass) is stable over pellets + blobs + viruses + playerCells,
+   * each in canonical (creation sequence) order */
+  if (a->c->mass != b->c->mass) return a->c->mass < b->c->mass ? -1 : 1;
+  if (a->kind != b->kind) return a->kind - b->kind;
+  return a->c->seq < b->c->seq ? -1 : (a->c->seq > b->c->seq);
+}
+
+static void pixels_one(Arena *A, int p, int L, uint64_t seed, uint8_t *out) {
+  Player *P = &A->pl[p];
+  memset(out, 0, (size_t)L * L * 3);
+  if (!P->alive) return;
+  double fx, fy, fs = player_fov_size(P);
+  player_fov_pos(P, &fx, &fy);
+  CVec q = {0};
+  PixObj *objs = NULL;
+  int n = 0, cap = 0;
+  const Hash *hs[4] = {&A->ph, &A->bh, &A->vh, &A->plh}; /* drawAllCells (rgbGenerator.py:60-68) */
+  for (int k = 0; k < 4; k++) {
+    hash_query(hs[k], fx, fy, fs / 2, &q);
+    for (int i = 0; i < q.n; i++) {
+      if (!in_fov(q.a[i], fx, fy, fs)) continue;
+      if (n == cap) { cap = cap ? 2 * cap : 64; objs = (PixObj *)realloc(objs, sizeof(PixObj) * cap); }
+      objs[n].c = q.a[i];
+      objs[n++].kind = k;
+    }
+  }
+  if (n > 1) qsort(objs, n, sizeof(PixObj), cmp_pix);
+  Frame f = {(uint8_t *)malloc((size_t)L * L * 3), L};
+  memset(f.px, 255, (size_t)L * L * 3); /* screen.fill(WHITE) */
+  const double scale = (double)L / fs;  /* screenDims / fovSize */
+  for (int i = 0; i < n; i++) { /* drawSingleCell (rgbGenerator.py:36-53) */
+    const Cell *c = objs[i].c;
+    uint8_t col[3], rim[3];
+    if (objs[i].kind == 3) player_rgb(c->player, seed, col);
+    else if (objs[i].kind == 2) { col[0] = 0; col[1] = 255; col[2] = 0; }
+    else pellet_rgb(c->seq, seed, col);
+    int rad = (int)(c->radius * scale);
+    int x = (int)(int64_t)(((c->x - fx) + fs / 2) * scale), y = (int)(int64_t)(((c->y - fy) + fs / 2) * scale);
+    if (rad >= 4) {
+      sdl_filled_circle(&f, x, y, rad, col);
+      if (objs[i].kind == 2) { rim[0] = rim[1] = rim[2] = 0; } /* viruses: black rim */
+      else memcpy(rim, col, 3);
+      sdl_aa_ellipse(&f, x, y, rad, rad, rim);
+    } else {
+      sdl_filled_ellipse(&f, x, y, rad, rad, col); /* pygame.draw.circle(width 0) */
+    }
+  }
+  for (int x = 0; x < L; x++) /* surfarray.array3d: [x][y][rgb] */
+    for (int y = 0; y < L; y++) memcpy(out + ((size_t)x * L + y) * 3, f.px + ((size_t)y * L + x) * 3, 3);
+  free(f.px);
+  free(objs);
+  cv_free(&q);
+}
+
 /* ------------------------------------------------------------ API ---- */
+int oracle_pixels(void *h, int L, uint64_t seed, uint8_t *out) {
+  Oracle *O = (Oracle *)h;
+  for (int a = 0; a < O->A; a++) {
+    Arena *A = &O->ar[a];
+    for (int p = 0; p < A->B; p++) pixels_one(A, p, L, seed, out + (size_t)L * L * 3 * ((size_t)a * A->B + p));
+  }
+  return 0;
+}
+
 static int obs_len(const aigar_config *c) {
   int G = c->grid_squares ? c->grid_squares : 11, n = 0, e = 0;
   for (int b = 0; b < 10; b++) n += (c->obs_channels >> b) & 1;

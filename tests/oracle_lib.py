@@ -42,6 +42,7 @@ def lib():
         L.oracle_step.argtypes = [vp, C.c_int]
         L.oracle_observe.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_obs_len.argtypes = [vp]
+        L.oracle_pixels.argtypes = [vp, C.c_int, C.c_uint64, C.POINTER(C.c_uint8)]
         L.oracle_player_stats.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_get_events.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.c_int]
         L.oracle_reset_obs_state.argtypes = [vp]
@@ -135,6 +136,13 @@ class Oracle:
     def observe(self):
         out = np.zeros((self.n_total, self.obs_len), np.float64)
         self._chk(self.L.oracle_observe(self.h, _dp(out)))
+        return out
+
+    def pixels(self, side=42, color_seed=0):
+        """RGB frames of RGBGenerator.get_cnn_inputRGB (surfarray order [x][y][rgb]),
+        uint8 [players, side, side, 3]; dead players all zero."""
+        out = np.zeros((self.n_total, side, side, 3), np.uint8)
+        self._chk(self.L.oracle_pixels(self.h, side, color_seed, out.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out
 
     def player_stats(self):

@@ -1,0 +1,98 @@
+"""GPU parity of the pixel observation (RGBGenerator.get_cnn_inputRGB,
+rgbGenerator.py:95-110) against the CPU oracle's restatement (oracle.c
+pixels_one).  Byte work: the RGB frames must be bit-exact.  pygame is absent
+here, so parity with pygame itself is unpinned (the oracle follows the
+published SDL_gfx algorithms); this test pins the HIP kernel to the oracle.
+"""
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import Oracle, make_config
+import parity
+
+pytestmark = pytest.mark.gpu
+
+_lib = pytest.importorskip("aigar_amd._lib")
+
+CH = _abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY
+
+
+def pair(cfg, seed):
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    g.reset(seed)
+    o.reset(seed)
+    return g, o
+
+
+def step_both(g, o, ticks, seed, bots, ps=0.0, pe=0.0):
+    rng = np.random.default_rng(seed)
+    size = g.get_state()["field_size"]
+    err, _ = parity.run_pair(g, o, ticks, lambda t: parity.synthetic_commands(rng, None, bots, size, ps, pe))
+    assert err is None, err
+
+
+def assert_frames_equal(fg, fo):
+    bad = np.argwhere(np.any(fg != fo, axis=-1))
+    assert bad.size == 0, "%d pixels differ, first (player, x, y) %s: gpu %s oracle %s" % (
+        len(bad), tuple(bad[0]), fg[tuple(bad[0])], fo[tuple(bad[0])])
+
+
+@pytest.mark.parametrize("bots,ticks,seed,side,kw", [
+    (1, 0, 1, 42, dict(max_pellets=100, field_size=1000)),
+    (1, 200, 1, 84, dict(max_pellets=100, field_size=1000)),
+    (32, 60, 2, 42, dict(p_split=0.05, p_eject=0.05)),
+    (32, 60, 3, 84, dict(virus=True, max_viruses=40, p_split=0.05, p_eject=0.05)),
+    (48, 120, 4, 42, dict(field_size=120, p_split=0.05, p_eject=0.05)),   # crowded: big cells, deaths
+    (256, 20, 5, 42, dict(max_pellets=10000, field_size=1200)),           # C2
+])
+def test_pixels_match_oracle(bots, ticks, seed, side, kw):
+    kw = dict(kw)
+    ps, pe = kw.pop("p_split", 0.0), kw.pop("p_eject", 0.0)
+    virus = kw.pop("virus", False)
+    cfg = make_config(bots=bots, virus=virus, channels=CH, extras=0, **kw)
+    g, o = pair(cfg, seed)
+    if ticks:
+        step_both(g, o, ticks, seed, bots, ps, pe)
+    for cseed in (0, 12345):
+        fg, fo = g.observe_pixels(side, cseed), o.pixels(side, cseed)
+        assert fg.shape == fo.shape == (bots, side, side, 3)
+        assert_frames_equal(fg, fo)
+    if ticks == 0:  # cells enter the player hash only at the first tick (field.py:121-132)
+        return
+    # the frames are not trivially white: the own cell is drawn
+    alive = g.player_stats()[:, 0] > 0
+    assert np.all(np.any(fg[alive] != 255, axis=(1, 2, 3)))
+
+
+def test_pixels_gray_is_weighted_average():
+    cfg = make_config(bots=16, virus=True, max_viruses=10, channels=CH, extras=0)
+    g, o = pair(cfg, 9)
+    step_both(g, o, 30, 9, 16, 0.05, 0.0)
+    rgb = g.observe_pixels(42, 3)
+    gray = g.observe_pixels(42, 3, rgb=False)
+    gray32 = g.observe_pixels(42, 3, out=np.zeros((16, 42, 42), np.float32))
+    alive = g.player_stats()[:, 0] > 0
+    ref = np.average(rgb.astype(np.float64), axis=-1, weights=[0.298, 0.587, 0.114])
+    assert np.array_equal(gray[alive], ref[alive])
+    assert np.array_equal(gray32[alive], ref[alive].astype(np.float32))
+    assert np.all(np.isnan(gray[~alive]))
+
+
+def test_pixels_on_device_matches_host():
+    torch = pytest.importorskip("torch")
+    cfg = make_config(bots=64, channels=CH, extras=0)
+    g = _lib.Stepper(cfg)
+    g.reset(21)
+    host = g.observe_pixels(42, 0)
+    dev = torch.zeros((64, 42, 42, 3), dtype=torch.uint8, device="cuda")
+    g.observe_pixels(42, 0, out=dev)
+    g.sync()
+    assert np.array_equal(dev.cpu().numpy(), host)
+
+
+def test_pixels_rejects_bad_side():
+    g = _lib.Stepper(make_config(bots=2, channels=CH, extras=0))
+    g.reset(0)
+    with pytest.raises(RuntimeError):
+        g.observe_pixels(85, 0)
