@@ -172,6 +172,7 @@ def main():
                     help="also time this many independent arenas of the same workload stepped together on "
                          "the GPU (reported under 'batched', never as 'value'); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pixels", action="store_true", help="skip the pixel-observation side measurement")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--policy", default="random", choices=["random", "greedy"],
@@ -239,6 +240,21 @@ def main():
     pol_ms, pol_n = stp.kernel_time("policy")
     stp.profile(False)
     stp.sync()
+    pixels = None
+    if not args.no_pixels:  # RGBGenerator.get_cnn_inputRGB for every bot (side 42, uint8 RGB): a side line,
+        side, reps = 42, 20  # not part of the env-step metric (the reference's CNN pixel mode is off by default)
+        frames = torch.empty((bots, side, side, 3), dtype=torch.uint8, device="cuda")
+        stp.observe_pixels(side, 0, out=frames)
+        stp.profile(True)
+        for _ in range(reps):
+            stp.observe_pixels(side, 0, out=frames)
+        torch.cuda.synchronize()
+        pix_ms, pix_n = stp.kernel_time("observe_pixels")
+        stp.profile(False)
+        stp.sync()
+        pix_s = pix_ms / max(1, pix_n) / 1e3
+        pixels = {"side": side, "dtype": "u8 rgb", "frames_per_s": bots / pix_s, "avg_launch_ms": pix_s * 1e3,
+                  "output_GB_s": bots * side * side * 3 / pix_s / 1e9}
     st = stp.get_state()
     work = stp.counters()
     value = replicas.job_throughput(bots * args.steps, world, elapsed)
@@ -285,6 +301,8 @@ def main():
                   "serial_work_per_tick": {k: round(v / max(1, work["ticks"]), 3) for k, v in work.items()
                                            if k != "ticks"}},
     }
+    if pixels is not None:
+        out["pixels"] = pixels
     if rank == 0 and world == 1 and args.batched_arenas > 1 and not args.arenas:
         out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (N = 1 only)
