@@ -45,6 +45,8 @@ def assert_frames_equal(fg, fo):
     (32, 60, 3, 84, dict(virus=True, max_viruses=40, p_split=0.05, p_eject=0.05)),
     (48, 120, 4, 42, dict(field_size=120, p_split=0.05, p_eject=0.05)),   # crowded: big cells, deaths
     (256, 20, 5, 42, dict(max_pellets=10000, field_size=1200)),           # C2
+    (8, 30, 6, 42, dict(field_size=100, max_pellets=1500)),                # >255 small objects per frame
+    (8, 30, 7, 84, dict(field_size=100, max_pellets=1500, p_split=0.1)),
 ])
 def test_pixels_match_oracle(bots, ticks, seed, side, kw):
     kw = dict(kw)
