@@ -19,7 +19,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
                  const RandomPolicy *rp = nullptr);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch);
-int launch_observe_pixels(const Dev &d, hipStream_t s, void *out, int dtype, int side, uint64_t seed);
+int launch_observe_pixels(const Dev &d, hipStream_t s, void *out, int dtype, int side, uint64_t seed, uint8_t *ovf);
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
 void launch_player_stats(const Dev &d, hipStream_t s, double *out);
 void launch_player_fov(const Dev &d, hipStream_t s);
@@ -63,6 +63,7 @@ struct aigar_handle {
   uint8_t *d_mask = nullptr;
   void *d_obs = nullptr;
   void *d_pix = nullptr;  // host-destination staging for aigar_observe_pixels
+  uint8_t *d_pix_ovf = nullptr;  // per player: frame left to the pixel kernel's second pass
   size_t pix_bytes = 0;
   std::vector<void *> allocs;
   bool profile = false;
@@ -122,6 +123,7 @@ static void free_all(aigar_handle *h) {
   h->allocs.clear();
   if (h->d_pix) (void)hipFree(h->d_pix);
   h->d_pix = nullptr;
+  h->d_pix_ovf = nullptr;  // (one of allocs)
   h->pix_bytes = 0;
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -531,6 +533,10 @@ extern "C" int aigar_observe_pixels(aigar_handle *h, void *out, int side, uint64
   if (dtype < 0 || dtype > 2) return fail("dtype must be 0 (float64 gray), 1 (float32 gray) or 2 (uint8 rgb)");
   HIPCHK(hipSetDevice(h->cfg.device));
   const size_t bytes = (size_t)h->d.NP * side * side * (dtype == 0 ? 8 : dtype == 1 ? 4 : 3);
+  if (!h->d_pix_ovf) {
+    h->d_pix_ovf = dalloc<uint8_t>(h, h->d.NP);
+    if (!h->d_pix_ovf) return fail("out of device memory");
+  }
   void *dst = out;
   if (!on_device) {
     if (bytes > h->pix_bytes) {
@@ -544,7 +550,7 @@ extern "C" int aigar_observe_pixels(aigar_handle *h, void *out, int side, uint64
   }
   {
     Mark m(h, "observe_pixels");
-    if (launch_observe_pixels(h->d, h->stream, dst, dtype, side, color_seed)) return fail("bad pixel launch");
+    if (launch_observe_pixels(h->d, h->stream, dst, dtype, side, color_seed, h->d_pix_ovf)) return fail("bad pixel launch");
   }
   HIPCHK(hipGetLastError());
   if (!on_device) {

@@ -42,6 +42,7 @@ def assert_frames_equal(fg, fo):
     (1, 0, 1, 42, dict(max_pellets=100, field_size=1000)),
     (1, 200, 1, 84, dict(max_pellets=100, field_size=1000)),
     (32, 60, 2, 42, dict(p_split=0.05, p_eject=0.05)),
+    (32, 60, 2, 41, dict(p_split=0.05, p_eject=0.05)),                    # odd side: byte-store path
     (32, 60, 3, 84, dict(virus=True, max_viruses=40, p_split=0.05, p_eject=0.05)),
     (48, 120, 4, 42, dict(field_size=120, p_split=0.05, p_eject=0.05)),   # crowded: big cells, deaths
     (256, 20, 5, 42, dict(max_pellets=10000, field_size=1200)),           # C2
