@@ -354,6 +354,11 @@ class Field:
         """Ordered (tick, code, a, b) rows of the last step (record_events=True)."""
         return self.stepper.events()
 
+    def observe_pixels_all(self, side=42, rgb=False, out=None, color_seed=None):
+        """RGBGenerator.get_cnn_inputRGB of every player in one launch: uint8 [B, side, side, 3]
+        (rgb) or float64 grayscale [B, side, side]; surfarray order [x][y]."""
+        return self.stepper.observe_pixels(side, self.seed if color_seed is None else color_seed, rgb=rgb, out=out)
+
     # ---- snapshot-backed compatibility getters
     def _snapshot(self):
         if "state" not in self._cache:
@@ -579,6 +584,53 @@ class Bot:
     def getLearningAlg(self): return self.learningAlg
     def getCurrentAction(self): return self.currentAction
     def getMassOverTime(self): return self.totalMasses
+
+
+class RGBGenerator:
+    """rgbGenerator.py:10-110 -- pixel observations, drawn on the device for every player at once
+    (aigar_observe_pixels); get_cnn_inputRGB(player) returns one player's frame of that launch.
+    Colours come from player_color / pellet_color (seeded) rather than numpy's global RNG
+    (cell.py:31, player.py:39)."""
+
+    def __init__(self, field, parameters=None):
+        self.field = field
+        self.parameters = parameters
+
+        def prm(name, default):
+            return getattr(parameters, name, default) if parameters is not None else default
+        if prm("CNN_USE_L1", True):
+            self.length = int(prm("CNN_INPUT_DIM_1", 42))
+        elif prm("CNN_USE_L2", True):
+            self.length = int(prm("CNN_INPUT_DIM_2", 84))
+        else:
+            self.length = int(prm("CNN_INPUT_DIM_3", 42))
+        self.rgb = bool(prm("CNN_P_RGB", False))
+        self.screenDims = np.array([self.length, self.length])
+
+    def modelToViewScaling(self, pos, fovPos, fovSize):  # rgbGenerator.py:80-83
+        return (np.asarray(pos) - fovPos + (fovSize / 2)) * (self.screenDims / fovSize)
+
+    def viewToModelScaling(self, pos, fovPos, fovSize):  # rgbGenerator.py:86-89
+        return np.asarray(pos) / (self.screenDims / fovSize) + fovPos - (fovSize / 2)
+
+    def modelToViewScaleRadius(self, rad, fovSize):  # rgbGenerator.py:92-93
+        return rad * (self.screenDims[0] / fovSize)
+
+    def get_all_inputs(self):
+        """Every player's frame: uint8 [B, L, L, 3] (CNN_P_RGB) or float64 [B, L, L, 1]."""
+        f = self.field.observe_pixels_all(self.length, rgb=self.rgb)
+        return f if self.rgb else f[..., None]
+
+    def get_cnn_inputRGB(self, player):  # rgbGenerator.py:95-100
+        key = ("pixels", self.length, self.rgb)  # Field drops its cache at every update / reset
+        if key not in self.field._cache:
+            self.field._cache[key] = self.get_all_inputs()
+        return self.field._cache[key][player.index]
+
+    @staticmethod
+    def grayscale(arr):  # rgbGenerator.py:102-106
+        arr = np.average(arr, axis=2, weights=[0.298, 0.587, 0.114])
+        return arr.reshape(list(np.shape(arr)) + [1])
 
 
 class Model:

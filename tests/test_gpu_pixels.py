@@ -99,3 +99,33 @@ def test_pixels_rejects_bad_side():
     g.reset(0)
     with pytest.raises(RuntimeError):
         g.observe_pixels(85, 0)
+
+
+def test_rgb_generator_facade():
+    """aigar_amd.model.RGBGenerator (rgbGenerator.py:10-110) over a Model: frames equal the oracle's."""
+    from aigar_amd import model as M
+    from test_facade import reference_like_parameters
+    params = reference_like_parameters(virus=True, split=True, eject=False, n_bots=6)
+    params.CNN_P_RGB, params.CNN_USE_L1, params.CNN_INPUT_DIM_1 = True, True, 42
+    mdl = M.Model(False, False, params, seed=11, field_size=200, max_viruses=4)
+    for _ in range(6):
+        mdl.createBot("Random")
+    mdl.initialize()
+    field = mdl.getField()
+    orc = Oracle(field._config())
+    orc.reset(11)
+    gen = M.RGBGenerator(field, params)
+    for _ in range(20):
+        mdl.takeBotActions()
+        cmd = field._cmd.copy()
+        field.update()
+        orc.set_commands(cmd)
+        orc.step(1)
+    want = orc.pixels(42, 11)
+    for p in mdl.getPlayers():
+        if p.getIsAlive():
+            assert np.array_equal(gen.get_cnn_inputRGB(p), want[p.index])
+    params.CNN_P_RGB = False
+    gray = M.RGBGenerator(field, params).get_cnn_inputRGB(mdl.getPlayers()[0])
+    assert gray.shape == (42, 42, 1)
+    orc.close()
