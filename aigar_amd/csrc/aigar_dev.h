@@ -76,7 +76,7 @@ enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4
 struct Dev {
   int A, B, NP, size, cols, H;
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
-  double pow_n032[17];  // pow_cr(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
+  double pow_n032[17];  // pow_glibc(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)
   int cshift_c;  // player-cell grid: smallest shift with <= 4096 cells (k_cgrid_count / k_cgrid_scatter)
   int Pcap, Ecap, Vcap, Wcap, EVcap;

@@ -1,14 +1,18 @@
-// aigar_math.h -- correctly rounded pow(x, y) for the stepper (host + device).
+// aigar_math.h -- pow(x, y) exactly as the reference's glibc computes it, and
+// an exact non-negative fmod, for the stepper (host + device).
 //
 // Why: the reference's observation grid has a quirk (spatialHashTable.py:19 vs
 // bot.py:389): cols = ceil(fov / (fov / 11)) is 12 instead of 11 for ~3% of
 // fov sizes, and fov = r^0.475 * n^0.32 * 35 (player.py:163-167).  Whether the
-// quirk fires depends on the LAST BIT of fov, i.e. of libm's pow.  The
-// reference runs glibc pow (correctly rounded except ~0.1% of inputs); OCML's
-// pow differs far more often.  This double-double pow (~96 correct bits before
-// the final rounding) returns the correctly rounded result, so it agrees with
-// glibc wherever glibc is correctly rounded.
-// Domain used by the path: x > 0 finite, |y| < 1 (also fine for moderate y).
+// quirk fires depends on the LAST BIT of fov, i.e. of libm's pow, which
+// CPython's float power calls.  glibc 2.35's pow is not correctly rounded
+// (< 0.52 ulp), so the device restates glibc's algorithm itself: same tables
+// (aigar_glibc_pow_tables.h, dumped from the host's libm by
+// tools/gen/glibc_pow_tables.c), same operation sequence, and the same fused
+// multiply-adds as the x86-64 FMA variant the reference's host dispatches to
+// (glibc's __ieee754_pow_fma, whose contractions were read off its object code;
+// sysdeps/ieee754/dbl-64/e_pow.c).  tests/test_pow_host.py checks the host
+// build against libm's pow on 10^7 inputs; tests/test_gpu_parity.py the device.
 #pragma once
 #include <stdint.h>
 
@@ -19,7 +23,7 @@
 #include <cmath>
 #define AIGAR_HD static inline
 #endif
-#include "aigar_pow_tables.h"
+#include "aigar_glibc_pow_tables.h"
 
 namespace aigar_math {
 
@@ -40,6 +44,7 @@ AIGAR_HD double mod_pos(double a, double b, double inv_b) {
   return r == 0 ? 0.0 : r;
 }
 
+// double-double helpers (aigar_trig.h)
 struct dd {
   double hi, lo;
 };
@@ -90,167 +95,129 @@ AIGAR_HD dd dd_div(dd a, dd b) {
 }
 
 
-// ln 2 = LN2_HI + LN2_LO
-#define AIGAR_LN2_HI 6.93147180559945286227e-01
-#define AIGAR_LN2_LO 2.31904681384629955842e-17
-
-// log(x) in double-double: x = 2^k m, m in [sqrt(1/2), sqrt(2)),
-// log m = 2 atanh(s), s = (m-1)/(m+1), |s| <= 0.1716
-AIGAR_HD dd log_dd(double x) {
-  int k;
-  double m = frexp(x, &k);
-  if (m < 0.70710678118654752440) {
-    m *= 2;
-    k -= 1;
-  }
-  dd num = two_sum(m, -1.0);
-  dd den = two_sum(m, 1.0);
-  dd s = dd_div(num, den);
-  dd s2 = dd_mul(s, s);
-  // 1/(2j+1) as double-double (generated with 80-digit decimal arithmetic)
-  constexpr double kOddInv[25][2] = {{0x1.0000000000000p+0, 0x0.0p+0}, {0x1.5555555555555p-2, 0x1.5555555555555p-56}, {0x1.999999999999ap-3, -0x1.999999999999ap-57}, {0x1.2492492492492p-3, 0x1.2492492492492p-57}, {0x1.c71c71c71c71cp-4, 0x1.c71c71c71c71cp-58}, {0x1.745d1745d1746p-4, -0x1.745d1745d1746p-59}, {0x1.3b13b13b13b14p-4, -0x1.3b13b13b13b14p-58}, {0x1.1111111111111p-4, 0x1.1111111111111p-60}, {0x1.e1e1e1e1e1e1ep-5, 0x1.e1e1e1e1e1e1ep-61}, {0x1.af286bca1af28p-5, 0x1.af286bca1af28p-59}, {0x1.8618618618618p-5, 0x1.8618618618618p-59}, {0x1.642c8590b2164p-5, 0x1.642c8590b2164p-60}, {0x1.47ae147ae147bp-5, -0x1.eb851eb851eb8p-61}, {0x1.2f684bda12f68p-5, 0x1.2f684bda12f68p-59}, {0x1.1a7b9611a7b96p-5, 0x1.1a7b9611a7b96p-61}, {0x1.0842108421084p-5, 0x1.0842108421084p-60}, {0x1.f07c1f07c1f08p-6, -0x1.f07c1f07c1f08p-61}, {0x1.d41d41d41d41dp-6, 0x1.0750750750750p-60}, {0x1.bacf914c1bad0p-6, -0x1.bacf914c1bad0p-60}, {0x1.a41a41a41a41ap-6, 0x1.0690690690690p-60}, {0x1.8f9c18f9c18fap-6, -0x1.f3831f3831f38p-61}, {0x1.7d05f417d05f4p-6, 0x1.7d05f417d05f4p-62}, {0x1.6c16c16c16c17p-6, -0x1.f49f49f49f49fp-61}, {0x1.5c9882b931057p-6, 0x1.310572620ae4cp-61}, {0x1.4e5e0a72f0539p-6, 0x1.e0a72f0539783p-60}};
-  dd acc = dd{kOddInv[24][0], kOddInv[24][1]};
-  for (int j = 23; j >= 0; j--) acc = dd_add(dd_mul(acc, s2), dd{kOddInv[j][0], kOddInv[j][1]});
-  dd lm = dd_mul_d(dd_mul(s, acc), 2.0);
-  dd kl = dd_add(two_prod((double)k, AIGAR_LN2_HI), dd{(double)k * AIGAR_LN2_LO, 0.0});
-  return dd_add(kl, lm);
-}
-
-// exp(p) in double-double: p = k ln2 + r, exp(r) = (Taylor(r / 2^10))^(2^10)
-AIGAR_HD dd exp_dd(dd p) {
-  double kd = rint(p.hi / AIGAR_LN2_HI);
-  dd kl = dd_add(two_prod(kd, AIGAR_LN2_HI), two_prod(kd, AIGAR_LN2_LO));
-  dd r = dd_sub(p, kl);
-  r.hi *= 0x1p-10;
-  r.lo *= 0x1p-10;
-  // 1/n as double-double
-  constexpr double kInvN[15][2] = {{0.0, 0.0}, {0x1.0000000000000p+0, 0x0.0p+0}, {0x1.0000000000000p-1, 0x0.0p+0}, {0x1.5555555555555p-2, 0x1.5555555555555p-56}, {0x1.0000000000000p-2, 0x0.0p+0}, {0x1.999999999999ap-3, -0x1.999999999999ap-57}, {0x1.5555555555555p-3, 0x1.5555555555555p-57}, {0x1.2492492492492p-3, 0x1.2492492492492p-57}, {0x1.0000000000000p-3, 0x0.0p+0}, {0x1.c71c71c71c71cp-4, 0x1.c71c71c71c71cp-58}, {0x1.999999999999ap-4, -0x1.999999999999ap-58}, {0x1.745d1745d1746p-4, -0x1.745d1745d1746p-59}, {0x1.5555555555555p-4, 0x1.5555555555555p-58}, {0x1.3b13b13b13b14p-4, -0x1.3b13b13b13b14p-58}, {0x1.2492492492492p-4, 0x1.2492492492492p-58}};
-  dd acc = dd{1.0, 0.0};
-  for (int n = 14; n >= 1; n--) acc = dd_add(dd{1.0, 0.0}, dd_mul(dd_mul(acc, r), dd{kInvN[n][0], kInvN[n][1]}));
-  for (int i = 0; i < 10; i++) acc = dd_mul(acc, acc);
-  int ki = (int)kd;
-  acc.hi = ldexp(acc.hi, ki);
-  acc.lo = ldexp(acc.lo, ki);
-  return acc;
-}
-
-// ---------------------------------------------------------------- fast path
-// Table-driven x^y with ~2^-70 relative error as a double-double, plus Ziv's
-// rounding test: when the error interval rounds to one double, that double is
-// the correctly rounded result; otherwise (about 1 call in 2^16) the slow
-// series above decides.  log: x = 2^E m, m in [1,2), t = m r_i - 1 exact
-// (r_i has 8 significant bits, |t| < 2^-7), log1p(t) = t - t^2/2 + t^3 P(t).
-// exp: p = (128 kk + j) ln2/128 + r, |r| < 2^-8, 2^(j/128) from a table.
-struct PowLogEnt {
-  double r, lh, ll;
-};
-struct PowExpEnt {
-  double h, l;
-};
-#ifdef __HIPCC__
-static __constant__ PowLogEnt kPowLogDev[128] = AIGAR_POW_LOG_TABLE;
-static __constant__ PowExpEnt kPowExpDev[128] = AIGAR_POW_EXP_TABLE;
-#endif
-static const PowLogEnt kPowLogHost[128] = AIGAR_POW_LOG_TABLE;
-static const PowExpEnt kPowExpHost[128] = AIGAR_POW_EXP_TABLE;
-AIGAR_HD PowLogEnt pow_log_ent(int i) {
-#ifdef __HIP_DEVICE_COMPILE__
-  return kPowLogDev[i];
-#else
-  return kPowLogHost[i];
-#endif
-}
-AIGAR_HD PowExpEnt pow_exp_ent(int j) {
-#ifdef __HIP_DEVICE_COMPILE__
-  return kPowExpDev[j];
-#else
-  return kPowExpHost[j];
-#endif
-}
 AIGAR_HD dd dd_add_d(dd a, double b) {
   dd s = two_sum(a.hi, b);
   s.lo += a.lo;
   return fast_two_sum(s.hi, s.lo);
 }
-// relative error bound of the fast double-double result (measured max 2^-75.7 over
-// 3M samples of the path's domain, tools/gen/check_pow.cpp; 2^5.7 margin)
-#define AIGAR_POW_FAST_ERR 0x1p-70
-AIGAR_HD bool pow_fast(double x, double y, double &res, dd *raw = nullptr) {
-  uint64_t bits;
-  __builtin_memcpy(&bits, &x, 8);
-  int E = (int)((bits >> 52) & 0x7ff);
-  if (E == 0 || E == 0x7ff || (bits >> 63)) return false;  // zero/subnormal/inf/nan/negative
-  E -= 1023;
-  const int i = (int)((bits >> 45) & 127);
-  const uint64_t mb = (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
-  double m;
-  __builtin_memcpy(&m, &mb, 8);
-  const PowLogEnt L = pow_log_ent(i);
-  const double t = fma(m, L.r, -1.0);  // exact
-  const dd t2 = two_prod(t, t);
-  double P = -0x1.999999999999ap-4;  // -1/10
-  P = fma(P, t, 0x1.c71c71c71c71cp-4);   // 1/9
-  P = fma(P, t, -0x1.0000000000000p-3);  // -1/8
-  P = fma(P, t, 0x1.2492492492492p-3);   // 1/7
-  P = fma(P, t, -0x1.5555555555555p-3);  // -1/6
-  P = fma(P, t, 0x1.999999999999ap-3);   // 1/5
-  P = fma(P, t, -0x1.0000000000000p-2);  // -1/4
-  P = fma(P, t, 0x1.5555555555555p-2);   // 1/3
-  const double ln2[3] = AIGAR_POW_LN2;
-  const double Ed = (double)E;
-  // small terms first (all << 2^-20 in magnitude)
-  const double small = Ed * ln2[1] + Ed * ln2[2] + L.ll - 0.5 * t2.lo + t * t2.hi * P;
-  dd lg = two_sum(Ed * ln2[0], L.lh);  // E ln2_hi is exact
-  lg = dd_add_d(lg, t);
-  lg = dd_add_d(lg, -0.5 * t2.hi);
-  lg = dd_add_d(lg, small);
-  // p = y log x
-  dd p = two_prod(y, lg.hi);
-  p.lo += y * lg.lo;
-  p = fast_two_sum(p.hi, p.lo);
-  if (!(p.hi > -700.0 && p.hi < 700.0)) return false;
-  const double l128[3] = AIGAR_POW_LN2_128;
-  const double kd = rint(p.hi * AIGAR_POW_INV_LN2_128);
-  const int k = (int)kd;
-  dd r = two_sum(p.hi, -kd * l128[0]);  // kd * ln2/128_hi is exact
-  double rl = r.lo + p.lo - kd * l128[1] - kd * l128[2];
-  r = two_sum(r.hi, rl);
-  const double rh = r.hi;
-  rl = r.lo;
-  const dd r2 = two_prod(rh, rh);
-  double Q = 0x1.a01a01a01a01ap-16;  // 1/40320
-  Q = fma(Q, rh, 0x1.a01a01a01a01ap-13);  // 1/5040
-  Q = fma(Q, rh, 0x1.6c16c16c16c17p-10);  // 1/720
-  Q = fma(Q, rh, 0x1.1111111111111p-7);   // 1/120
-  Q = fma(Q, rh, 0x1.5555555555555p-5);   // 1/24
-  Q = fma(Q, rh, 0x1.5555555555555p-3);   // 1/6
-  const double tail = rl + 0.5 * r2.lo + rh * rl + rh * r2.hi * Q;
-  dd e = fast_two_sum(1.0, rh);
-  e = dd_add_d(e, 0.5 * r2.hi);
-  e = dd_add_d(e, tail);
-  const PowExpEnt T = pow_exp_ent(k & 127);
-  e = dd_mul(e, dd{T.h, T.l});
-  if (raw) *raw = dd{ldexp(e.hi, k >> 7), ldexp(e.lo, k >> 7)};  // (diagnostics: tools/gen/check_pow.cpp)
-  const double err = fabs(e.hi) * AIGAR_POW_FAST_ERR;
-  const double u1 = e.hi + (e.lo - err), u2 = e.hi + (e.lo + err);
-  if (u1 != u2) return false;
-  res = ldexp(u1, k >> 7);  // (arithmetic shift: k = 128 (k >> 7) + (k & 127))
-  return true;
+
+// ------------------------------------------------------------ glibc pow
+#ifdef __HIPCC__
+static __constant__ uint64_t kGlibcPowLogDev[521] = AIGAR_GLIBC_POW_LOG_DATA;
+static __constant__ uint64_t kGlibcExpDev[270] = AIGAR_GLIBC_EXP_DATA;
+#endif
+static const uint64_t kGlibcPowLogHost[521] = AIGAR_GLIBC_POW_LOG_DATA;
+static const uint64_t kGlibcExpHost[270] = AIGAR_GLIBC_EXP_DATA;
+
+AIGAR_HD double as_double(uint64_t u) {
+  double d;
+  __builtin_memcpy(&d, &u, 8);
+  return d;
+}
+AIGAR_HD uint64_t as_u64(double d) {
+  uint64_t u;
+  __builtin_memcpy(&u, &d, 8);
+  return u;
+}
+// __pow_log_data: [0] ln2hi [1] ln2lo [2..8] poly A[0..6] [9 + 4i] {invc, pad, logc, logctail}
+AIGAR_HD double glog_data(int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return as_double(kGlibcPowLogDev[i]);
+#else
+  return as_double(kGlibcPowLogHost[i]);
+#endif
+}
+// __exp_data: [0] invln2N [1] shift [2] negln2hiN [3] negln2loN [4..7] C2..C5 ... [14 + j] tab
+AIGAR_HD uint64_t gexp_data(int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return kGlibcExpDev[i];
+#else
+  return kGlibcExpHost[i];
+#endif
 }
 
-// correctly rounded x^y (x > 0)
-AIGAR_HD double pow_cr_slow(double x, double y) {
-  dd l = log_dd(x);
-  dd p = dd_add(two_prod(l.hi, y), dd{l.lo * y, 0.0});
-  dd e = exp_dd(p);
-  return e.hi + e.lo;
+// log(x) as hi + tail for the bit pattern ix of a positive normal x
+// (glibc e_pow.c log_inline, __FP_FAST_FMA branch).
+AIGAR_HD double glibc_log_inline(uint64_t ix, double *tail) {
+  const uint64_t OFF = 0x3fe6955500000000ull;
+  const uint64_t tmp = ix - OFF;
+  const int i = (int)((tmp >> 45) & 127);
+  const int k = (int)((int64_t)tmp >> 52);
+  const uint64_t iz = ix - (tmp & (0xfffull << 52));
+  const double z = as_double(iz);
+  const double kd = (double)k;
+  const double invc = glog_data(9 + 4 * i), logc = glog_data(11 + 4 * i), logctail = glog_data(12 + 4 * i);
+  const double ln2hi = glog_data(0), ln2lo = glog_data(1);
+  const double A0 = glog_data(2), A1 = glog_data(3), A2 = glog_data(4), A3 = glog_data(5), A4 = glog_data(6),
+               A5 = glog_data(7), A6 = glog_data(8);
+  const double r = fma(z, invc, -1.0);  // exact: 1/c is j/128 or j/256
+  const double t1 = fma(kd, ln2hi, logc);
+  const double t2 = t1 + r;
+  const double lo1 = fma(kd, ln2lo, logctail);
+  const double lo2 = t1 - t2 + r;
+  const double ar = A0 * r;
+  const double ar2 = r * ar;
+  const double ar3 = r * ar2;
+  const double hi = t2 + ar2;
+  const double lo3 = fma(ar, r, -ar2);
+  const double lo4 = t2 - hi + ar2;
+  // p = ar3 * (A1 + r A2 + ar2 (A3 + r A4 + ar2 (A5 + r A6))), folded into lo by one fma
+  const double q = fma(ar2, fma(ar2, fma(r, A6, A5), fma(r, A4, A3)), fma(r, A2, A1));
+  const double lo = fma(ar3, q, lo1 + lo2 + lo3 + lo4);
+  const double y = hi + lo;
+  *tail = hi - y + lo;
+  return y;
 }
-AIGAR_HD double pow_cr(double x, double y) {
-  if (y == 0.0 || x == 1.0) return 1.0;
+
+// exp(x + xtail) for the pow result, sign_bias 0 (glibc e_pow.c exp_inline).
+AIGAR_HD double glibc_exp_inline(double x, double xtail) {
+  uint32_t abstop = (uint32_t)(as_u64(x) >> 52) & 0x7ff;
+  if (abstop - 0x3c9u >= 0x3fu) {
+    if ((int32_t)(abstop - 0x3c9u) < 0) return 1.0 + x;  // |x| < 2^-54
+    if (abstop >= 0x409u) return (as_u64(x) >> 63) ? 0.0 : __builtin_inf();  // __math_uflow / oflow
+    abstop = 0;  // large |x| below the overflow bound: specialcase below
+  }
+  const double InvLn2N = as_double(gexp_data(0)), Shift = as_double(gexp_data(1));
+  const double NegLn2hiN = as_double(gexp_data(2)), NegLn2loN = as_double(gexp_data(3));
+  const double C2 = as_double(gexp_data(4)), C3 = as_double(gexp_data(5)), C4 = as_double(gexp_data(6)),
+               C5 = as_double(gexp_data(7));
+  double kd = fma(x, InvLn2N, Shift);  // z + Shift, contracted
+  const uint64_t ki = as_u64(kd);
+  kd -= Shift;
+  double r = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x));
+  r = xtail + r;
+  const uint64_t idx = 2 * (ki % 128);
+  const uint64_t top = ki << 45;
+  const double tail = as_double(gexp_data(14 + (int)idx));
+  uint64_t sbits = gexp_data(15 + (int)idx) + top;
+  const double r2 = r * r;
+  const double tmp = fma(fma(r, C5, C4), r2 * r2, fma(fma(r, C3, C2), r2, r + tail));
+  if (abstop == 0) {  // glibc specialcase (results near overflow / underflow; not on the stepper's path)
+    if ((ki & 0x80000000ull) == 0) {
+      sbits -= 1009ull << 52;
+      const double scale = as_double(sbits);
+      return 0x1p1009 * fma(tmp, scale, scale);
+    }
+    sbits += 1022ull << 52;
+    const double scale = as_double(sbits);
+    return 0x1p-1022 * (scale + scale * tmp);  // (subnormal double rounding not restated)
+  }
+  const double scale = as_double(sbits);
+  return fma(tmp, scale, scale);
+}
+
+// pow(x, y) bit-identical to glibc 2.35 for x >= 0 finite and 2^-65 <= |y| < 2^63
+// (fovSize, move speed; other inputs are outside the stepper's domain).
+AIGAR_HD double pow_glibc(double x, double y) {
+  if (x == 1.0 || y == 0.0) return 1.0;
   if (x == 0.0) return y > 0 ? 0.0 : __builtin_inf();
-  double r;
-  if (pow_fast(x, y, r)) return r;
-  return pow_cr_slow(x, y);
+  uint64_t ix = as_u64(x);
+  if ((ix >> 52) == 0) ix = as_u64(x * 0x1p52) - (52ull << 52);  // subnormal x
+  double lo;
+  const double hi = glibc_log_inline(ix, &lo);
+  const double ehi = y * hi;
+  const double elo = fma(y, lo, fma(y, hi, -ehi));
+  return glibc_exp_inline(ehi, elo);
 }
 
 }  // namespace aigar_math

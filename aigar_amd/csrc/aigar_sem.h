@@ -93,7 +93,7 @@ AIGAR_D void set_move_direction(double x, double y, double m, double r, double c
   double hyp = xd * xd + yd * yd, r2 = r * r;
   double mod = py_min(hyp, r2) / r2;
   double ang = aigar_math::trig_atan2(yd, xd);  // correctly rounded (aigar_trig.h)
-  double sp = kMoveSpeed * aigar_math::pow_cr(m, -0.35);  // correctly rounded (see aigar_math.h)
+  double sp = kMoveSpeed * aigar_math::pow_glibc(m, -0.35);  // glibc pow, bit for bit (aigar_math.h)
   double c, s;
   aigar_math::trig_sincos(ang, s, c);
   vx = sp * mod * c;

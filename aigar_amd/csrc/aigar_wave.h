@@ -112,7 +112,7 @@ __device__ inline Fov player_fov(const Dev &d, int gp) {
     if (k == 0 || r > rb) rb = r;
   }
   f.mass = n ? np_sum(ms, n) : 0.0;
-  f.fs = aigar_math::pow_cr(rb, 0.475) * d.pow_n032[n] * 35;  // (table: same correctly rounded values)
+  f.fs = aigar_math::pow_glibc(rb, 0.475) * d.pow_n032[n] * 35;  // (table: same glibc pow values)
   f.fx = np_sum(xs, n) / f.mass;
   f.fy = np_sum(ys, n) / f.mass;
   f.rmax = rb;

