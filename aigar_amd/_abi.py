@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 RNG_PHILOX = 0
 RNG_MT19937 = 1
@@ -20,6 +20,7 @@ EV_MERGE, EV_VIRUS_EAT_BLOB, EV_VIRUS_SPLIT, EV_CELL_EAT_VIRUS, EV_EXPLODE = 1, 
 EV_CELL_EAT_PELLET, EV_CELL_EAT_BLOB, EV_CELL_EAT_CELL, EV_PLAYER_DEATH, EV_RESPAWN = 6, 7, 8, 9, 10
 
 FLAG_EVENTS = 0x1
+TILE_OWNED_ONLY = 0x1
 
 
 POLICY_NONE, POLICY_RANDOM, POLICY_GREEDY = 0, 1, 2
@@ -50,6 +51,8 @@ class Config(C.Structure):
         ("grid_squares", C.c_int32), ("obs_channels", C.c_uint32), ("obs_extras", C.c_uint32),
         ("rng_mode", C.c_int32), ("device", C.c_int32), ("pellet_cap", C.c_int32),
         ("blob_cap", C.c_int32), ("virus_cap", C.c_int32), ("event_cap", C.c_int32), ("flags", C.c_int32),
+        ("tile_x", C.c_int32), ("tile_y", C.c_int32), ("tile_id", C.c_int32), ("tile_halo", C.c_int32),
+        ("tile_cap", C.c_int32), ("tile_flags", C.c_int32),
     ]
 
 

@@ -79,6 +79,14 @@ def load(build_if_missing=False):
         "aigar_set_split_likelihood": [vp, i32, C.POINTER(C.c_int32)],
         "aigar_run": [vp, i32, C.POINTER(_abi.RunParams), vp, i32],
         "aigar_env_step": [vp, vp, i32, i32, i32, C.POINTER(_abi.RewardParams), vp, vp, i32],
+        "aigar_get_events_raw": [vp, i32, C.POINTER(C.c_int64), i32, C.POINTER(i32)],
+        "aigar_tile_info": [vp, C.POINTER(C.c_int32), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_int64)],
+        "aigar_tile_set_buffers": [vp, vp, vp],
+        "aigar_tile_begin": [vp, C.POINTER(_abi.RunParams)],
+        "aigar_tile_apply": [vp, C.POINTER(i32)],
+        "aigar_tile_resume": [vp],
+        "aigar_tile_end": [vp, vp, i32],
+        "aigar_tile_exchange_local": [C.POINTER(vp), i32],
     }
     for name, args in sig.items():
         f = getattr(L, name, None)
@@ -264,6 +272,50 @@ class Stepper:
                                               C.byref(n)))
         return out
 
+    def events_raw(self, arena=0):
+        """Unsorted event rows with their sort keys: (key_hi, key_lo, code, a, b)."""
+        n = C.c_int(0)
+        self._chk(self.L.aigar_get_events_raw(self.h, arena, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 5), np.int64)
+        if n.value:
+            self._chk(self.L.aigar_get_events_raw(self.h, arena, out.ctypes.data_as(C.POINTER(C.c_int64)), n.value,
+                                                  C.byref(n)))
+        return out
+
+    # ---- C4 tiles (include/aigar.h: aigar_tile_*)
+    def tile_info(self):
+        info = (C.c_int32 * 12)()
+        ob, ib, nb = C.c_void_p(), C.c_void_p(), C.c_int64(0)
+        self._chk(self.L.aigar_tile_info(self.h, info, C.byref(ob), C.byref(ib), C.byref(nb)))
+        v = list(info)
+        return {"ntiles": v[0], "tile_id": v[1], "own": tuple(v[2:6]), "held": tuple(v[6:10]), "tcap": v[10],
+                "bm_words": v[11], "outbox": ob.value, "inbox": ib.value, "msg_bytes": nb.value}
+
+    def tile_set_buffers(self, outbox_ptr, inbox_ptr):
+        self._chk(self.L.aigar_tile_set_buffers(self.h, C.c_void_p(int(outbox_ptr)), C.c_void_p(int(inbox_ptr))))
+
+    def tile_begin(self, policy="none", p_split=0.0, p_eject=0.0, seed=0):
+        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM}[policy]
+        prm = _abi.RunParams(pol, 0, float(p_split), float(p_eject), int(seed))
+        self._chk(self.L.aigar_tile_begin(self.h, C.byref(prm)))
+
+    def tile_apply(self):
+        u = C.c_int(0)
+        self._chk(self.L.aigar_tile_apply(self.h, C.byref(u)))
+        return u.value
+
+    def tile_resume(self):
+        self._chk(self.L.aigar_tile_resume(self.h))
+
+    def tile_end(self, out=None):
+        p, dt = None, 0
+        if out is not None:
+            if not getattr(out, "is_cuda", False) or tuple(out.shape) != (self.NP, self.obs_len):
+                raise ValueError("tile_end writes observations to a device tensor [%d, %d]" % (self.NP, self.obs_len))
+            dt = 0 if str(out.dtype) == "torch.float64" else 1
+            p = C.c_void_p(out.data_ptr())
+        self._chk(self.L.aigar_tile_end(self.h, p, dt))
+
     COUNTERS = ("vb_serial", "pv_serial", "food_serial", "-", "pp_serial_players", "-", "-", "ticks")
 
     def counters(self, arena=0):
@@ -286,8 +338,16 @@ class Stepper:
         return ms.value, n.value
 
 
+def tile_exchange_local(steppers):
+    """In-process transport of a tiled arena: every tile's outbox into every tile's inbox."""
+    L = load()
+    arr = (C.c_void_p * len(steppers))(*[s.h.value for s in steppers])
+    if L.aigar_tile_exchange_local(arr, len(steppers)) < 0:
+        raise RuntimeError("aigar: " + L.aigar_last_error().decode())
+
+
 def selftest_pow(x, y):
-    """Device pow_cr(x, y) for host arrays (diagnostics)."""
+    """Device pow (glibc's, restated in aigar_math.h) for host arrays (diagnostics)."""
     L = load()
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)

@@ -55,7 +55,10 @@ struct ArenaCtl {
   int food_undone[3];  // cells that failed reservation round r (index r % 3)
   uint32_t pl_epoch;  // k_players look-back epoch / finished-tile ticket
   int pl_ticket;  // pellet rebuild: source counts snapshotted by the scan epilogue
-  int pad1;
+  // C4 tiling (Dev::tiled): global pellet count at the tick's start, pellets every
+  // tile ate this tick, this pass's outbox fill / pellet kills / undone owned
+  // cells, and the undone owned cells of all tiles after the last exchange
+  int n_pel_glob, n_eaten_glob, n_out, n_out_pel, n_undone, n_undone_glob;
   // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
   // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
   int64_t stat[8];
@@ -63,9 +66,9 @@ struct ArenaCtl {
 
 enum : uint32_t {
   ERR_PELLET_CAP = 1, ERR_BLOB_CAP = 2, ERR_VIRUS_CAP = 4, ERR_EVENT_CAP = 8, ERR_WORK_CAP = 16,
-  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256
+  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256, ERR_TILE_CAP = 512, ERR_TILE_LOOKUP = 1024
 };
-enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2 };
+enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
 // pellet rebuild modes (also the scan's epilogue selector)
 enum : int { PR_NONE = 0, PR_RESET = 1, PR_CLOSE = 2 };
@@ -73,8 +76,28 @@ enum : int { PR_NONE = 0, PR_RESET = 1, PR_CLOSE = 2 };
 // event phases (sort key high word), in reference order within a tick
 enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4, PH_PP = 5, PH_SPAWN = 6 };
 
+// C4: one arena tiled 2-D over tile_x * tile_y handles (one per GPU).  Every
+// handle holds a replica of the players, cells, blobs and viruses (a few
+// thousand records: the player-ordered phases then need no exchange) and only
+// the pellets whose centre bucket lies in its tile plus a halo.  The eat phase
+// is resolved per tile; the outcomes of the cells a tile owns (centre bucket in
+// the tile) travel in one all-gathered message per pass:
+//   outbox = [TR_HDR][tcap records][final-cell bitmap, 16 * NP bits]
+struct TileRec {
+  int32_t kind, idx;  // TR_*; idx: blob slot / cell pool index / (header) record count
+  int64_t seq;        // pellet creation sequence / (header) undone owned cells
+  double x, y;        // pellet position / cell mass, radius / (header) pellet kills, -
+};
+enum : int32_t { TR_HDR = 0, TR_PELLET = 1, TR_BLOB = 2, TR_CELL = 3 };
+
 struct Dev {
   int A, B, NP, size, cols, H;
+  int tiled, tile_id, ntiles, tcap, bm_words;  // tcap: records per outbox; bm_words: u64 words of the bitmap
+  int tile_flags;                              // AIGAR_TILE_*
+  int own_bx0, own_bx1, own_by0, own_by1;      // owned centre buckets [x0, x1) x [y0, y1)
+  int loc_bx0, loc_bx1, loc_by0, loc_by1;      // held pellets: owned range + halo
+  TileRec *outbox;       // [1 + tcap] records + bitmap
+  const TileRec *inbox;  // [ntiles] outboxes (the transport fills it)
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
   double pow_n032[17];  // pow_glibc(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)

@@ -26,6 +26,30 @@ __device__ __forceinline__ void wave_atomic_max_pos(double *addr, double v) {
   }
 }
 
+// C4 tiles (aigar_dev.h): ownership by centre bucket; a tile holds the pellets of
+// its owned range grown by the halo.  Untiled handles own and hold everything.
+__device__ __forceinline__ bool tile_owns(const Dev &d, double x, double y) {
+  if (!d.tiled) return true;
+  const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
+  return bx >= d.own_bx0 && bx < d.own_bx1 && by >= d.own_by0 && by < d.own_by1;
+}
+__device__ __forceinline__ bool tile_holds_bucket(const Dev &d, int bx, int by) {
+  return !d.tiled || (bx >= d.loc_bx0 && bx < d.loc_bx1 && by >= d.loc_by0 && by < d.loc_by1);
+}
+// bucket rectangle r (inclusive) grown by e buckets, clamped to the field
+__device__ __forceinline__ Rect rect_grow(Rect r, int e, int cols) {
+  return Rect{max(0, r.x0 - e), min(cols - 1, r.x1 + e), max(0, r.y0 - e), min(cols - 1, r.y1 + e)};
+}
+// every bucket of r lies in the held range
+__device__ __forceinline__ bool tile_holds_rect(const Dev &d, Rect r) {
+  return !d.tiled || r.x1 < r.x0 || r.y1 < r.y0 ||
+         (r.x0 >= d.loc_bx0 && r.x1 < d.loc_bx1 && r.y0 >= d.loc_by0 && r.y1 < d.loc_by1);
+}
+// r touches the held range grown by e buckets
+__device__ __forceinline__ bool tile_near_rect(const Dev &d, Rect r, int e) {
+  return !d.tiled || (r.x0 <= r.x1 && r.y0 <= r.y1 && r.x1 >= d.loc_bx0 - e && r.x0 < d.loc_bx1 + e &&
+                      r.y1 >= d.loc_by0 - e && r.y0 < d.loc_by1 + e);
+}
 
 // Wave-parallel walk over the grid rows around q (expanded by E): the rows'
 // item ranges are loaded by one lane each and flattened with a prefix sum, so

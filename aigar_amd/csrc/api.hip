@@ -17,6 +17,10 @@
 namespace aigar {
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v,
                  const RandomPolicy *rp = nullptr);
+void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp);
+void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v);
+void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first);
+void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch);
 int launch_observe_pixels(const Dev &d, hipStream_t s, void *out, int dtype, int side, uint64_t seed, uint8_t *ovf);
@@ -66,6 +70,7 @@ struct aigar_handle {
   uint8_t *d_pix_ovf = nullptr;  // per player: frame left to the pixel kernel's second pass
   size_t pix_bytes = 0;
   std::vector<void *> allocs;
+  int box_recs = 0;  // C4: TileRec slots of one exchange message (header + records + bitmap)
   bool profile = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // timer name -> recorded (start, stop) event pairs, resolved lazily
@@ -207,6 +212,40 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.occ_words = (d.H + 63) / 64;
   d.scan_tiles = (d.H + 2047) / 2048;
   d.pl_tiles = (d.B + 255) / 256;
+  // C4 tiles: bucket-aligned tiles, ownership by centre bucket
+  const int tx = std::max(1, cfg->tile_x), ty = std::max(1, cfg->tile_y);
+  d.ntiles = tx * ty;
+  d.tiled = d.ntiles > 1;
+  d.own_bx0 = d.own_by0 = d.loc_bx0 = d.loc_by0 = 0;
+  d.own_bx1 = d.own_by1 = d.loc_bx1 = d.loc_by1 = d.cols;
+  if (d.tiled) {
+    auto bad = [&](const char *m) {
+      delete h;
+      return fail("aigar_create: %s", m);
+    };
+    if (d.A != 1) return bad("a tiled handle steps one arena (n_arenas must be 1)");
+    if (cfg->tile_id < 0 || cfg->tile_id >= d.ntiles) return bad("tile_id out of range");
+    if (tx > d.cols || ty > d.cols) return bad("more tiles than hash buckets along a side");
+    const int ix = cfg->tile_id % tx, iy = cfg->tile_id / tx;
+    const int halo = cfg->tile_halo > 0 ? cfg->tile_halo : 400;
+    // an owned cell's boxes (pellet turn, blob turn, one bucket of food footprint)
+    // reach <= 6 buckets from its centre bucket at the mass cap: with 7 its owner
+    // holds every food it can touch, so every cell is decidable somewhere
+    const int hb = std::max(7, (halo + kBucket - 1) / kBucket);
+    d.tile_id = cfg->tile_id;
+    d.tile_flags = cfg->tile_flags;
+    d.own_bx0 = ix * d.cols / tx;
+    d.own_bx1 = (ix + 1) * d.cols / tx;
+    d.own_by0 = iy * d.cols / ty;
+    d.own_by1 = (iy + 1) * d.cols / ty;
+    d.loc_bx0 = std::max(0, d.own_bx0 - hb);
+    d.loc_bx1 = std::min(d.cols, d.own_bx1 + hb);
+    d.loc_by0 = std::max(0, d.own_by0 - hb);
+    d.loc_by1 = std::min(d.cols, d.own_by1 + hb);
+  }
+  d.tcap = cfg->tile_cap > 0 ? cfg->tile_cap : 4096;
+  d.bm_words = (int)(((size_t)kMaxCells * d.NP + 255) / 256 * 4);  // 16 * NP bits, whole TileRecs
+  h->box_recs = 1 + d.tcap + d.bm_words / 4;
   for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_glibc((double)k, 0.32);
   d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (k_grid_small)
   while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
@@ -267,6 +306,13 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(ob_epoch, uint32_t, 1);
   AL(p_split_lh, int, NP);
   AL(o_last_mass, double, NP);
+  if (d.tiled) {
+    AL(outbox, TileRec, h->box_recs);
+    TileRec *ib = nullptr;
+    ib = dalloc<TileRec>(h, (size_t)h->box_recs * d.ntiles);
+    ok = ok && ib != nullptr;
+    d.inbox = ib;
+  }
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
 #undef AL
@@ -454,6 +500,104 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
     else launch_env_step(h, h->stream, *p, obs_out, dtype);
   }
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- C4 tiles
+static int need_tiled(aigar_handle *h) {
+  if (!h) return fail("null handle");
+  if (!h->d.tiled) return fail("not a tiled handle (tile_x * tile_y must be > 1)");
+  return 0;
+}
+extern "C" int aigar_tile_info(aigar_handle *h, int32_t *info, void **outbox, void **inbox, int64_t *msg_bytes) {
+  if (need_tiled(h)) return -1;
+  const Dev &d = h->d;
+  if (info) {
+    const int32_t v[12] = {d.ntiles, d.tile_id, d.own_bx0, d.own_bx1, d.own_by0, d.own_by1,
+                           d.loc_bx0, d.loc_bx1, d.loc_by0, d.loc_by1, d.tcap, d.bm_words};
+    memcpy(info, v, sizeof v);
+  }
+  if (outbox) *outbox = d.outbox;
+  if (inbox) *inbox = (void *)d.inbox;
+  if (msg_bytes) *msg_bytes = (int64_t)h->box_recs * (int64_t)sizeof(TileRec);
+  return 0;
+}
+extern "C" int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox) {
+  if (need_tiled(h)) return -1;
+  if (!outbox || !inbox) return fail("tile_set_buffers: null buffer");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->d.outbox = (TileRec *)outbox;
+  h->d.inbox = (const TileRec *)inbox;
+  return 0;
+}
+extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
+  if (need_tiled(h) || !p) return p ? -1 : fail("null argument");
+  if (p->policy != AIGAR_POLICY_NONE && p->policy != AIGAR_POLICY_RANDOM)
+    return fail("tile_begin: policy must be NONE or RANDOM (the greedy policy reads pellets other tiles hold)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log holds this tick
+    hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, h->stream, h->d);
+  const RandomPolicy rp{p->policy == AIGAR_POLICY_RANDOM, p->p_split, p->p_eject, p->seed};
+  Mark m(h, "tile_begin");
+  launch_tick_pre(h->d, h->stream, h->scr_k, h->scr_v, &rp);
+  launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 1);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+extern "C" int aigar_tile_apply(aigar_handle *h, int *undone) {
+  if (need_tiled(h) || !undone) return undone ? -1 : fail("null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  {
+    Mark m(h, "tile_apply");
+    launch_tile_apply(h->d, h->stream, h->box_recs);
+  }
+  HIPCHK(hipGetLastError());
+  ArenaCtl c;
+  HIPCHK(hipMemcpyAsync(&c, h->d.ctl, sizeof c, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (c.err) return check_device_errors(h);
+  *undone = c.n_undone_glob;
+  return 0;
+}
+extern "C" int aigar_tile_resume(aigar_handle *h) {
+  if (need_tiled(h)) return -1;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  Mark m(h, "tile_resume");
+  launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 0);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+extern "C" int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype) {
+  if (need_tiled(h)) return -1;
+  if (obs_out && dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  {
+    Mark m(h, "tile_end");
+    launch_tick_post(h->d, h->stream, h->scr_k, h->scr_v);
+  }
+  if (obs_out) {
+    Mark m(h, "observe");
+    launch_observe(h->d, h->stream, obs_out, dtype, 0);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+// in-process transport: every handle's outbox into every handle's inbox slot
+extern "C" int aigar_tile_exchange_local(aigar_handle **hs, int n) {
+  if (!hs || n < 1) return fail("null argument");
+  for (int i = 0; i < n; i++) {
+    if (need_tiled(hs[i])) return -1;
+    if (hs[i]->d.ntiles != n || hs[i]->box_recs != hs[0]->box_recs) return fail("tile_exchange_local: mismatched tiles");
+    HIPCHK(hipSetDevice(hs[i]->cfg.device));
+    HIPCHK(hipStreamSynchronize(hs[i]->stream));
+  }
+  const size_t bytes = (size_t)hs[0]->box_recs * sizeof(TileRec);
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < n; k++) {
+      const aigar_handle *src = hs[k];
+      HIPCHK(hipMemcpyAsync((char *)hs[i]->d.inbox + (size_t)src->d.tile_id * bytes, src->d.outbox, bytes,
+                            hipMemcpyDeviceToDevice, hs[i]->stream));
+    }
   return 0;
 }
 
@@ -713,6 +857,13 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
     if (vfl[i] & F_ALIVE) vl.push_back(i);
   std::sort(bl.begin(), bl.end(), [&](int x, int y) { return bseq[x] < bseq[y]; });
   std::sort(vl.begin(), vl.end(), [&](int x, int y) { return vseq[x] < vseq[y]; });
+  std::vector<int> pord;
+  for (int i = 0; i < c.n_pel; i++) {
+    const int bx = std::min(d.cols - 1, std::max(0, (int)(px[i] / kBucket)));
+    const int by = std::min(d.cols - 1, std::max(0, (int)(py[i] / kBucket)));
+    if (bx >= d.own_bx0 && bx < d.own_bx1 && by >= d.own_by0 && by < d.own_by1) pord.push_back(i);  // (tiles: owned)
+  }
+  std::sort(pord.begin(), pord.end(), [&](int x, int y) { return ps[x] < ps[y]; });
   int caps[5] = {st->n_cells, st->n_pellets, st->n_blobs, st->n_viruses, st->n_dead};
   st->n_players = B;
   st->field_size = d.size;
@@ -729,12 +880,12 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
   memset(st->mt_key, 0, sizeof st->mt_key);
   st->mt_pos = 0;
   st->n_cells = nc;
-  st->n_pellets = c.n_pel;
+  st->n_pellets = (int)pord.size();
   st->n_blobs = (int)bl.size();
   st->n_viruses = (int)vl.size();
   st->n_dead = c.n_dead;
   if (!st->cells_f) return 0;
-  if (caps[0] < nc || caps[1] < c.n_pel || caps[2] < (int)bl.size() || caps[3] < (int)vl.size() || caps[4] < c.n_dead)
+  if (caps[0] < nc || caps[1] < (int)pord.size() || caps[2] < (int)bl.size() || caps[3] < (int)vl.size() || caps[4] < c.n_dead)
     return fail("get_state: caller arrays too small");
   for (int p = 0; p < B; p++) {
     st->players_f[2 * p] = cmdx[p];
@@ -750,10 +901,7 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
       int64_t *q = st->cells_i + 4 * k;
       q[0] = p; q[1] = csvc[hi]; q[2] = cseq[hi]; q[3] = (cfl[hi] & F_INHASH) ? 1 : 0;
     }
-  std::vector<int> pord(c.n_pel);
-  for (int i = 0; i < c.n_pel; i++) pord[i] = i;
-  std::sort(pord.begin(), pord.end(), [&](int x, int y) { return ps[x] < ps[y]; });
-  for (int i = 0; i < c.n_pel; i++) {
+  for (size_t i = 0; i < pord.size(); i++) {
     int j = pord[i];
     double *f = st->pellets_f + 4 * i;
     f[0] = px[j]; f[1] = py[j]; f[2] = pm[j]; f[3] = pm[j] > 0 ? std::sqrt(pm[j] / 3.141592653589793) : 0.0;
@@ -871,13 +1019,18 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
     HIPCHK(hipMemcpyAsync(d.citems + (size_t)arena * CB, items.data(), 4 * items.size(), hipMemcpyHostToDevice,
                           h->stream));
   // pellets -> P0 sorted by bucket
-  std::vector<double> px(st->n_pellets), py(st->n_pellets), pm(st->n_pellets);
-  std::vector<int64_t> ps(st->n_pellets);
+  // (tiles: only the pellets in the held range)
+  std::vector<double> px, py, pm;
+  std::vector<int64_t> ps;
   for (int i = 0; i < st->n_pellets; i++) {
-    px[i] = st->pellets_f[4 * i];
-    py[i] = st->pellets_f[4 * i + 1];
-    pm[i] = st->pellets_f[4 * i + 2];
-    ps[i] = st->pellets_seq[i];
+    const double x = st->pellets_f[4 * i], y = st->pellets_f[4 * i + 1];
+    const int bx = std::min(d.cols - 1, std::max(0, (int)(x / kBucket)));
+    const int by = std::min(d.cols - 1, std::max(0, (int)(y / kBucket)));
+    if (bx < d.loc_bx0 || bx >= d.loc_bx1 || by < d.loc_by0 || by >= d.loc_by1) continue;
+    px.push_back(x);
+    py.push_back(y);
+    pm.push_back(st->pellets_f[4 * i + 2]);
+    ps.push_back(st->pellets_seq[i]);
   }
   host_grid(d.cols, px, py, start, order);
   {
@@ -935,7 +1088,8 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   c.key1 = st->philox_key[1];
   c.ctr_pellet = st->ctr_pellet;
   c.ctr_virus = st->ctr_virus;
-  c.n_pel = st->n_pellets;
+  c.n_pel = (int)px.size();
+  c.n_pel_glob = st->n_pellets;
   c.n_blob = st->n_blobs;
   c.n_vir = st->n_viruses;
   c.n_dead = st->n_dead;
@@ -1063,6 +1217,23 @@ extern "C" int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int ca
     out[4 * i + 2] = e[3];
     out[4 * i + 3] = e[4];
   }
+  return 0;
+}
+
+// the raw event rows (sort keys kept) -- tiles merge their logs by key
+extern "C" int aigar_get_events_raw(aigar_handle *h, int arena, int64_t *out, int cap, int *n) {
+  if (!h || !n) return fail("null argument");
+  Dev &d = h->d;
+  if (arena < 0 || arena >= d.A) return fail("arena %d out of range", arena);
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (check_device_errors(h)) return -1;
+  ArenaCtl c;
+  HIPCHK(hipMemcpy(&c, d.ctl + arena, sizeof c, hipMemcpyDeviceToHost));
+  const int ne = std::min(c.n_ev, d.EVcap);
+  *n = ne;
+  if (!out) return 0;
+  if (cap < ne) return fail("get_events_raw: cap %d < %d events", cap, ne);
+  if (ne) HIPCHK(hipMemcpy(out, d.ev + (size_t)arena * d.EVcap * 5, (size_t)ne * 5 * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -276,6 +276,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const int cols = (int)ceil(fs / gs);
   const double lim = fs - 1;
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
+  // C4 tiles: a bot whose view reaches beyond the held pellets gets its pellet
+  // channel from the tiles that hold them all (NaN here); everything else --
+  // cells, viruses, walls and the last-frame history, all replicated -- every
+  // tile computes, so the history stays the same on every tile
+  const bool held = tile_holds_rect(d, rect_grow(Q, 1, d.cols));
+  if (!held && lane == 0 && alive && tile_owns(d, fx, fy)) atomicOr(&d.ctl[a].warn, WARN_TILE_OBS);  // halo < view / 2
   // owner of cell pool index g = slot * NP + player, without a 64-bit modulo
   const double inv_np = 1.0 / NP;
   auto pool_owner = [&](size_t g) {
@@ -323,7 +329,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       }
       list_append(c, CLx, capC, nc);
     };
-    wave_fov_walk(d, a, Q, fx, fy, fs, rmax_c, rmax_v, d.obs_ch & AIGAR_OBS_PELLET, d.virus_enabled, own_cells,
+    wave_fov_walk(d, a, Q, fx, fy, fs, rmax_c, rmax_v, held && (d.obs_ch & AIGAR_OBS_PELLET), d.virus_enabled, own_cells,
                   [&](bool valid, int kd, size_t g) {
       const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
       const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
@@ -551,7 +557,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     double freeA = (rb - lb) * (bb - tb);
     // a square wholly inside the field: freeA / (gs*gs) is exactly 1 -> round(0, 3) = +0
     double vw = (freeA == gs * gs) ? 0.0 : py_round3(1 - (freeA / (gs * gs)));
-    if (o_pel >= 0) row[o_pel + t] = (OutT)vp;
+    if (o_pel >= 0) row[o_pel + t] = held ? (OutT)vp : (OutT)__builtin_nan("");
     if (o_self >= 0) row[o_self + t] = (OutT)vs;
     if (o_wall >= 0) row[o_wall + t] = (OutT)vw;
     if (o_enemy >= 0) row[o_enemy + t] = (OutT)ve;

@@ -34,8 +34,25 @@ namespace aigar {
 
 __device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { atomicOr(&d.ctl[a].err, bit); }
 
+__device__ __forceinline__ void tile_out(const Dev &d, int32_t kind, int32_t idx, int64_t seq, double x, double y) {
+  const int i = atomicAdd(&d.ctl[0].n_out, 1);
+  if (i >= d.tcap) {
+    atomicOr(&d.ctl[0].err, (uint32_t)ERR_TILE_CAP);
+    return;
+  }
+  if (kind == TR_PELLET) atomicAdd(&d.ctl[0].n_out_pel, 1);
+  TileRec &r = d.outbox[1 + i];
+  r.kind = kind;
+  r.idx = idx;
+  r.seq = seq;
+  r.x = x;
+  r.y = y;
+}
+
 __device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int code, int64_t x, int64_t y) {
   if (!(d.flags & 1)) return;
+  // tiles: the replicated phases are logged by tile 0, the eat phases by the cell's owner
+  if (d.tiled && d.tile_id != 0 && phase != PH_PELLET && phase != PH_BLOB) return;
   int i = atomicAdd(&d.ctl[a].n_ev, 1);
   if (i >= d.EVcap) {
     set_err(d, a, ERR_EVENT_CAP);
@@ -888,10 +905,15 @@ __device__ __forceinline__ void pgrid_count_bucket(const Dev &d, int a, int i, i
   d.pcnt[H1 + i] = k;
 }
 // staged record j (index into the staging list): atomic rank in its bucket
+// (tiles: a record outside the held range is dropped, rank -1)
 __device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
   const size_t g = (size_t)a * d.Pcap + j, H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
-  const int b = center_bucket_coord(d.pn_y[g], d.cols) * d.cols + center_bucket_coord(d.pn_x[g], d.cols);
-  d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + b], 1);
+  const int bx = center_bucket_coord(d.pn_x[g], d.cols), by = center_bucket_coord(d.pn_y[g], d.cols);
+  if (!tile_holds_bucket(d, bx, by)) {
+    d.pel_rank[R0 + d.Pcap + j] = -1;
+    return;
+  }
+  d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + by * d.cols + bx], 1);
 }
 // mode PR_RESET: staging -> buffer 0 (the closing rebuild of a tick takes its
 // counts in k_spawn_all)
@@ -944,12 +966,14 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
         return;
       }
     }
+    const int rk = d.pel_rank[R0 + d.Pcap + j];
+    if (rk < 0) return;  // (tiles: not held here)
     x = d.pn_x[g];
     y = d.pn_y[g];
     m = d.pn_m[g];
     s = d.pn_seq[g];
     int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-    pos = d.pstart[H1 + b + 1] - 1 - d.pel_rank[R0 + d.Pcap + j];
+    pos = d.pstart[H1 + b + 1] - 1 - rk;
   }
   if (pos >= d.Pcap) {
     set_err(d, a, ERR_PELLET_CAP);
@@ -1423,7 +1447,14 @@ __device__ __forceinline__ double wave_sum(double v) {
 // with a key that dominates all rounds and are resolved by the serial pass.
 constexpr int PREP_CAND = 128;
 constexpr int PREP_WAVES = 1;  // wavefronts per player (wave h takes cells h, h + PREP_WAVES, ...; 2 measured slower)
-__global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
+// C4 tiles: a cell whose boxes reach beyond the held pellets is EXCLUDED -- it
+// reserves what it can see with a key that dominates every round and never eats
+// here; cells sharing a food with it go to the serial pass, which lets the
+// higher-priority ones eat and TAINTS the rest (left undone, resolved by a later
+// pass once the owners' outcomes arrived).  Cells that cannot touch a held food
+// are skipped.  resume: only cells not yet final (f_done != 1) are prepared.
+__device__ __forceinline__ double tile_rall() { return sqrt(kMaxMass / kPi) * (1 + 1e-9); }  // any cell's radius bound
+__global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume) {
   const int nprep = (d.NP * PREP_WAVES + 3) / 4;
   if ((int)blockIdx.x >= nprep) {  // extra blocks: player-cell grid counts
     const int e = blockIdx.x - nprep, nb = cgrid_blocks(d);
@@ -1444,9 +1475,17 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
   for (int k = h; k < n; k += PREP_WAVES) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
+    if (resume && d.f_done[ci] == 1) continue;  // final (here or by its owner's message)
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     int64_t cseq = d.c_seq[ci];
     Rect q = footprint(x, y, r, d.size);
+    if (d.tiled && !tile_near_rect(d, rect_grow(footprint(x, y, fmax(r, tile_rall()), d.size), 1, d.cols), 2)) {
+      if (lane == 0) {  // cannot compete for any held food: its owner decides it
+        d.f_cnt[ci] = 0;
+        d.f_done[ci] = 2;
+      }
+      continue;
+    }
     int cnt = 0;
     double lsum = 0;
     auto visit = [&](bool valid, int j) {
@@ -1508,6 +1547,24 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
     double M = py_min(kMaxMass, (m + sum) * (1 + 1e-9));
     double Rm = fmax(r, radius_of(M)) * (1 + 1e-9);
     wave_sync_lds();
+    if (d.tiled && (!(tile_holds_rect(d, rect_grow(q, 1, d.cols)) && tile_holds_rect(d, rect_grow(qb, 1, d.cols))) ||
+                    ((d.tile_flags & AIGAR_TILE_OWNED_ONLY) && !tile_owns(d, x, y)))) {
+      const uint64_t key = food_key(base + rounds + 2, prio);  // excluded: dominates overflow keys too
+      const Rect qm = footprint(x, y, fmax(r, tile_rall()), d.size);
+      if (lane == 0) {
+        d.f_cnt[ci] = kOverflow;
+        d.f_done[ci] = 2;
+      }
+      F.walk_pellets(q, [&](bool valid, int j) {
+        if (valid && F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), q))
+          atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
+      });
+      F.walk_blobs(qm, [&](bool valid, int j) {
+        if (valid && F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), qm))
+          atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
+      });
+      continue;
+    }
     int nsel = 0;
     bool ovf = cnt > PREP_CAND;
     if (!ovf) {
@@ -1568,10 +1625,18 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds) {
 }
 // one eaten food: the event (in its reference phase), kill, growth
 // (eatCell -> adjustCellSize -> grow, field.py:327-344)
+// (tiles: only the cell's owner logs and reports it; fx, fy locate a pellet on the other tiles)
 __device__ __forceinline__ void food_eat(const Dev &d, const Food &F, int a, int j, uint32_t prio, int t,
-                                         int64_t cseq, int64_t fseq, double fm, double &m, double &r, int &eaten) {
+                                         int64_t cseq, int64_t fseq, double fm, double &m, double &r, int &eaten,
+                                         bool own, double fx, double fy) {
   const bool bl = Food::blob(j);
-  ev_push(d, a, bl ? PH_BLOB : PH_PELLET, ((uint64_t)prio << 16) | (uint64_t)t, bl ? 7 : 6, cseq, fseq);
+  if (own) {
+    ev_push(d, a, bl ? PH_BLOB : PH_PELLET, ((uint64_t)prio << 16) | (uint64_t)t, bl ? 7 : 6, cseq, fseq);
+    if (d.tiled) {
+      if (bl) tile_out(d, TR_BLOB, j & ~kBlobBit, fseq, 0.0, 0.0);
+      else tile_out(d, TR_PELLET, 0, fseq, fx, fy);
+    }
+  }
   m = grow_mass(m, fm);
   r = radius_of(m);
   F.kill(j);
@@ -1581,6 +1646,7 @@ __device__ bool food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, uin
                               int cnt) {
   double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
   int64_t cseq = d.c_seq[ci];
+  const bool own = tile_owns(d, x, y);
   int eaten = 0;
   bool blobs = false, ate = false;
   Rect qb{};
@@ -1594,11 +1660,12 @@ __device__ bool food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, uin
     double fm = F.m(j), fx = F.x(j), fy = F.y(j), fr = F.r(j);
     if (blobs && !rect_hit(footprint(fx, fy, fr, d.size), qb)) continue;
     if (!(overlap(x, y, m, r, fx, fy, fm, fr) && can_eat(m, fm))) continue;
-    food_eat(d, F, a, j, prio, t, cseq, F.seq(j), fm, m, r, eaten);
+    food_eat(d, F, a, j, prio, t, cseq, F.seq(j), fm, m, r, eaten, own, fx, fy);
     ate = true;
   }
   d.c_m[ci] = m;
   d.c_r[ci] = r;
+  if (d.tiled && own && ate) tile_out(d, TR_CELL, (int32_t)ci, cseq, m, r);
   if (eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
   return ate;
 }
@@ -1673,6 +1740,7 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
   const int a = blockIdx.x, lane = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int nw = min(c.n_pend, d.Wcap);
+  const uint32_t excl_round = c.food_round + rounds + 2;  // tiles: excluded / tainted keys (k_food_prep)
   wave_fence();
   if (lane == 0) {
     c.n_pend = 0;
@@ -1714,7 +1782,39 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
     const double x = d.c_x[ci], y = d.c_y[ci];
     double m = d.c_m[ci], r = d.c_r[ci];
     const int64_t cseq = d.c_seq[ci];
+    const bool own = tile_owns(d, x, y);
+    if (d.tiled) {
+      // taint: a higher-priority excluded or tainted cell may eat one of this cell's
+      // foods; its outcome is not known here, so neither is this cell's (left undone)
+      const Rect q = footprint(x, y, r, d.size), qm = footprint(x, y, fmax(r, tile_rall()), d.size);
+      bool taint = false;
+      Rect box = q;
+      auto check = [&](bool valid, int j) {
+        bool hit = valid && F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), box);
+        if (hit) {
+          const uint64_t w = *F.owner(j);
+          hit = (uint32_t)(w >> 32) == excl_round && (0xFFFFFFFFu - (uint32_t)w) < prio;
+        }
+        if (__ballot(hit)) taint = true;
+      };
+      auto mark = [&](bool valid, int j) {
+        if (valid && F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), box))
+          atomicMax((unsigned long long *)F.owner(j), (unsigned long long)food_key(excl_round, prio));
+      };
+      F.walk_pellets(q, check);
+      box = qm;
+      F.walk_blobs(qm, check);
+      if (taint) {
+        box = q;
+        F.walk_pellets(q, mark);
+        box = qm;
+        F.walk_blobs(qm, mark);
+        wave_fence();
+        continue;
+      }
+    }
     int eaten = 0, t_base = 0;
+    bool ate = false;
     for (int kind = 0; kind < 2; kind++) {  // pellet turn, then blob turn (box after the pellets)
     const Rect q = footprint(x, y, r, d.size);
     int nc = 0;
@@ -1760,8 +1860,9 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
       if (!(overlap(x, y, m, r, s_x[k], s_y[k], fm, s_r[k]) && can_eat(m, fm))) continue;
       const int j = s_val[k];
       const int64_t fseq = s_key[k] & ~(1ll << 62);
+      ate = true;
       if (lane == 0) {
-        food_eat(d, F, a, j, prio, t_base + t, cseq, fseq, fm, m, r, eaten);
+        food_eat(d, F, a, j, prio, t_base + t, cseq, fseq, fm, m, r, eaten, own, s_x[k], s_y[k]);
       } else {
         m = grow_mass(m, fm);
         r = radius_of(m);
@@ -1774,6 +1875,7 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
       d.c_m[ci] = m;
       d.c_r[ci] = r;
       d.f_done[ci] = 1;
+      if (d.tiled && own && ate) tile_out(d, TR_CELL, (int32_t)ci, cseq, m, r);
       if (eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
       atomic_max_pos(&c.rmax_cell, r);  // (radii only grow while eating)
     }
@@ -2181,7 +2283,8 @@ __device__ void spawn_counts(const Dev &d, int a, int init) {
   ArenaCtl &c = d.ctl[a];
   c.dirty = 0;
   // spawnPellets: while len(pellets) < maxCollectibleCount
-  int alive_p = c.n_pel - c.n_pel_eaten + c.n_pnew;
+  // (tiles: the global count -- every tile spawns the same global list and keeps what it holds)
+  int alive_p = d.tiled ? c.n_pel_glob - c.n_eaten_glob + c.n_pnew : c.n_pel - c.n_pel_eaten + c.n_pnew;
   int kp = 0;
   if ((double)alive_p < d.max_pellets) kp = (int)ceil(d.max_pellets) - alive_p;
   if (alive_p + kp > d.Pcap || c.n_pnew + kp > d.Pcap) {
@@ -2193,6 +2296,7 @@ __device__ void spawn_counts(const Dev &d, int a, int init) {
   c.ctr_pellet_base = c.ctr_pellet;
   c.ctr_pellet += kp;
   c.n_spawn_p = kp;
+  c.n_pel_glob = alive_p + kp;
   // spawnViruses
   int kv = 0;
   if (d.virus_enabled && (double)c.n_vir < d.max_viruses) kv = (int)ceil(d.max_viruses) - c.n_vir;
@@ -2364,6 +2468,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.pcur = c.peat = 0;
   c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
+  c.n_pel_glob = c.n_eaten_glob = c.n_out = c.n_out_pel = c.n_undone = c.n_undone_glob = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
 }
 
@@ -2389,12 +2494,13 @@ void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
 // playerPelletOverlap + playerBlobOverlap: prep, reservation rounds, serial rest;
 // the player-cell grid (counts, scatter) rides along as extra blocks of the
 // prep and of the first round
-static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr) {
+// (resume: a further eat pass of a tiled tick -- the cell grid is built already)
+static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr, int resume = 0) {
   const int g = nblk(d.NP, 256);
   const long per = (long)kMaxCells * d.B;
   const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
-  const int ncg = nblk(std::max(per, (long)cc * cc + 1), 256) * d.A;
-  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4) + ncg), dim3(256), 0, s, d, rounds);
+  const int ncg = resume ? 0 : nblk(std::max(per, (long)cc * cc + 1), 256) * d.A;
+  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4) + ncg), dim3(256), 0, s, d, rounds, resume);
   for (int r = 1; r <= rounds; r++) {
     hipLaunchKernelGGL(k_food_commit, dim3(g + (r == 1 ? ncg : 0)), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
   }
@@ -2406,9 +2512,8 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 // hipGraph by api.hip).  Forking independent phases onto a second stream was
 // measured slower on MI355X (cross-queue dependencies cost more than the
 // overlap gains at this kernel size), so the graph stays linear.
-void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
-  Scratch scr{scr_k, scr_v};
-  const int gP = nblk(d.NP, 256);
+// the phases before the eat phase (field.py:94-198, 225-231, 246-253)
+void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
@@ -2420,7 +2525,9 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
     hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
   }
-  launch_food(d, s, rounds, scr);
+}
+// the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
+void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);  // + end-of-tick virus grid
@@ -2433,6 +2540,119 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
   // scatter's own threads it stretched that kernel ~5x; as separate blocks it
   // only adds them to the grid.
   launch_pellet_rebuild(d, s, PR_CLOSE);
+}
+void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
+  launch_tick_pre(d, s, scr_k, scr_v, rp);
+  launch_food(d, s, rounds, Scratch{scr_k, scr_v});
+  launch_tick_post(d, s, scr_k, scr_v);
+}
+
+// ------------------------------------------------------------ C4 tile passes
+// One eat pass of a tiled tick: (first: the tick's pellet-kill total restarts)
+// the eat phase for the not-yet-final cells, then the message -- records were
+// appended by the eat loops; the bitmap marks the owned cells now final; the
+// header carries the record count, the owned cells left undone and the pellet
+// kills.
+__global__ void k_tile_pass_begin(Dev d, int first) {
+  ArenaCtl &c = d.ctl[0];
+  c.n_out = c.n_out_pel = c.n_undone = 0;
+  if (first) c.n_eaten_glob = 0;
+}
+__global__ void __launch_bounds__(256) k_tile_collect(Dev d) {
+  const int gp = GTID;
+  if (gp >= d.NP || !d.p_alive[gp]) return;
+  unsigned long long *bm = (unsigned long long *)(d.outbox + 1 + d.tcap);
+  const int NP = d.NP, n = d.p_ncells[gp];
+  int und = 0;
+  for (int k = 0; k < n; k++) {
+    const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    if (!tile_owns(d, d.c_x[ci], d.c_y[ci])) continue;
+    if (d.f_done[ci] == 1) atomicOr(&bm[ci >> 6], 1ull << (ci & 63));
+    else und++;
+  }
+  if (und) atomicAdd(&d.ctl[0].n_undone, und);
+}
+__global__ void k_tile_header(Dev d) {
+  const ArenaCtl &c = d.ctl[0];
+  TileRec &h = d.outbox[0];
+  h.kind = TR_HDR;
+  h.idx = min(c.n_out, d.tcap);
+  h.seq = c.n_undone;
+  h.x = (double)c.n_out_pel;
+  h.y = 0;
+}
+void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first) {
+  hipLaunchKernelGGL(k_tile_pass_begin, dim3(1), dim3(1), 0, s, d, first);
+  launch_food(d, s, rounds, Scratch{scr_k, scr_v}, first ? 0 : 1);
+  (void)hipMemsetAsync(d.outbox + 1 + d.tcap, 0, 8 * (size_t)d.bm_words, s);
+  hipLaunchKernelGGL(k_tile_collect, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_tile_header, dim3(1), dim3(1), 0, s, d);
+}
+// the other tiles' messages: their owned cells' outcomes (pellet and blob kills,
+// new masses), their final cells, and the totals (thread 0)
+__global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
+  const int T = d.ntiles, nrec = T * d.tcap, nbm = T * d.bm_words;
+  int gi = GTID;
+  ArenaCtl &c = d.ctl[0];
+  if (gi == 0) {
+    int kills = 0, und = 0;
+    for (int k = 0; k < T; k++) {
+      const TileRec &h = d.inbox[(size_t)k * box_recs];
+      kills += (int)h.x;
+      und += (int)h.seq;
+    }
+    c.n_eaten_glob += kills;
+    c.n_undone_glob = und;
+  }
+  if (gi < nrec) {
+    const int k = gi / d.tcap, i = gi - k * d.tcap;
+    const TileRec *box = d.inbox + (size_t)k * box_recs;
+    if (k == d.tile_id || i >= box[0].idx) return;
+    const TileRec r = box[1 + i];
+    if (r.kind == TR_PELLET) {
+      const int bx = center_bucket_coord(r.x, d.cols), by = center_bucket_coord(r.y, d.cols);
+      if (!tile_holds_bucket(d, bx, by)) return;
+      const Food F(d, 0);
+      const int b = by * d.cols + bx, lo = min(d.pstart[b], F.n0), hi = min(d.pstart[b + 1], F.n0);
+      for (int t = lo; t < hi; t++)
+        if (d.pel_seq[F.pb][F.g(t)] == r.seq) {
+          d.pel_dead[F.g(t)] = 1;
+          return;
+        }
+      for (int j = F.n0; j < F.n0 + F.nst; j++)  // this tick's blob conversions (staged)
+        if (d.pn_seq[F.gs(j)] == r.seq) {
+          d.pel_dead[F.g(j)] = 1;
+          return;
+        }
+      set_err(d, 0, ERR_TILE_LOOKUP);
+    } else if (r.kind == TR_BLOB) {
+      if (d.b_seq[r.idx] != r.seq) return set_err(d, 0, ERR_TILE_LOOKUP);
+      d.b_flags[r.idx] = 0;
+      atomicOr(&c.dirty, DIRTY_BLOB);
+    } else if (r.kind == TR_CELL) {
+      if (d.c_seq[r.idx] != r.seq) return set_err(d, 0, ERR_TILE_LOOKUP);
+      d.c_m[r.idx] = r.x;
+      d.c_r[r.idx] = r.y;
+      d.f_done[r.idx] = 1;
+      atomic_max_pos(&c.rmax_cell, r.y);
+    }
+    return;
+  }
+  gi -= nrec;
+  if (gi < nbm) {
+    const int k = gi / d.bm_words, w = gi - k * d.bm_words;
+    if (k == d.tile_id) return;
+    unsigned long long b = ((const unsigned long long *)(d.inbox + (size_t)k * box_recs + 1 + d.tcap))[w];
+    while (b) {
+      const int t = __ffsll((long long)b) - 1;
+      b &= b - 1;
+      d.f_done[(size_t)w * 64 + t] = 1;
+    }
+  }
+}
+void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs) {
+  const long n = (long)d.ntiles * (d.tcap + d.bm_words);
+  hipLaunchKernelGGL(k_tile_apply, dim3(nblk(n, 256)), dim3(256), 0, s, d, box_recs);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty

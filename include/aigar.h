@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AIGAR_ABI_VERSION 1
+#define AIGAR_ABI_VERSION 2
 
 /* random number stream of the world (spawns, explosion angles) */
 #define AIGAR_RNG_PHILOX 0   /* Philox4x64-10 keyed by (seed, site, index): device + oracle */
@@ -67,6 +67,9 @@ extern "C" {
 #define AIGAR_EV_RESPAWN        10  /* (player index, new cell seq)  field.py:277  */
 
 #define AIGAR_FLAG_EVENTS 0x1       /* record the event log of each step */
+/* tile_flags: decide only the cells this tile owns (the others wait for their
+ * owners' messages) -- the strictest exchange pattern, used by the tests */
+#define AIGAR_TILE_OWNED_ONLY 0x1
 
 typedef struct aigar_handle aigar_handle;
 
@@ -87,6 +90,14 @@ typedef struct aigar_config {
   int32_t virus_cap;       /* 0 -> 2 * max_viruses + 64                               */
   int32_t event_cap;       /* events kept per arena per step (0 -> 65536)             */
   int32_t flags;           /* AIGAR_FLAG_*                                            */
+  /* C4: one arena tiled 2-D over tile_x * tile_y handles, one per GPU (SURVEY.md
+   * §8e).  1 x 1 (or 0 x 0) = untiled.  A tiled handle needs n_arenas == 1.     */
+  int32_t tile_x, tile_y;  /* tiles along x and y                                     */
+  int32_t tile_id;         /* this handle's tile, row-major: ty * tile_x + tx         */
+  int32_t tile_halo;       /* pellets held beyond the tile, field units (0 -> 400;    *
+                            * at least 140: an owned cell's reach; 370 covers any view) */
+  int32_t tile_cap;        /* records per exchange message (0 -> 4096)                */
+  int32_t tile_flags;      /* AIGAR_TILE_*                                            */
 } aigar_config;
 
 /*
@@ -248,6 +259,51 @@ int aigar_load_state(aigar_handle *h, int arena, const aigar_state *st);
  * in reference order.  *n gets the count; returns < 0 if cap is too small. */
 int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int cap, int *n);
 
+/*
+ * C4 tiled arena (field.py:85-92, 200-253, 256-313).  Every tile
+ * handle replays the whole tick on its replica of the players, cells, blobs and
+ * viruses; it holds only the pellets of its tile plus the halo.  The eat phase
+ * (field.py:207-222) is resolved per tile; the cells a tile owns (centre bucket
+ * in the tile) report their outcomes in ONE message per pass, and the caller's
+ * transport all-gathers the messages (RCCL all-gather over xGMI; in-process
+ * device copies for tests):
+ *   aigar_tile_begin(h, p)  policy (NONE / RANDOM) + the tick up to the first
+ *                           eat pass; the outbox holds the message
+ *   <all-gather every tile's outbox into every tile's inbox>
+ *   aigar_tile_apply(h, &u) the other tiles' outcomes; u = owned cells still
+ *                           undone on all tiles (same value on every tile)
+ *   while (u > 0) { aigar_tile_resume(h); <all-gather>; aigar_tile_apply(h, &u); }
+ *   aigar_tile_end(h, obs, dtype)  playerPlayerOverlap .. spawnStuff; then, if obs
+ *                           (DEVICE) is given, every bot's observation: exact for
+ *                           the bots whose view lies in the held pellets; the
+ *                           others have NaN in the pellet channel (their tile --
+ *                           the one owning the view's centre -- has it)
+ * The spawn deficit is global: each tile's message carries its pellet kills.
+ * aigar_tile_info: info[12] = ntiles, tile_id, owned bucket range x0, x1, y0, y1
+ * (half-open), held range x0, x1, y0, y1, records per message, bitmap words;
+ * the device outbox / inbox and the bytes of one message (the inbox holds
+ * ntiles messages, tile k at k * bytes).  A message is 32-byte records:
+ * [header: kind 0, record count, undone owned cells, pellet kills as double]
+ * [records: kind 1 pellet kill (seq, x, y) | 2 blob kill (slot, seq) | 3 cell
+ * outcome (pool index, seq, mass, radius)] [bitmap: owned cells now final].
+ * aigar_tile_set_buffers: use caller-owned device buffers instead (e.g. torch
+ * tensors that RCCL fills); aigar_tile_exchange_local: the in-process transport
+ * -- copies every handle's outbox into every handle's inbox (same process).
+ * aigar_get_state on a tiled handle returns the pellets the tile OWNS; the
+ * union over the tiles is the arena's pellet list.
+ */
+int aigar_tile_info(aigar_handle *h, int32_t *info, void **outbox, void **inbox, int64_t *msg_bytes);
+int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox);
+int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p);
+int aigar_tile_apply(aigar_handle *h, int *undone);
+int aigar_tile_resume(aigar_handle *h);
+int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype);
+int aigar_tile_exchange_local(aigar_handle **hs, int n);
+
+/* The event log as raw rows (key_hi = tick << 8 | phase, key_lo = order within the
+ * phase, code, a, b), unsorted: tiled arenas merge their tiles' logs by key. */
+int aigar_get_events_raw(aigar_handle *h, int arena, int64_t *out, int cap, int *n);
+
 /* Stream control. */
 int aigar_set_stream(aigar_handle *h, void *hip_stream);
 int aigar_sync(aigar_handle *h);
@@ -262,8 +318,8 @@ int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *laun
  * pellet + blob eating (cells), -, playerPlayerOverlap (players), -, -, ticks.  n <= 8. */
 int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n);
 
-/* Diagnostics: evaluate the device's correctly rounded pow (aigar_math.h) on
- * host arrays of n (x, y) pairs -- used by the parity tests. */
+/* Diagnostics: evaluate the device's pow (aigar_math.h: glibc 2.35's pow, bit
+ * for bit) on host arrays of n (x, y) pairs -- used by the parity tests. */
 int aigar_selftest_pow(const double *x, const double *y, double *out, int n);
 
 #ifdef __cplusplus

@@ -35,6 +35,12 @@ def load_golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 
 
+def load_snapshot(name):
+    """A matured world written by tools/mature.py (data/<name>.npz) as a state dict."""
+    z = np.load(os.path.join(ROOT, "data", name + ".npz"))
+    return {k: z[k] for k in z.files}
+
+
 def diff_states(a, b, ftol=FTOL):
     """Return a list of human-readable differences (empty == parity)."""
     out = []

@@ -68,3 +68,74 @@ def test_device_is_deterministic_at_full_size():
     for k in _abi.LAYOUT:
         assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
     assert parity.obs_close(oa, ob, 0.0)
+
+
+@pytest.mark.parametrize("policy", ["synthetic", "greedy"])
+def test_c3_matured_world_matches_oracle(policy):
+    """C3 from the matured tick-300 world (tools/mature.py: cells past 36 and 125,
+    387 multi-cell players): 60 ticks, every event, state and observation.  Split,
+    eject, blob eating, virus explosions, merges and cell-eats-cell all happen at
+    full size (field.py:200-253)."""
+    cfg = c3()
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    snap = parity.load_snapshot("c3_t300")
+    g.load_state(snap)
+    o.load_state(snap)
+    rng = np.random.default_rng(23)
+    kinds = set()
+    for t in range(60):
+        if policy == "greedy":
+            o.policy_greedy(True)
+            cmd = o.commands()
+        else:
+            cmd = parity.synthetic_commands(rng, None, 4096, 4800, 2.5e-3, 1e-2)
+        err, st = parity.run_pair(g, o, 1, lambda _: cmd, obs=(t % 10 == 9))
+        assert err is None, "tick %d: %s" % (t, err)
+        kinds |= set(o.events()[:, 1].tolist())
+    want = {_abi.EV_MERGE, _abi.EV_CELL_EAT_VIRUS, _abi.EV_EXPLODE, _abi.EV_CELL_EAT_PELLET, _abi.EV_CELL_EAT_CELL}
+    if policy == "synthetic":  # (the greedy bots never eject, bot.py:94)
+        want |= {_abi.EV_CELL_EAT_BLOB}
+    assert want <= kinds, kinds
+    s = g.get_state()
+    assert np.sum(s["players_i"][:, 4] > 1) > 100  # multi-cell players
+    g.close()
+    o.close()
+
+
+def test_c5_gpu_slice_matches_eight_oracles():
+    """C5's per-GPU slice: 8 independent arenas x 512 bots, field
+    1697, 43,200 pellets, viruses off, stepped by the same launches; each arena
+    against its own single-arena oracle (loaded from the arena's reset state, so
+    it carries that arena's Philox key) for 60 ticks: events every tick, states
+    and observations every 20."""
+    A, B = 8, 512
+    ch, ex = _abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY, _abi.EX_FOV | _abi.EX_MASS
+    g = _lib.Stepper(make_config(n_arenas=A, bots=B, field_size=1697, max_pellets=43200.0, channels=ch, extras=ex))
+    g.reset(40)
+    orcs = []
+    for a in range(A):
+        o = Oracle(make_config(bots=B, field_size=1697, max_pellets=43200.0, channels=ch, extras=ex))
+        o.load_state(g.get_state(a))
+        orcs.append(o)
+    rng = np.random.default_rng(40)
+    nev = 0
+    for t in range(60):
+        cmd = parity.synthetic_commands(rng, None, A * B, 1697, 0.01, 0.02)
+        g.set_commands(cmd)
+        g.step(1)
+        for a, o in enumerate(orcs):
+            o.set_commands(cmd[a * B:(a + 1) * B])
+            o.step(1)
+            ev = o.events()
+            assert np.array_equal(g.events(a), ev), "tick %d arena %d" % (t, a)
+            nev += len(ev)
+        if t % 20 == 19:
+            obs = g.observe()
+            for a, o in enumerate(orcs):
+                dif = parity.diff_states(g.get_state(a), o.get_state())
+                assert not dif, (t, a, dif[:3])
+                assert parity.obs_close(obs[a * B:(a + 1) * B], o.observe()), (t, a)
+    assert nev > 8 * 60 * 5
+    g.close()
+    for o in orcs:
+        o.close()

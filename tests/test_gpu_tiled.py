@@ -1,0 +1,152 @@
+"""GPU: C4 -- one arena tiled 2-D over tile handles (aigar_amd/tiles.py, the
+aigar_tile_* C-ABI) against the UNTILED oracle.
+
+Every tile replays the tick on its replica of the players, cells, blobs and
+viruses and holds only its tile's pellets plus a halo; the eat phase
+(field.py:207-222) is resolved per tile and the owners' outcomes are
+all-gathered (in-process device copies here; RCCL in production).  The bar is
+the untiled one: the merged event log (every eat / merge / split / explosion /
+death / respawn, indices and order) equals the oracle's exactly, the merged
+state (replicated part from tile 0, pellets as the union of the owned sets)
+within 1e-5, observations within 1e-5 for every bot.  Small halos force the
+cross-tile paths: cells whose reach leaves the held pellets (excluded), the
+taint of cells that share a food with them, and further exchange passes.
+"""
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import Oracle, make_config
+import parity
+
+pytestmark = pytest.mark.gpu
+_lib = pytest.importorskip("aigar_amd._lib")
+from aigar_amd.tiles import TiledArena  # noqa: E402
+
+C3_CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
+         | _abi.OBS_ENEMY_LF)
+
+
+def run(cfg, tx, ty, ticks, seed, cmd_fn, halo=0, obs_every=0, check_every=10, ftol=parity.FTOL, flags=0,
+        start=None):
+    ta, o = TiledArena(cfg, tx, ty, halo=halo, flags=flags), Oracle(cfg)
+    if start is None:
+        ta.reset(seed)
+        o.reset(seed)
+    else:  # a matured world (tools/mature.py): every tile keeps the pellets it holds
+        ta.load_state(start)
+        o.load_state(start)
+    dif = parity.diff_states(ta.get_state(), o.get_state())
+    assert not dif, dif
+    kinds, nev = set(), 0
+    for t in range(ticks):
+        cmd = cmd_fn(t, o)
+        ta.set_commands(cmd)
+        o.set_commands(cmd)
+        ta.tick()
+        o.step(1)
+        eg, eo = ta.events(), o.events()
+        if not np.array_equal(eg, eo):
+            n = min(len(eg), len(eo))
+            bad = next((i for i in range(n) if not np.array_equal(eg[i], eo[i])), n)
+            raise AssertionError("tick %d: event %d differs (tiles %d events, oracle %d): %s vs %s" % (
+                t, bad, len(eg), len(eo), eg[bad:bad + 2].tolist(), eo[bad:bad + 2].tolist()))
+        kinds |= set(eo[:, 1].tolist())
+        nev += len(eo)
+        if (t + 1) % check_every == 0 or t == ticks - 1:
+            dif = parity.diff_states(ta.get_state(), o.get_state(), ftol)
+            assert not dif, "tick %d: %s" % (t, dif[:3])
+        if obs_every and (t + 1) % obs_every == 0:
+            og, oo = ta.observe(), o.observe()
+            assert parity.obs_close(og, oo), "tick %d: observations differ" % t
+    stats = {"kinds": kinds, "events": nev, "passes": list(ta.passes)}
+    ta.close()
+    o.close()
+    return stats
+
+
+def synthetic(n, size, ps, pe, seed):
+    rng = np.random.default_rng(seed)
+    return lambda t, o: parity.synthetic_commands(rng, None, n, size, ps, pe)
+
+
+def greedy(gsplit):
+    def f(t, o):
+        o.policy_greedy(gsplit)
+        return o.commands()
+    return f
+
+
+def c3_config(**kw):
+    return make_config(bots=4096, field_size=4800, virus=True, max_pellets=100000.0, channels=C3_CH, extras=0x1F,
+                       **kw)
+
+
+@pytest.mark.parametrize("tx,ty", [(2, 1), (2, 2)])
+def test_c3_tiled_matches_untiled_oracle(tx, ty):
+    """C3 (4096 bots, 100k pellets, 1152 viruses, split p 2.5e-3 / eject p 1e-2)
+    from the matured tick-300 world (cells past 125, multi-cell players), 200 ticks:
+    splits, ejections, blob eating, explosions, merges, cell-eats-cell across the
+    tile borders."""
+    st = run(c3_config(), tx, ty, 200, 31, synthetic(4096, 4800, 2.5e-3, 1e-2, 31), obs_every=25, check_every=25,
+             start=parity.load_snapshot("c3_t300"))
+    assert st["events"] > 10000
+    assert {_abi.EV_CELL_EAT_PELLET, _abi.EV_CELL_EAT_BLOB, _abi.EV_RESPAWN, _abi.EV_MERGE, _abi.EV_EXPLODE,
+            _abi.EV_CELL_EAT_CELL, _abi.EV_CELL_EAT_VIRUS} <= st["kinds"], st["kinds"]
+
+
+def test_c3_small_halo_forces_cross_tile_passes():
+    """2 x 2 tiles with the smallest halo (an owned cell's reach) deciding only the
+    cells they own (AIGAR_TILE_OWNED_ONLY): every cell near a border that shares a
+    food with a higher-priority cell of another tile is tainted and waits for that
+    tile's message, so ticks take several exchange passes; the result must still
+    be the untiled world."""
+    st = run(c3_config(), 2, 2, 60, 32, synthetic(4096, 4800, 2.5e-3, 1e-2, 32), halo=140, check_every=20,
+             flags=_abi.TILE_OWNED_ONLY, start=parity.load_snapshot("c3_t300"))
+    assert st["events"] > 3000
+    assert max(st["passes"]) > 1
+
+
+@pytest.mark.parametrize("tx,ty,flags,seed", [(2, 2, _abi.TILE_OWNED_ONLY, 4), (2, 1, _abi.TILE_OWNED_ONLY, 5),
+                                               (2, 2, 0, 6)])
+def test_border_crowded_greedy_tiles(tx, ty, flags, seed):
+    """64 greedy bots in a 250-unit field cut into 2 x 2 (or 2 x 1) tiles: bots
+    chase each other across the tile edges, cells eat pellets, blobs and each
+    other there and explode on viruses near them; 300 ticks against the untiled
+    oracle.  With AIGAR_TILE_OWNED_ONLY every tile decides only its own cells,
+    so contested border foods go through the taint / extra-pass exchange."""
+    cfg = make_config(bots=64, virus=True, max_viruses=30, field_size=250,
+                      channels=_abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY, extras=0x3)
+    st = run(cfg, tx, ty, 300, seed, greedy(True), check_every=10, ftol=1e-9, flags=flags)
+    assert {_abi.EV_CELL_EAT_CELL, _abi.EV_PLAYER_DEATH, _abi.EV_CELL_EAT_PELLET,
+            _abi.EV_EXPLODE} <= st["kinds"], st["kinds"]
+    if flags:
+        assert max(st["passes"]) > 1, "the scenario never needed a second exchange pass"
+
+
+def test_tiled_load_state_continues_like_the_oracle():
+    """A tiled arena loaded from a mid-run oracle snapshot (each tile keeps its
+    held pellets) continues exactly like the oracle."""
+    cfg = make_config(bots=256, virus=True, max_viruses=40, channels=C3_CH, extras=0x1F)
+    o = Oracle(cfg)
+    o.reset(9)
+    rng = np.random.default_rng(9)
+    for _ in range(40):
+        o.set_commands(parity.synthetic_commands(rng, None, 256, 1200, 0.02, 0.05))
+        o.step(1)
+    snap = o.get_state()
+    ta = TiledArena(cfg, 2, 2, halo=100)
+    ta.load_state(snap)
+    dif = parity.diff_states(ta.get_state(), snap)
+    assert not dif, dif
+    for t in range(60):
+        cmd = parity.synthetic_commands(rng, None, 256, 1200, 0.02, 0.05)
+        ta.set_commands(cmd)
+        o.set_commands(cmd)
+        ta.tick()
+        o.step(1)
+        assert np.array_equal(ta.events(), o.events()), "tick %d" % t
+    dif = parity.diff_states(ta.get_state(), o.get_state())
+    assert not dif, dif
+    ta.close()
+    o.close()
