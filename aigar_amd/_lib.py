@@ -82,6 +82,7 @@ def load(build_if_missing=False):
         "aigar_get_events_raw": [vp, i32, C.POINTER(C.c_int64), i32, C.POINTER(i32)],
         "aigar_tile_info": [vp, C.POINTER(C.c_int32), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_int64)],
         "aigar_tile_set_buffers": [vp, vp, vp],
+        "aigar_tile_msg_bytes": [vp, C.POINTER(C.c_int64)],
         "aigar_tile_begin": [vp, C.POINTER(_abi.RunParams)],
         "aigar_tile_apply": [vp, C.POINTER(i32)],
         "aigar_tile_resume": [vp],
@@ -223,10 +224,27 @@ class Stepper:
                                         int(skip), C.byref(prm), C.c_void_p(reward.data_ptr()),
                                         C.c_void_p(obs.data_ptr()), dt))
 
+    def _check_out(self, out, shape, dtypes, what):
+        """The library writes prod(shape) elements of the dtype into out: refuse a
+        buffer of another shape / dtype, a strided view or a tensor on another device."""
+        d = str(getattr(out, "dtype", "")).replace("torch.", "")
+        if tuple(out.shape) != tuple(shape):
+            raise ValueError("%s: out must have shape %s, got %s" % (what, tuple(shape), tuple(out.shape)))
+        if d not in dtypes:
+            raise ValueError("%s: out dtype must be one of %s, got %s" % (what, dtypes, d))
+        contig = out.flags["C_CONTIGUOUS"] if isinstance(out, np.ndarray) else out.is_contiguous()
+        if not contig:
+            raise ValueError("%s: out must be C-contiguous" % what)
+        if hasattr(out, "is_cuda") and out.is_cuda and out.device.index not in (None, self.cfg.device):
+            raise ValueError("%s: out is on cuda:%s, the stepper on device %d" % (what, out.device.index,
+                                                                                 self.cfg.device))
+        return d
+
     def observe(self, out=None, dtype=np.float64):
         if out is None:
             out = np.zeros((self.NP, self.obs_len), dtype)
-        dt = 0 if (getattr(out, "dtype", None) in (np.float64,) or str(getattr(out, "dtype", "")) == "torch.float64") else 1
+        d = self._check_out(out, (self.NP, self.obs_len), ("float64", "float32"), "observe")
+        dt = 0 if d == "float64" else 1
         p, dev = _ptr(out)
         self._chk(self.L.aigar_observe(self.h, p, dt, dev))
         return out
@@ -236,8 +254,12 @@ class Stepper:
         uint8 [NP, side, side, 3] when rgb, else float64/float32 grayscale [NP, side, side]."""
         if out is None:
             out = np.zeros((self.NP, side, side, 3), np.uint8) if rgb else np.zeros((self.NP, side, side), np.float64)
-        d = str(getattr(out, "dtype", ""))
-        dt = 2 if "uint8" in d else 0 if "float64" in d else 1
+        d = str(getattr(out, "dtype", "")).replace("torch.", "")
+        if d == "uint8":
+            self._check_out(out, (self.NP, side, side, 3), ("uint8",), "observe_pixels")
+        else:
+            self._check_out(out, (self.NP, side, side), ("float64", "float32"), "observe_pixels")
+        dt = 2 if d == "uint8" else 0 if d == "float64" else 1
         p, dev = _ptr(out)
         self._chk(self.L.aigar_observe_pixels(self.h, p, int(side), int(color_seed), dt, dev))
         return out
@@ -291,6 +313,12 @@ class Stepper:
         return {"ntiles": v[0], "tile_id": v[1], "own": tuple(v[2:6]), "held": tuple(v[6:10]), "tcap": v[10],
                 "bm_words": v[11], "outbox": ob.value, "inbox": ib.value, "msg_bytes": nb.value}
 
+    def tile_msg_bytes(self):
+        """Bytes of the current pass's message (the first pass sends no bitmap)."""
+        n = C.c_int64(0)
+        self._chk(self.L.aigar_tile_msg_bytes(self.h, C.byref(n)))
+        return n.value
+
     def tile_set_buffers(self, outbox_ptr, inbox_ptr):
         self._chk(self.L.aigar_tile_set_buffers(self.h, C.c_void_p(int(outbox_ptr)), C.c_void_p(int(inbox_ptr))))
 
@@ -316,7 +344,8 @@ class Stepper:
             p = C.c_void_p(out.data_ptr())
         self._chk(self.L.aigar_tile_end(self.h, p, dt))
 
-    COUNTERS = ("vb_serial", "pv_serial", "food_serial", "-", "pp_serial_players", "-", "-", "ticks")
+    COUNTERS = ("vb_serial", "pv_serial", "food_serial", "pellets_eaten", "pp_serial_players", "pellets_spawned", "-",
+                "ticks")
 
     def counters(self, arena=0):
         out = np.zeros(8, np.int64)

@@ -70,7 +70,8 @@ struct aigar_handle {
   uint8_t *d_pix_ovf = nullptr;  // per player: frame left to the pixel kernel's second pass
   size_t pix_bytes = 0;
   std::vector<void *> allocs;
-  int box_recs = 0;  // C4: TileRec slots of one exchange message (header + records + bitmap)
+  int box_recs = 0;   // C4: TileRec slots of a full exchange message (header + records + bitmap)
+  int pass_recs = 0;  // ... of the current pass's message (the first pass sends no bitmap)
   bool profile = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // timer name -> recorded (start, stop) event pairs, resolved lazily
@@ -243,7 +244,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
     d.loc_by0 = std::max(0, d.own_by0 - hb);
     d.loc_by1 = std::min(d.cols, d.own_by1 + hb);
   }
-  d.tcap = cfg->tile_cap > 0 ? cfg->tile_cap : 4096;
+  d.tcap = cfg->tile_cap > 0 ? cfg->tile_cap : 2048;
   d.bm_words = (int)(((size_t)kMaxCells * d.NP + 255) / 256 * 4);  // 16 * NP bits, whole TileRecs
   h->box_recs = 1 + d.tcap + d.bm_words / 4;
   for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_glibc((double)k, 0.32);
@@ -522,6 +523,12 @@ extern "C" int aigar_tile_info(aigar_handle *h, int32_t *info, void **outbox, vo
   if (msg_bytes) *msg_bytes = (int64_t)h->box_recs * (int64_t)sizeof(TileRec);
   return 0;
 }
+extern "C" int aigar_tile_msg_bytes(aigar_handle *h, int64_t *bytes) {
+  if (need_tiled(h) || !bytes) return bytes ? -1 : fail("null argument");
+  if (!h->pass_recs) return fail("tile_msg_bytes: no pass begun");
+  *bytes = (int64_t)h->pass_recs * (int64_t)sizeof(TileRec);
+  return 0;
+}
 extern "C" int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox) {
   if (need_tiled(h)) return -1;
   if (!outbox || !inbox) return fail("tile_set_buffers: null buffer");
@@ -541,6 +548,7 @@ extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
   Mark m(h, "tile_begin");
   launch_tick_pre(h->d, h->stream, h->scr_k, h->scr_v, &rp);
   launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 1);
+  h->pass_recs = 1 + h->d.tcap;
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -549,7 +557,7 @@ extern "C" int aigar_tile_apply(aigar_handle *h, int *undone) {
   HIPCHK(hipSetDevice(h->cfg.device));
   {
     Mark m(h, "tile_apply");
-    launch_tile_apply(h->d, h->stream, h->box_recs);
+    launch_tile_apply(h->d, h->stream, h->pass_recs);
   }
   HIPCHK(hipGetLastError());
   ArenaCtl c;
@@ -564,6 +572,7 @@ extern "C" int aigar_tile_resume(aigar_handle *h) {
   HIPCHK(hipSetDevice(h->cfg.device));
   Mark m(h, "tile_resume");
   launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 0);
+  h->pass_recs = h->box_recs;
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -587,11 +596,12 @@ extern "C" int aigar_tile_exchange_local(aigar_handle **hs, int n) {
   if (!hs || n < 1) return fail("null argument");
   for (int i = 0; i < n; i++) {
     if (need_tiled(hs[i])) return -1;
-    if (hs[i]->d.ntiles != n || hs[i]->box_recs != hs[0]->box_recs) return fail("tile_exchange_local: mismatched tiles");
+    if (hs[i]->d.ntiles != n || hs[i]->pass_recs != hs[0]->pass_recs || hs[i]->pass_recs == 0)
+      return fail("tile_exchange_local: tiles are not at the same pass");
     HIPCHK(hipSetDevice(hs[i]->cfg.device));
     HIPCHK(hipStreamSynchronize(hs[i]->stream));
   }
-  const size_t bytes = (size_t)hs[0]->box_recs * sizeof(TileRec);
+  const size_t bytes = (size_t)hs[0]->pass_recs * sizeof(TileRec);
   for (int i = 0; i < n; i++)
     for (int k = 0; k < n; k++) {
       const aigar_handle *src = hs[k];

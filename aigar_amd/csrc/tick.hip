@@ -2297,6 +2297,10 @@ __device__ void spawn_counts(const Dev &d, int a, int init) {
   c.ctr_pellet += kp;
   c.n_spawn_p = kp;
   c.n_pel_glob = alive_p + kp;
+  if (!init) {  // diagnostics: pellets eaten / respawned this tick (whole arena)
+    c.stat[3] += d.tiled ? c.n_eaten_glob : c.n_pel_eaten;
+    c.stat[5] += kp;
+  }
   // spawnViruses
   int kv = 0;
   if (d.virus_enabled && (double)c.n_vir < d.max_viruses) kv = (int)ceil(d.max_viruses) - c.n_vir;
@@ -2558,7 +2562,7 @@ __global__ void k_tile_pass_begin(Dev d, int first) {
   c.n_out = c.n_out_pel = c.n_undone = 0;
   if (first) c.n_eaten_glob = 0;
 }
-__global__ void __launch_bounds__(256) k_tile_collect(Dev d) {
+__global__ void __launch_bounds__(256) k_tile_collect(Dev d, int with_bitmap) {
   const int gp = GTID;
   if (gp >= d.NP || !d.p_alive[gp]) return;
   unsigned long long *bm = (unsigned long long *)(d.outbox + 1 + d.tcap);
@@ -2567,8 +2571,8 @@ __global__ void __launch_bounds__(256) k_tile_collect(Dev d) {
   for (int k = 0; k < n; k++) {
     const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     if (!tile_owns(d, d.c_x[ci], d.c_y[ci])) continue;
-    if (d.f_done[ci] == 1) atomicOr(&bm[ci >> 6], 1ull << (ci & 63));
-    else und++;
+    if (d.f_done[ci] != 1) und++;
+    else if (with_bitmap) atomicOr(&bm[ci >> 6], 1ull << (ci & 63));
   }
   if (und) atomicAdd(&d.ctl[0].n_undone, und);
 }
@@ -2581,17 +2585,22 @@ __global__ void k_tile_header(Dev d) {
   h.x = (double)c.n_out_pel;
   h.y = 0;
 }
+// The first pass's message has no bitmap: a tick that needs a second pass
+// learns the other tiles' non-eating final cells from the second pass's
+// bitmaps (it may take one pass longer; ticks rarely need a second at all).
 void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first) {
   hipLaunchKernelGGL(k_tile_pass_begin, dim3(1), dim3(1), 0, s, d, first);
   launch_food(d, s, rounds, Scratch{scr_k, scr_v}, first ? 0 : 1);
-  (void)hipMemsetAsync(d.outbox + 1 + d.tcap, 0, 8 * (size_t)d.bm_words, s);
-  hipLaunchKernelGGL(k_tile_collect, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d);
+  if (!first) (void)hipMemsetAsync(d.outbox + 1 + d.tcap, 0, 8 * (size_t)d.bm_words, s);
+  hipLaunchKernelGGL(k_tile_collect, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, first ? 0 : 1);
   hipLaunchKernelGGL(k_tile_header, dim3(1), dim3(1), 0, s, d);
 }
 // the other tiles' messages: their owned cells' outcomes (pellet and blob kills,
 // new masses), their final cells, and the totals (thread 0)
+// box_recs: records per inbox slot (the pass's message size); bitmaps only when
+// the messages carry them (box_recs covers them)
 __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
-  const int T = d.ntiles, nrec = T * d.tcap, nbm = T * d.bm_words;
+  const int T = d.ntiles, nrec = T * d.tcap, nbm = box_recs > 1 + d.tcap ? T * d.bm_words : 0;
   int gi = GTID;
   ArenaCtl &c = d.ctl[0];
   if (gi == 0) {
@@ -2651,7 +2660,7 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
   }
 }
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs) {
-  const long n = (long)d.ntiles * (d.tcap + d.bm_words);
+  const long n = (long)d.ntiles * (d.tcap + (box_recs > 1 + d.tcap ? d.bm_words : 0));
   hipLaunchKernelGGL(k_tile_apply, dim3(nblk(n, 256)), dim3(256), 0, s, d, box_recs);
 }
 

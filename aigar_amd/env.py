@@ -55,8 +55,10 @@ class AgarVecEnv:
         return self.observe()
 
     def observe(self):
+        """A fresh tensor: the device buffer is rewritten by the next decision, so
+        (s, a, r, s') tuples must not alias it (self.obs is that buffer)."""
         self.stepper.observe(self.obs)
-        return self.obs
+        return self.obs.clone()
 
     def step(self, actions):
         """actions: [n_players, 2..4] tensor/array in [0, 1] -> (obs, reward, alive).
@@ -70,7 +72,7 @@ class AgarVecEnv:
         buf.copy_(act)
         self.stepper.env_step(buf, self._r, self.obs, self.enable_split, self.skip, self.reward_params)
         alive = ~torch.isnan(self.obs[:, 0])
-        return self.obs, self._r.clone(), alive
+        return self.obs.clone(), self._r.clone(), alive
 
     def step_calls(self, actions):
         """The same decision as separate calls (apply_actions / step / rewards / observe)."""

@@ -180,28 +180,62 @@ class TorchTransport:
     over the process group (RCCL on `nccl`, gloo on CPU).  The tile's outbox /
     inbox are torch tensors the collective writes in place; `for_stepper` hands
     them to the tile handle (and the handle adopts torch's stream, so the
-    collective and the tile kernels are ordered on one queue)."""
+    collective and the tile kernels are ordered on one queue).  staged: the
+    process group cannot take device tensors (gloo rehearsal on GPUs): the
+    message goes through host copies."""
 
-    def __init__(self, msg_bytes, ntiles, device, group=None):
+    def __init__(self, msg_bytes, ntiles, device, group=None, staged=False):
         import torch
         import torch.distributed as dist
-        self.dist, self.group = dist, group
+        self.torch, self.dist, self.group = torch, dist, group
         self.msg_bytes, self.ntiles = int(msg_bytes), int(ntiles)
         self.outbox = torch.zeros(self.msg_bytes, dtype=torch.uint8, device=device)
         self.inbox = torch.zeros(self.ntiles * self.msg_bytes, dtype=torch.uint8, device=device)
+        self.staged = bool(staged) and self.outbox.is_cuda
+        if self.staged:
+            self._ho = torch.zeros(self.msg_bytes, dtype=torch.uint8)
+            self._hi = torch.zeros(self.ntiles * self.msg_bytes, dtype=torch.uint8)
+        self._marks = []
 
     @classmethod
-    def for_stepper(cls, stepper, group=None):
+    def for_stepper(cls, stepper, group=None, staged=False):
         import torch
         info = stepper.tile_info()
         dev = torch.device("cuda", torch.cuda.current_device())
-        t = cls(info["msg_bytes"], info["ntiles"], dev, group)
+        t = cls(info["msg_bytes"], info["ntiles"], dev, group, staged)
         stepper.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         stepper.tile_set_buffers(t.outbox.data_ptr(), t.inbox.data_ptr())
         return t
 
     def exchange(self, steppers=None):
-        self.dist.all_gather_into_tensor(self.inbox, self.outbox, group=self.group)
+        """All-gather this pass's messages (steppers: this rank's tile, whose current
+        message size is taken; default: the full message)."""
+        torch = self.torch
+        n = steppers[0].tile_msg_bytes() if steppers else self.msg_bytes
+        nt = self.ntiles * n
+        timed = self.outbox.is_cuda
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        if self.staged:
+            self._ho[:n].copy_(self.outbox[:n])
+            self.dist.all_gather_into_tensor(self._hi[:nt], self._ho[:n], group=self.group)
+            self.inbox[:nt].copy_(self._hi[:nt])
+        else:
+            self.dist.all_gather_into_tensor(self.inbox[:nt], self.outbox[:n], group=self.group)
+        if timed:
+            e1.record()
+            self._marks.append((e0, e1))
+
+    def reset_timing(self):
+        self._marks = []
+
+    def avg_exchange_ms(self):
+        """Average device time of one exchange since reset_timing (CUDA events)."""
+        if not self._marks:
+            return None
+        self.torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self._marks) / len(self._marks)
 
 
 # ---- message layout (include/aigar.h aigar_tile_info; aigar_dev.h TileRec)

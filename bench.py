@@ -5,10 +5,14 @@ One step = one synthetic-population policy pass + Field.update() for the
 whole arena + the grid observation for every bot.
 env-steps = bots x steps.  Default workload = BASELINE.json configs[2] (C3):
 4096 bots, 100k pellets, 1152 viruses, split + eject on, field 4800, on one
-MI355X.  For N > 1 (launched by torch.distributed.run, one rank per GPU) each
-rank steps its own C3 arena (independent replicas, weak scaling, no collective
-in the data path); the timed region is bracketed by barrier + synchronize and
-the max over ranks is taken.
+MI355X, started from the matured tick-50 world of data/c3_t50.npz (the
+survey's warm distribution: mean cell mass 17.4, max ~54; tools/mature.py).
+For N > 1 (launched by torch.distributed.run, one rank per GPU) `value` is
+every rank stepping its own C3 arena (independent replicas, weak scaling, no
+collective in the data path); the timed region is bracketed by barrier +
+synchronize and the max over ranks is taken.  Beside it, the "c4" object
+times ONE C3 arena tiled over the N ranks (BASELINE configs[3]: RCCL
+all-gather of the tiles' eat-phase messages over xGMI, strong scaling).
 
 The timed steps are issued with aigar_run: each step (policy + tick +
 observation) is one hipGraph replay.  The per-phase breakdown and the roofline
@@ -31,6 +35,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from aigar_amd import _abi, replicas  # noqa: E402
+
+# the reference's own Python src/model at C3 (tick + observation of every bot, one
+# core), timed in the build container by the survey: the reference
+# itself cannot travel to the GPU box, so it is quoted beside the C-port baseline
+REFERENCE_PY_C3 = {"value": 356.0, "unit": "env-steps/s", "cores": 1, "kind": "reference",
+                   "source": "SURVEY.md §6: reference src/model (Python, Greedy bots) Field.update + "
+                             "getGridStateRepresentation for all 4096 bots, build container, 1 core"}
+SNAPSHOTS = {"c3": "c3_t50"}  # matured start worlds (tools/mature.py)
 
 # C3 observation config: VIRUS_SPAWN + ENABLE_SPLIT (networkParameters.py:76-96)
 C3_CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
@@ -136,6 +148,46 @@ def cpu_baseline(name, budget_s=12.0, seed=1, policy="random"):
                       "steps, oracle/oracle.c single thread, %.1f s" % (name.upper(), n, policy, bots, dt)}
 
 
+def _c5_arena_worker(args):
+    """One process of the C5 CPU baseline: a 512-bot arena stepped by the oracle."""
+    seed, budget_s = args
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+    bots, field, pellets, virus, ps, pe, ch, ex, _ = WORKLOADS["c5"]
+    o = Oracle(make_cfg("c5", arenas=1))
+    o.reset(seed)
+    rng = np.random.default_rng(seed)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        cmd = np.zeros((bots, 4))
+        cmd[:, 0] = rng.random(bots) * field
+        cmd[:, 1] = rng.random(bots) * field
+        o.set_commands(cmd)
+        o.step(1)
+        o.observe()
+        n += 1
+    dt = time.perf_counter() - t0
+    o.close()
+    return bots * n, dt
+
+
+def cpu_baseline_c5(budget_s=12.0):
+    """SURVEY.md §8d C5 CPU baseline: min(64, cores) processes, one 512-bot arena
+    each (the reference's own mp.Pool pattern, aigar.py:549), aggregate env-steps/s."""
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    nproc = max(1, min(64, cores, 16))  # (the GPU box grants 16 CPUs per GPU)
+    with mp.get_context("spawn").Pool(nproc) as pool:
+        res = pool.map(_c5_arena_worker, [(1000 + k, budget_s) for k in range(nproc)])
+    rate = sum(u / dt for u, dt in res)
+    return {"value": rate, "unit": "env-steps/s", "cores": nproc, "kind": "port",
+            "sample": "C5: %d processes x one 512-bot arena (field 1697, 43,200 pellets), random commands + "
+                      "Field.update + obs, oracle/oracle.c, %.0f s each" % (nproc, budget_s)}
+
+
 def batched(name, arenas, policy, ps, pe, seed, device, steps=20, warmup=5):
     """The same per-arena workload, `arenas` independent arenas stepped by the
     same launches (batched-env mode, SURVEY.md §8e C5 pattern): what one MI355X
@@ -160,6 +212,77 @@ def batched(name, arenas, policy, ps, pe, seed, device, steps=20, warmup=5):
             "ms_per_step": dt / steps * 1e3, "steps": steps}
 
 
+def start_world(stp, name, seed, arenas):
+    """Reset, or load the workload's matured snapshot into every arena."""
+    snap = SNAPSHOTS.get(name)
+    path = os.path.join(ROOT, "data", "%s.npz" % snap) if snap else None
+    if path is None or not os.path.exists(path):
+        stp.reset(seed)
+        return "reset(seed %d)" % seed
+    z = np.load(path)
+    d = {k: z[k] for k in z.files}
+    stp.reset(seed)
+    for a in range(arenas):
+        stp.load_state(d, a)
+    return "data/%s.npz (tick %d, mean cell mass %.2f, max %.1f)" % (
+        snap, int(d["tick"]), float(d["cells_f"][:, 2].mean()), float(d["cells_f"][:, 2].max()))
+
+
+def tick_bytes(st, alive, field, n_eaten):
+    """Algorithmic HBM bytes of one Field.update (SURVEY.md §8d formula, fp64
+    records): every cell record read and written (88 B), the pellet / enemy-cell
+    candidates each cell's overlap tests read (32 B / 88 B, expected counts from
+    the densities over the cell's hash box), the eaten and respawned pellet
+    records (32 B each), and the cell hash (4 B per bucket + 4 B per cell)."""
+    n_c = st["n_cells"]
+    if n_c == 0:
+        return 0.0
+    r = np.sqrt(np.asarray(st["cells_f"])[:, 2] / np.pi)
+    box = float(np.mean((2 * r + 20.0) ** 2))
+    k_p = st["n_pellets"] / float(field * field) * box
+    k_e = n_c / float(field * field) * box
+    H = int(np.ceil(field / 20.0)) ** 2
+    return 2 * 88 * n_c + n_c * k_p * 32 + n_c * k_e * 88 + 2 * n_eaten * 32 + 4 * H + 4 * n_c
+
+
+def c4_leg(args, name, rank, world, local, seed, dist, backend):
+    """BASELINE configs[3]: ONE C3 arena tiled over the N ranks (aigar_amd/tiles.py),
+    each rank one tile; the eat-phase messages all-gathered over RCCL (xGMI).
+    Strong scaling: the same 4096 bots whatever N.  Returns the side object."""
+    import torch
+    from aigar_amd import _lib, tiles
+    tx, ty = tiles.tile_grid(world)
+    cfg = tiles.tile_config(make_cfg(name, device=local, arenas=1), tx, ty, rank)
+    stp = _lib.Stepper(cfg)
+    tr = tiles.TorchTransport.for_stepper(stp, staged=(backend != "nccl"))
+    start = start_world(stp, name, seed, 1)
+    bots, field, pellets, virus, ps, pe, ch, ex, _ = WORKLOADS[name]
+    obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
+    steps, warm = max(10, min(args.steps, 100)), 5
+    tick = lambda: tiles.tiled_tick([stp], tr, "random", ps, pe, args.seed, [obs])
+    for _ in range(warm):
+        tick()
+    torch.cuda.synchronize()
+    replicas.barrier(dist)
+    tr.reset_timing()
+    passes = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        passes += tick()
+    torch.cuda.synchronize()
+    replicas.barrier(dist)
+    el = replicas.max_over_ranks(dist, time.perf_counter() - t0, device="cuda" if backend == "nccl" else None)
+    ex_ms = tr.avg_exchange_ms()
+    stp.sync()
+    info = stp.tile_info()
+    stp.close()
+    return {"workload": "C4: one C3 arena (%d bots) tiled %dx%d over %d GPUs, start %s" % (bots, tx, ty, world, start),
+            "value": bots * steps / el, "unit": "env-steps/s", "scaling": "strong", "steps": steps,
+            "ms_per_step": el / steps * 1e3, "eat_passes_per_tick": passes / steps,
+            "exchange": {"collective": "all_gather_into_tensor (%s)" % backend, "bytes_per_rank": info["msg_bytes"],
+                         "avg_ms": ex_ms}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -173,6 +296,9 @@ def main():
                          "the GPU (reported under 'batched', never as 'value'); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pixels", action="store_true", help="skip the pixel-observation side measurement")
+    ap.add_argument("--no-c4", action="store_true", help="skip the tiled single-arena (C4) side measurement")
+    ap.add_argument("--profile-run", action="store_true",
+                    help="only the warm-up and the timed graph replays (for rocprofv3: one call per step)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--policy", default="random", choices=["random", "greedy"],
@@ -182,6 +308,9 @@ def main():
 
     import torch
     rank, world, local = replicas.world_from_env()
+    if args.gpus != world:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE is %d: launch N > 1 ranks with torch.distributed.run "
+                 "(one process per GPU)" % (args.gpus, world))
     dist = None
     # AIGAR_DIST_BACKEND=gloo rehearses the N-rank path with several ranks
     # sharing the GPUs there are (ranks wrap around the visible devices)
@@ -202,23 +331,24 @@ def main():
     stream = torch.cuda.current_stream()
     stp.set_stream(stream.cuda_stream)
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
-    stp.reset(replicas.rank_seed(args.seed, rank))
+    start = start_world(stp, name, replicas.rank_seed(args.seed, rank), arenas)
+    salt = args.seed + 7919 * rank  # replicas of one snapshot diverge through their policy draws
 
     def run(n):  # n whole steps (policy + tick + observation), one graph replayed n times
-        stp.run(n, args.policy, obs, p_split=ps, p_eject=pe, seed=args.seed, greedy_split=True)
+        stp.run(n, args.policy, obs, p_split=ps, p_eject=pe, seed=salt, greedy_split=True)
 
     def one_step():  # the same step as separate calls, each bracketed by HIP events
         if args.policy == "greedy":
             stp.policy_greedy(True)
         else:
-            stp.policy_random(ps, pe, args.seed)
+            stp.policy_random(ps, pe, salt)
         stp.step(1)
         stp.observe(obs)
 
     run(args.warmup)
     torch.cuda.synchronize()
     stp.sync()
-    stats = stp.player_stats()
+    w0 = stp.counters()
     replicas.barrier(dist)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -229,19 +359,73 @@ def main():
     elapsed = t1 - t0
     stp.sync()  # raises on any device-side capacity error
     elapsed = replicas.max_over_ranks(dist, elapsed, device="cuda" if backend == "nccl" else None)
-    # per-phase breakdown and the roofline kernel's duration: the next
-    # min(steps, 50) steps issued as separate calls, HIP events on the stepper's stream
-    stp.profile(True)
-    for _ in range(min(args.steps, 50)):
-        one_step()
-    torch.cuda.synchronize()
-    obs_ms, obs_n = stp.kernel_time("observe")
-    tick_ms, tick_n = stp.kernel_time("tick")
-    pol_ms, pol_n = stp.kernel_time("policy")
-    stp.profile(False)
-    stp.sync()
-    pixels = None
-    if not args.no_pixels:  # RGBGenerator.get_cnn_inputRGB for every bot (side 42, uint8 RGB): a side line,
+    value = replicas.job_throughput(bots * args.steps, world, elapsed)
+    st = stp.get_state()
+    stats = stp.player_stats()
+    work = stp.counters()
+    ticks_timed = max(1, work["ticks"] - w0["ticks"])
+    out = {
+        "metric": "env-steps/sec at 4096 bots x 100k pellets; 1/2/4/8 MI355X scaling",
+        "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (Philox bot population, %s)" % ("reference Greedy bots on the device" if args.policy == "greedy"
+                                                           else "random-action policy"),
+        "config": {"workload": "%s: %s%d bots, %d pellets, %s viruses, %s, field %d, obs %d floats/bot; start: %s" % (
+            name.upper(), "%d arenas x " % arenas if arenas > 1 else "", bots // arenas, int(pellets),
+            "1152" if virus else "no",
+            "greedy bots with ENABLE_GREEDY_SPLIT" if args.policy == "greedy" else "split p=%g, eject p=%g" % (ps, pe),
+            field, stp.obs_len, start),
+                   "policy": args.policy,
+                   "parallelism": "replicas%d" % world if world > 1 else "single-gpu"},
+    }
+    if not args.profile_run:
+        # per-phase breakdown and the roofline kernel's duration: the next
+        # min(steps, 50) steps issued as separate calls, HIP events on the stepper's stream
+        stp.profile(True)
+        for _ in range(min(args.steps, 50)):
+            one_step()
+        torch.cuda.synchronize()
+        obs_ms, obs_n = stp.kernel_time("observe")
+        tick_ms, tick_n = stp.kernel_time("tick")
+        pol_ms, pol_n = stp.kernel_time("policy")
+        stp.profile(False)
+        stp.sync()
+        # roofline of the dominant kernel (k_observe): algorithmic bytes per launch / avg duration
+        alive = int(np.sum(stats[:, 0] > 0))
+        fs = np.nan_to_num(stats[:, 4])
+        area = float(np.mean((fs + 2.0) ** 2))  # FOV box incl. object radii
+        dens_p = st["n_pellets"] / float(field * field * arenas)
+        dens_c = st["n_cells"] / float(field * field * arenas)
+        dens_v = st["n_viruses"] / float(field * field * arenas)
+        ncell = st["n_cells"] / max(1, alive)
+        per_bot = obs_bytes_per_bot(stp.obs_len, dens_p * area, dens_c * area, dens_v * area, n_cells=ncell)
+        reads_bot = per_bot - stp.obs_len * 8 - 2 * 121 * 8  # minus the output row and the history writes
+        obs_bytes_launch = per_bot * alive
+        obs_avg_s = (obs_ms / max(1, obs_n)) / 1e3
+        achieved = obs_bytes_launch / obs_avg_s / 1e9
+        peak = 8000.0
+        traffic, traffic_src = pmc_traffic("k_observe", name)
+        eaten = work["pellets_eaten"] - w0["pellets_eaten"] if "pellets_eaten" in work else 0
+        step_bytes = tick_bytes(st, alive, field, eaten / ticks_timed) * arenas + obs_bytes_launch
+        out["roofline"] = {
+            "bound": "hbm", "kernel": "k_observe", "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
+            "frac": achieved / peak, "traffic": None if traffic is None else int(traffic),
+            "traffic_source": traffic_src, "bytes_per_launch": int(obs_bytes_launch), "avg_launch_ms": obs_avg_s * 1e3,
+            "reads": {"bytes_per_launch": int(reads_bot * alive),
+                      "frac": reads_bot * alive / obs_avg_s / 1e9 / peak},
+            "step": {"bytes_per_step": int(step_bytes), "frac": step_bytes / (elapsed / args.steps) / 1e9 / peak,
+                     "note": "algorithmic bytes of the whole env step (tick + observation) / ms_per_step"}}
+        out["breakdown_ms_per_step"] = {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
+                                        "observe": obs_ms / max(1, obs_n)}
+    out["world"] = {"pellets": st["n_pellets"], "cells": st["n_cells"], "viruses": st["n_viruses"],
+                    "blobs": st["n_blobs"], "alive_bots": int(np.sum(stats[:, 0] > 0)), "tick": int(st["tick"]),
+                    "mean_cell_mass": float(np.asarray(st["cells_f"])[:, 2].mean()) if st["n_cells"] else 0.0,
+                    "multi_cell_players": int(np.sum(np.asarray(st["players_i"])[:, 4] > 1)),
+                    "per_tick_in_timed_region": {k: round((work[k] - w0[k]) / ticks_timed, 3) for k in work
+                                                 if k != "ticks"}}
+    if not args.profile_run and not args.no_pixels:
+        # RGBGenerator.get_cnn_inputRGB for every bot (side 42, uint8 RGB): a side line,
         side, reps = 42, 20  # not part of the env-step metric (the reference's CNN pixel mode is off by default)
         frames = torch.empty((bots, side, side, 3), dtype=torch.uint8, device="cuda")
         stp.observe_pixels(side, 0, out=frames)
@@ -253,65 +437,52 @@ def main():
         stp.profile(False)
         stp.sync()
         pix_s = pix_ms / max(1, pix_n) / 1e3
-        pixels = {"side": side, "dtype": "u8 rgb", "frames_per_s": bots / pix_s, "avg_launch_ms": pix_s * 1e3,
-                  "output_GB_s": bots * side * side * 3 / pix_s / 1e9}
-    st = stp.get_state()
-    work = stp.counters()
-    value = replicas.job_throughput(bots * args.steps, world, elapsed)
-
-    # roofline of the dominant kernel (k_observe): algorithmic bytes per launch / avg duration
-    alive = int(np.sum(stats[:, 0] > 0))
-    fs = np.nan_to_num(stats[:, 4])
-    area = float(np.mean((fs + 2.0) ** 2))  # FOV box incl. object radii
-    dens_p = st["n_pellets"] / float(field * field)
-    dens_c = st["n_cells"] / float(field * field)
-    dens_v = st["n_viruses"] / float(field * field)
-    per_bot = obs_bytes_per_bot(stp.obs_len, dens_p * area, dens_c * area, dens_v * area,
-                                n_cells=st["n_cells"] / max(1, alive))
-    obs_bytes_launch = per_bot * alive
-    obs_avg_s = (obs_ms / max(1, obs_n)) / 1e3
-    achieved = obs_bytes_launch / obs_avg_s / 1e9
-    peak = 8000.0
-    traffic, traffic_src = pmc_traffic("k_observe", name)
-    roofline = {"bound": "hbm", "kernel": "k_observe", "achieved": round(achieved, 2), "peak": peak,
-                "unit": "GB/s", "frac": achieved / peak,
-                "traffic": None if traffic is None else int(traffic),
-                "traffic_source": traffic_src,
-                "bytes_per_launch": int(obs_bytes_launch), "avg_launch_ms": obs_avg_s * 1e3}
-
-    out = {
-        "metric": "env-steps/sec at 4096 bots x 100k pellets; 1/2/4/8 MI355X scaling",
-        "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (Philox bot population, %s)" % ("reference Greedy bots on the device" if args.policy == "greedy"
-                                                           else "random-action policy"),
-        "config": {"workload": "%s: %s%d bots, %d pellets, %s viruses, %s, field %d, obs %d floats/bot" % (
-            name.upper(), "%d arenas x " % arenas if arenas > 1 else "", bots // arenas, int(pellets),
-            "1152" if virus else "no",
-            "greedy bots with ENABLE_GREEDY_SPLIT" if args.policy == "greedy" else "split p=%g, eject p=%g" % (ps, pe),
-            field, stp.obs_len),
-                   "policy": args.policy,
-                   "parallelism": "replicas%d" % world if world > 1 else "single-gpu"},
-        "roofline": roofline,
-        "breakdown_ms_per_step": {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
-                                  "observe": obs_ms / max(1, obs_n)},
-        "world": {"pellets": st["n_pellets"], "cells": st["n_cells"], "viruses": st["n_viruses"],
-                  "blobs": st["n_blobs"], "alive_bots": alive, "tick": int(st["tick"]),
-                  "serial_work_per_tick": {k: round(v / max(1, work["ticks"]), 3) for k, v in work.items()
-                                           if k != "ticks"}},
-    }
-    if pixels is not None:
-        out["pixels"] = pixels
-    if rank == 0 and world == 1 and args.batched_arenas > 1 and not args.arenas:
-        out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (N = 1 only)
+        out["pixels"] = {"side": side, "dtype": "u8 rgb", "frames_per_s": bots / pix_s, "avg_launch_ms": pix_s * 1e3,
+                         "output_GB_s": bots * side * side * 3 / pix_s / 1e9}
+    stp.close()
+    if not args.profile_run and world == 1 and rank == 0:
+        if args.batched_arenas > 1 and not args.arenas:
+            out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
+        if args.policy == "random" and name == "c3":  # the same start with the reference's Greedy bots
+            out["greedy"] = greedy_side(name, args.seed, local)
+    if not args.profile_run and not args.no_c4 and world > 1 and name == "c3":
+        out["c4"] = c4_leg(args, name, rank, world, local, args.seed, dist, backend)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_run:  # (N = 1 only)
         out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget, policy=args.policy)
+        if name == "c3":
+            out["cpu_baseline"]["reference_python"] = REFERENCE_PY_C3
+        if name == "c5":
+            out["cpu_baseline_processes"] = cpu_baseline_c5(args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    stp.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def greedy_side(name, seed, device, steps=30, warmup=5):
+    """Side line: the same matured start stepped with the reference's Greedy bots
+    (bot.py:579-633, ENABLE_GREEDY_SPLIT) on the device: bots converge on food and
+    chase each other, so the serial phases carry real work."""
+    import torch
+    from aigar_amd import _lib
+    stp = _lib.Stepper(make_cfg(name, device=device))
+    stp.set_stream(torch.cuda.current_stream().cuda_stream)
+    start_world(stp, name, seed, 1)
+    bots = WORKLOADS[name][0]
+    obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
+    stp.run(warmup, "greedy", obs, greedy_split=True)
+    torch.cuda.synchronize()
+    w0 = stp.counters()
+    t0 = time.perf_counter()
+    stp.run(steps, "greedy", obs, greedy_split=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stp.sync()
+    w1 = stp.counters()
+    stp.close()
+    n = max(1, w1["ticks"] - w0["ticks"])
+    return {"value": bots * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+            "serial_work_per_tick": {k: round((w1[k] - w0[k]) / n, 3) for k in w1 if k != "ticks"}}
 
 
 if __name__ == "__main__":

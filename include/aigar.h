@@ -96,7 +96,7 @@ typedef struct aigar_config {
   int32_t tile_id;         /* this handle's tile, row-major: ty * tile_x + tx         */
   int32_t tile_halo;       /* pellets held beyond the tile, field units (0 -> 400;    *
                             * at least 140: an owned cell's reach; 370 covers any view) */
-  int32_t tile_cap;        /* records per exchange message (0 -> 4096)                */
+  int32_t tile_cap;        /* records per exchange message (0 -> 2048)                */
   int32_t tile_flags;      /* AIGAR_TILE_*                                            */
 } aigar_config;
 
@@ -294,6 +294,9 @@ int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int cap, int *n);
  */
 int aigar_tile_info(aigar_handle *h, int32_t *info, void **outbox, void **inbox, int64_t *msg_bytes);
 int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox);
+/* bytes of the current pass's message: the first pass of a tick sends the header
+ * and records only (no bitmap); the inbox then holds tile k's at k * these bytes */
+int aigar_tile_msg_bytes(aigar_handle *h, int64_t *bytes);
 int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p);
 int aigar_tile_apply(aigar_handle *h, int *undone);
 int aigar_tile_resume(aigar_handle *h);
@@ -315,7 +318,8 @@ int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *laun
 
 /* Diagnostics: per-arena work counters accumulated since reset/load_state --
  * out[0..n) of: serial work-list entries of virusBlobOverlap, playerVirusOverlap,
- * pellet + blob eating (cells), -, playerPlayerOverlap (players), -, -, ticks.  n <= 8. */
+ * pellet + blob eating (cells), pellets eaten, playerPlayerOverlap (players),
+ * pellets respawned, -, ticks.  n <= 8. */
 int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n);
 
 /* Diagnostics: evaluate the device's pow (aigar_math.h: glibc 2.35's pow, bit

@@ -72,13 +72,13 @@ def test_device_is_deterministic_at_full_size():
 
 @pytest.mark.parametrize("policy", ["synthetic", "greedy"])
 def test_c3_matured_world_matches_oracle(policy):
-    """C3 from the matured tick-300 world (tools/mature.py: cells past 36 and 125,
-    387 multi-cell players): 60 ticks, every event, state and observation.  Split,
+    """C3 from the matured tick-600 world (tools/mature.py: cells past 36 and 125,
+    673 multi-cell players): 60 ticks, every event, state and observation.  Split,
     eject, blob eating, virus explosions, merges and cell-eats-cell all happen at
     full size (field.py:200-253)."""
     cfg = c3()
     g, o = _lib.Stepper(cfg), Oracle(cfg)
-    snap = parity.load_snapshot("c3_t300")
+    snap = parity.load_snapshot("c3_t600")
     g.load_state(snap)
     o.load_state(snap)
     rng = np.random.default_rng(23)

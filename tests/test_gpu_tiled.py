@@ -85,11 +85,11 @@ def c3_config(**kw):
 @pytest.mark.parametrize("tx,ty", [(2, 1), (2, 2)])
 def test_c3_tiled_matches_untiled_oracle(tx, ty):
     """C3 (4096 bots, 100k pellets, 1152 viruses, split p 2.5e-3 / eject p 1e-2)
-    from the matured tick-300 world (cells past 125, multi-cell players), 200 ticks:
+    from the matured tick-600 world (cells past 125, multi-cell players), 200 ticks:
     splits, ejections, blob eating, explosions, merges, cell-eats-cell across the
     tile borders."""
     st = run(c3_config(), tx, ty, 200, 31, synthetic(4096, 4800, 2.5e-3, 1e-2, 31), obs_every=25, check_every=25,
-             start=parity.load_snapshot("c3_t300"))
+             start=parity.load_snapshot("c3_t600"))
     assert st["events"] > 10000
     assert {_abi.EV_CELL_EAT_PELLET, _abi.EV_CELL_EAT_BLOB, _abi.EV_RESPAWN, _abi.EV_MERGE, _abi.EV_EXPLODE,
             _abi.EV_CELL_EAT_CELL, _abi.EV_CELL_EAT_VIRUS} <= st["kinds"], st["kinds"]
@@ -102,7 +102,7 @@ def test_c3_small_halo_forces_cross_tile_passes():
     tile's message, so ticks take several exchange passes; the result must still
     be the untiled world."""
     st = run(c3_config(), 2, 2, 60, 32, synthetic(4096, 4800, 2.5e-3, 1e-2, 32), halo=140, check_every=20,
-             flags=_abi.TILE_OWNED_ONLY, start=parity.load_snapshot("c3_t300"))
+             flags=_abi.TILE_OWNED_ONLY, start=parity.load_snapshot("c3_t600"))
     assert st["events"] > 3000
     assert max(st["passes"]) > 1
 

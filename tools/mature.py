@@ -10,9 +10,9 @@ Greedy policy of the CPU oracle (oracle/oracle.c, Philox stream; the device
 matches it event for event) and saves the state at the requested ticks:
 
   data/c3_t50.npz   the bench's start (the survey's warm distribution)
-  data/c3_t300.npz  a late world (cells past 125, multi-cell players) for parity
+  data/c3_t600.npz  a late world (580 cells past 125, 673 multi-cell players) for parity
 
-usage: python tools/mature.py [ticks...]   (default 50 300)
+usage: python tools/mature.py [ticks...]   (default 50 600)
 """
 import os
 import sys
@@ -42,7 +42,7 @@ def stats(st):
 
 
 def main():
-    want = sorted(int(a) for a in sys.argv[1:]) or [50, 300]
+    want = sorted(int(a) for a in sys.argv[1:]) or [50, 600]
     cfg = make_config(bots=4096, field_size=4800, virus=True, max_pellets=100000.0, channels=C3_CH, extras=0x1F)
     o = Oracle(cfg)
     o.reset(SEED)
