@@ -4,8 +4,10 @@ import csv
 import sys
 
 path = sys.argv[1]
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 110.0
 rows = list(csv.DictReader(open(path)))
+# steps: given, else the number of ticks (k_tick_begin launches) in the trace
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else float(
+    next((r["Calls"] for r in rows if "k_tick_begin" in r["Name"]), 110.0))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print("%-58s %7s %8s %9s %6s" % ("kernel", "calls/s", "avg_us", "us/step", "%"))
 for r in rows:
