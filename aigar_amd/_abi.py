@@ -24,6 +24,14 @@ TILE_OWNED_ONLY = 0x1
 
 
 POLICY_NONE, POLICY_RANDOM, POLICY_GREEDY = 0, 1, 2
+ROLE_NN, ROLE_GREEDY, ROLE_RANDOM = 0, 1, 2
+ROLES = {"NN": ROLE_NN, "Greedy": ROLE_GREEDY, "Random": ROLE_RANDOM}
+
+
+class EnvParams(C.Structure):
+    """aigar_env_params (include/aigar.h): the device Greedy / Random bots of a mixed population."""
+    _fields_ = [("greedy_split", C.c_int32), ("random_skip", C.c_int32), ("random_split", C.c_int32),
+                ("random_eject", C.c_int32), ("salt", C.c_uint64)]
 
 
 class RunParams(C.Structure):

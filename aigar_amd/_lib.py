@@ -80,6 +80,10 @@ def load(build_if_missing=False):
         "aigar_run": [vp, i32, C.POINTER(_abi.RunParams), vp, i32],
         "aigar_env_step": [vp, vp, i32, i32, i32, C.POINTER(_abi.RewardParams), vp, vp, i32],
         "aigar_get_events_raw": [vp, i32, C.POINTER(C.c_int64), i32, C.POINTER(i32)],
+        "aigar_observe_masked": [vp, vp, i32, i32, vp, i32],
+        "aigar_set_roles": [vp, vp, i32],
+        "aigar_env_config": [vp, C.POINTER(_abi.EnvParams)],
+        "aigar_policy_random_bots": [vp],
         "aigar_tile_info": [vp, C.POINTER(C.c_int32), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_int64)],
         "aigar_tile_set_buffers": [vp, vp, vp],
         "aigar_tile_msg_bytes": [vp, C.POINTER(C.c_int64)],
@@ -133,6 +137,9 @@ class Stepper:
         return r
 
     def close(self):
+        if getattr(self, "_one", None) is not None:
+            self._one.close()
+            self._one = None
         if getattr(self, "h", None):
             self.L.aigar_destroy(self.h)
             self.h = None
@@ -240,14 +247,48 @@ class Stepper:
                                                                                  self.cfg.device))
         return d
 
-    def observe(self, out=None, dtype=np.float64):
+    def observe(self, out=None, dtype=np.float64, mask=None):
+        """getStateRepresentation of every player (mask: only where mask != 0; the
+        other rows of out are kept and those bots' history does not advance)."""
         if out is None:
             out = np.zeros((self.NP, self.obs_len), dtype)
         d = self._check_out(out, (self.NP, self.obs_len), ("float64", "float32"), "observe")
         dt = 0 if d == "float64" else 1
         p, dev = _ptr(out)
-        self._chk(self.L.aigar_observe(self.h, p, dt, dev))
+        if mask is None:
+            self._chk(self.L.aigar_observe(self.h, p, dt, dev))
+        else:
+            if isinstance(mask, np.ndarray):
+                mask = np.ascontiguousarray(mask, np.uint8).reshape(self.NP)
+            mp, mdev = _ptr(mask)
+            self._chk(self.L.aigar_observe_masked(self.h, p, dt, dev, mp, mdev))
         return out
+
+    def set_roles(self, roles):
+        """Player roles of a mixed population: AIGAR_ROLE_* codes or "NN" / "Greedy" / "Random"."""
+        r = np.array([_abi.ROLES.get(x, x) if isinstance(x, str) else x for x in roles], np.uint8).reshape(self.NP)
+        self._chk(self.L.aigar_set_roles(self.h, r.ctypes.data_as(C.c_void_p), 0))
+
+    def env_config(self, greedy_split=False, random_skip=7, random_split=False, random_eject=False, salt=0):
+        prm = _abi.EnvParams(int(bool(greedy_split)), int(random_skip), int(bool(random_split)),
+                             int(bool(random_eject)), int(salt))
+        self._chk(self.L.aigar_env_config(self.h, C.byref(prm)))
+
+    def policy_random_bots(self):
+        self._chk(self.L.aigar_policy_random_bots(self.h))
+
+    def reset_arena(self, arena, seed):
+        """Field.reset of ONE arena of a batched handle (a fresh world keyed by seed;
+        that arena's bots reset as by load_state), the others untouched."""
+        if self.A == 1:
+            return self.reset(seed)
+        c = _abi.Config()
+        C.memmove(C.byref(c), C.byref(self.cfg), C.sizeof(_abi.Config))
+        c.n_arenas = 1
+        if getattr(self, "_one", None) is None:
+            self._one = Stepper(c)
+        self._one.reset(seed)
+        self.load_state(self._one.get_state(0), arena)
 
     def observe_pixels(self, side=42, color_seed=0, rgb=True, out=None):
         """RGBGenerator.get_cnn_inputRGB for every player (rgbGenerator.py:95-110):

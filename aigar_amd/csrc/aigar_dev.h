@@ -114,6 +114,8 @@ struct Dev {
   double *p_cmdx, *p_cmdy;
   double *p_fx, *p_fy, *p_fs, *p_mass;  // FOV cache (getFovPos/getFovSize/getTotalMass at tick end)
   int *p_split_lh;       // Greedy bots' splitLikelihood (bot.py:93); <= 0: derived from the Philox key
+  uint8_t *p_role;       // AIGAR_ROLE_*: NN / external actions, Greedy, Random bot (batched populations)
+  int *p_time;           // Random bots' move counter (bot.py:243-249: a new action every FRAME_SKIP_RATE)
   double *o_last_mass;  // NN bots' lastMass (bot.py:229-230); NaN = None
   uint8_t *p_list;  // [16][NP]
   int *p_newc, *p_newb, *p_seqoff, *p_bloboff;

@@ -213,7 +213,7 @@ AIGAR_D int64_t ph_randint(uint64_t u, double lo, double hi) {  // randint(lo, h
 AIGAR_D double u01(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
 enum : uint64_t {
   ST_PELLET = 1, ST_VIRUS = 2, ST_PLAYER = 3, ST_ANGLE = 4, ST_INIT_PLAYER = 5, ST_POLICY = 6, ST_GREEDY = 7,
-  ST_GREEDY_LH = 8
+  ST_GREEDY_LH = 8, ST_REFRANDOM = 9
 };
 
 }  // namespace aigar

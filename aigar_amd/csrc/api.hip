@@ -22,7 +22,10 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v);
 void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first);
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
-void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch);
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch,
+                    const uint8_t *mask = nullptr);
+void launch_policy_refrandom(const Dev &d, hipStream_t s, int skip_rate, int enable_split, int enable_eject,
+                             uint64_t salt);
 int launch_observe_pixels(const Dev &d, hipStream_t s, void *out, int dtype, int side, uint64_t seed, uint8_t *ovf);
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt);
 void launch_player_stats(const Dev &d, hipStream_t s, double *out);
@@ -31,7 +34,7 @@ void launch_apply_actions(const Dev &d, hipStream_t s, const double *act, int n_
                           int record);
 void launch_rewards(const Dev &d, hipStream_t s, double *out, const aigar_reward_params &p, int update_last,
                     int mode);
-void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask);
+void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask, int want = -1);
 void launch_set_commands(const Dev &d, hipStream_t s, const double *cmd);
 }  // namespace aigar
 
@@ -65,6 +68,9 @@ struct aigar_handle {
   int *scr_v = nullptr;
   double *d_cmd = nullptr, *d_stats = nullptr;
   uint8_t *d_mask = nullptr;
+  uint8_t *d_nnmask = nullptr;  // 1 for the players of role NN (the env step's observations)
+  int n_greedy = 0, n_random = 0;  // role counts (aigar_set_roles)
+  aigar_env_params envp{};
   void *d_obs = nullptr;
   void *d_pix = nullptr;  // host-destination staging for aigar_observe_pixels
   uint8_t *d_pix_ovf = nullptr;  // per player: frame left to the pixel kernel's second pass
@@ -94,6 +100,8 @@ struct aigar_handle {
     aigar_reward_params prm;
     double *reward;
     void *obs;
+    aigar_env_params envp;
+    int n_greedy, n_random;
   } env_key{};
 };
 
@@ -306,6 +314,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(ob_used, unsigned long long, 1);
   AL(ob_epoch, uint32_t, 1);
   AL(p_split_lh, int, NP);
+  AL(p_role, uint8_t, NP);
+  AL(p_time, int, NP);
   AL(o_last_mass, double, NP);
   if (d.tiled) {
     AL(outbox, TileRec, h->box_recs);
@@ -321,9 +331,11 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   h->scr_v = dalloc<int>(h, A * d.Wcap);
   h->d_cmd = dalloc<double>(h, NP * 4);
   h->d_mask = dalloc<uint8_t>(h, NP);
+  h->d_nnmask = dalloc<uint8_t>(h, NP);
   h->d_stats = dalloc<double>(h, NP * 5);
   h->d_obs = dalloc<double>(h, NP * (size_t)d.L);
-  ok = ok && h->scr_k && h->scr_v && h->d_cmd && h->d_stats && h->d_obs && h->d_mask;
+  ok = ok && h->scr_k && h->scr_v && h->d_cmd && h->d_stats && h->d_obs && h->d_mask && h->d_nnmask;
+  if (ok) (void)hipMemset(h->d_nnmask, 1, NP);  // every player is NN until aigar_set_roles
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
   if (!ok) {
@@ -380,6 +392,8 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   HIPCHK(hipMemsetAsync(d.vstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.bstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.o_lastfov, 0, sizeof(double) * NP, h->stream));
+  // Bot.reset (bot.py:125-164): currentAction None (NN) / [0, 0, 0, 0] (Greedy, Random)
+  HIPCHK(hipMemsetAsync(d.o_act_cur, 0, sizeof(double) * NP * 4, h->stream));
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
     HIPCHK(hipMemsetAsync(p, 0, sizeof(double) * NP * GG, h->stream));
   launch_reset(d, h->stream, seed);
@@ -472,7 +486,7 @@ static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_para
 #else
   const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
 #endif
-  if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr);
+  if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr, -1);
   launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v, &rp);
   if (out) launch_observe(h->d, s, out, dtype, 0);  // epoch 0: the device-side epoch
 }
@@ -615,14 +629,21 @@ extern "C" int aigar_tile_exchange_local(aigar_handle **hs, int n) {
 // aigar.py:performModelSteps): the action through set_command_point, held for
 // skip + 1 ticks with split/eject dropped on the skipped ones, the rewards of
 // the window summed, then every bot's observation -- one graph replay.
+// Mixed populations (aigar_set_roles): per tick, the NN bots' held action, then
+// the Greedy and Random bots' moves (Model.takeBotActions, model.py:113-115; the
+// moves are independent of each other), then Field.update; the observation is
+// computed for the NN bots only.
 static void launch_env_decision(aigar_handle *h, hipStream_t s, const aigar_handle::EnvKey &k) {
   for (int t = 0; t <= k.skip; t++) {
     if (t > 0) launch_rewards(h->d, s, k.reward, k.prm, 0, t == 1 ? 1 : 2);  // updateRewards (bot.py:166-168)
     launch_apply_actions(h->d, s, k.act, k.n_act, k.enable_split, t > 0, t == 0);
+    if (k.n_greedy) launch_policy_greedy(h->d, s, k.envp.greedy_split, h->d.p_role, AIGAR_ROLE_GREEDY);
+    if (k.n_random)
+      launch_policy_refrandom(h->d, s, k.envp.random_skip, k.envp.random_split, k.envp.random_eject, k.envp.salt);
     launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v);
   }
   launch_rewards(h->d, s, k.reward, k.prm, 1, k.skip == 0 ? 1 : 2);  // end of move_NN (bot.py:220-230)
-  launch_observe(h->d, s, k.obs, k.dtype, 0);
+  launch_observe(h->d, s, k.obs, k.dtype, 0, (k.n_greedy || k.n_random) ? h->d_nnmask : nullptr);
 }
 
 extern "C" int aigar_env_step(aigar_handle *h, const double *act, int n_act, int enable_split, int skip,
@@ -641,6 +662,9 @@ extern "C" int aigar_env_step(aigar_handle *h, const double *act, int n_act, int
   k.prm = *p;
   k.reward = reward_out;
   k.obs = obs_out;
+  k.envp = h->envp;
+  k.n_greedy = h->n_greedy;
+  k.n_random = h->n_random;
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log holds the window's ticks
     hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
   if (!h->use_graph) {
@@ -659,16 +683,67 @@ extern "C" int aigar_env_step(aigar_handle *h, const double *act, int n_act, int
   return 0;
 }
 
+extern "C" int aigar_set_roles(aigar_handle *h, const uint8_t *roles, int on_device) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const int NP = h->d.NP;
+  std::vector<uint8_t> r(NP, AIGAR_ROLE_NN);
+  if (roles) {
+    if (on_device) HIPCHK(hipMemcpy(r.data(), roles, NP, hipMemcpyDeviceToHost));
+    else memcpy(r.data(), roles, NP);
+  }
+  std::vector<uint8_t> nn(NP);
+  int ng = 0, nr = 0;
+  for (int i = 0; i < NP; i++) {
+    if (r[i] > AIGAR_ROLE_RANDOM) return fail("set_roles: role %d of player %d is not an AIGAR_ROLE_*", r[i], i);
+    ng += r[i] == AIGAR_ROLE_GREEDY;
+    nr += r[i] == AIGAR_ROLE_RANDOM;
+    nn[i] = r[i] == AIGAR_ROLE_NN;
+  }
+  HIPCHK(hipMemcpyAsync(h->d.p_role, r.data(), NP, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_nnmask, nn.data(), NP, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->n_greedy = ng;
+  h->n_random = nr;
+  return 0;
+}
+extern "C" int aigar_env_config(aigar_handle *h, const aigar_env_params *p) {
+  if (!h || !p) return fail("null argument");
+  h->envp = *p;
+  return 0;
+}
+extern "C" int aigar_policy_random_bots(aigar_handle *h) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  launch_policy_refrandom(h->d, h->stream, h->envp.random_skip, h->envp.random_split, h->envp.random_eject,
+                          h->envp.salt);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 extern "C" int aigar_obs_len(aigar_handle *h) { return h ? h->d.L : -1; }
 
 extern "C" int aigar_observe(aigar_handle *h, void *out, int dtype, int on_device) {
+  return aigar_observe_masked(h, out, dtype, on_device, nullptr, 0);
+}
+extern "C" int aigar_observe_masked(aigar_handle *h, void *out, int dtype, int on_device, const uint8_t *mask,
+                                    int mask_on_device) {
   if (!h || !out) return fail("null argument");
   if (dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
   HIPCHK(hipSetDevice(h->cfg.device));
   void *dst = on_device ? out : h->d_obs;
+  const uint8_t *m = mask;
+  if (mask && !mask_on_device) {
+    HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)h->d.NP, hipMemcpyHostToDevice, h->stream));
+    m = h->d_mask;
+  }
+  if (!on_device && mask) {  // rows of masked-out bots are left as the caller's buffer has them
+    size_t bytes = (size_t)h->d.NP * h->d.L * (dtype == 0 ? 8 : 4);
+    HIPCHK(hipMemcpyAsync(h->d_obs, out, bytes, hipMemcpyHostToDevice, h->stream));
+  }
   {
-    Mark m(h, "observe");
-    launch_observe(h->d, h->stream, dst, dtype, ++h->obs_calls);
+    Mark mk(h, "observe");
+    launch_observe(h->d, h->stream, dst, dtype, ++h->obs_calls, m);
   }
   HIPCHK(hipGetLastError());
   if (!on_device) {
@@ -1118,6 +1193,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   HIPCHK(hipMemcpyAsync(d.ctl + arena, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
   // bot-side observation history restarts (NN bot reset, bot.py:151-158)
   HIPCHK(hipMemsetAsync(d.o_lastfov + p0, 0, 8 * B, h->stream));
+  HIPCHK(hipMemsetAsync(d.o_act_cur + p0 * 4, 0, 8 * 4 * (size_t)B, h->stream));  // currentAction reset
   hipLaunchKernelGGL(k_fill_d, dim3((B + 255) / 256), dim3(256), 0, h->stream, d.o_last_mass + p0, (size_t)B,
                      __builtin_nan(""));
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
@@ -1137,7 +1213,7 @@ extern "C" int aigar_policy_greedy(aigar_handle *h, int greedy_split, const uint
   }
   {
     Mark mk(h, "policy");
-    launch_policy_greedy(h->d, h->stream, greedy_split ? 1 : 0, m);
+    launch_policy_greedy(h->d, h->stream, greedy_split ? 1 : 0, m, -1);
   }
   HIPCHK(hipGetLastError());
   if (mask && !on_device) HIPCHK(hipStreamSynchronize(h->stream));  // (host mask buffer reused next call)

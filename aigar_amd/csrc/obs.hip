@@ -221,7 +221,7 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 #define OBS_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
 template <typename OutT>
-__global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch) {
+__global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch, const uint8_t *mask) {
   // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
   // masks in creation order (no indirection in the per-square sums)
   __shared__ union {
@@ -243,6 +243,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
 
   const int gp = blockIdx.x, lane = threadIdx.x;
   const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
+  // a masked-out bot does not compute its state this tick: no row, no history update
+  // (the reference's getStateRepresentation runs only for NN bots that are not skipping)
+  if (mask && !mask[gp]) return;
   if (epoch == 0) epoch = *d.ob_epoch;  // graph replay (aigar_run): the tick's closing kernel set it
 #ifdef AIGAR_OBS_TIMING
   __shared__ unsigned long long obs_ts_l[OBS_TS];
@@ -690,9 +693,10 @@ __device__ __forceinline__ double py_round5(double v) {
 // mass/distance^2 candidate, a wave reduction picks the maximum with the
 // reference's tie rule (first in list order: pellets, enemy cells, viruses,
 // each by creation sequence).  mask (optional): which players are Greedy bots.
-__global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, const uint8_t *mask) {
+// mask: NULL = every player; want < 0: players with mask != 0; else mask == want
+__global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, const uint8_t *mask, int want) {
   const int gp = blockIdx.x, lane = threadIdx.x, NP = d.NP, a = gp / d.B, p = gp - a * d.B;
-  if (!d.p_alive[gp] || (mask && !mask[gp])) return;  // makeMove: dead players keep their command
+  if (!d.p_alive[gp] || (mask && (want < 0 ? !mask[gp] : mask[gp] != want))) return;  // (dead players keep their command)
   const ArenaCtl &ctl = d.ctl[a];
   const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
   const int64_t ix = (int64_t)fx, iy = (int64_t)fy;
@@ -789,8 +793,42 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   d.p_split[gp] = split;
   d.p_eject[gp] = eject;
 }
-void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask) {
-  hipLaunchKernelGGL(k_policy_greedy, dim3(d.NP), dim3(64), 0, s, d, greedy_split, mask);
+void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask, int want) {
+  hipLaunchKernelGGL(k_policy_greedy, dim3(d.NP), dim3(64), 0, s, d, greedy_split, mask, want);
+}
+
+// Random bots (bot.py:243-249 make_random_bot_move + makeMove's set_command_point,
+// bot.py:252-269): every FRAME_SKIP_RATE of its moves the bot draws a new action
+// (two uniforms; split / eject uniforms when enabled, else False), and every tick
+// it steers by that action -- split / eject whenever the held value is > 0.5.
+// Draws are Philox-keyed by (player, move counter, salt) instead of numpy's stream.
+__global__ void k_policy_refrandom(Dev d, int skip_rate, int enable_split, int enable_eject, uint64_t salt) {
+  const int gp = GTID;
+  if (gp >= d.NP || d.p_role[gp] != AIGAR_ROLE_RANDOM || !d.p_alive[gp]) return;
+  const int a = gp / d.B;
+  double *cur = d.o_act_cur + (size_t)gp * 4;
+  const int t = d.p_time[gp];
+  if (skip_rate <= 0 || t % skip_rate == 0) {
+    uint64_t u[4];
+    philox((uint64_t)gp, ST_REFRANDOM, (uint64_t)t, salt, d.ctl[a].key0, d.ctl[a].key1, u);
+    cur[0] = u01(u[0]);
+    cur[1] = u01(u[1]);
+    cur[2] = enable_split ? u01(u[2]) : 0.0;
+    cur[3] = enable_eject ? u01(u[3]) : 0.0;
+  }
+  d.p_time[gp] = t + 1;
+  const int64_t x = (int64_t)d.p_fx[gp], y = (int64_t)d.p_fy[gp];
+  const double fs = d.p_fs[gp];
+  const int64_t left = x - (int64_t)(fs / 2), top = y - (int64_t)(fs / 2), size = (int64_t)fs;
+  d.p_cmdx[gp] = (double)left + cur[0] * (double)size;
+  d.p_cmdy[gp] = (double)top + cur[1] * (double)size;
+  d.p_split[gp] = cur[2] > 0.5;
+  d.p_eject[gp] = cur[3] > 0.5;
+}
+void launch_policy_refrandom(const Dev &d, hipStream_t s, int skip_rate, int enable_split, int enable_eject,
+                             uint64_t salt) {
+  hipLaunchKernelGGL(k_policy_refrandom, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, skip_rate, enable_split,
+                     enable_eject, salt);
 }
 
 // synthetic bot population: random action in [0,1]^2 through set_command_point
@@ -811,6 +849,7 @@ __global__ void k_policy_random(Dev d, double p_split, double p_eject, uint64_t 
 __global__ void k_apply_actions(Dev d, const double *act, int n_act, int enable_split, int skipping, int record) {
   int gp = GTID;
   if (gp >= d.NP || !d.p_alive[gp]) return;  // makeMove: dead players do not move
+  if (d.p_role[gp] != AIGAR_ROLE_NN) return;  // Greedy / Random bots steer themselves
   const double *ac = act + (size_t)gp * n_act;
   const double a0 = ac[0], a1 = ac[1];
   int split = 0, eject = 0;
@@ -917,9 +956,9 @@ void launch_player_fov(const Dev &d, hipStream_t s) {
 // blends are order-dependent).
 #include "pixels.inc"
 
-void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch) {
-  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch);
-  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch);
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch, const uint8_t *mask) {
+  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
+  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
 }
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt) {
   hipLaunchKernelGGL(k_policy_random, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, ps, pe, salt);

@@ -64,8 +64,11 @@ def obs_masks(parameters):
         return _abi.OBS_PELLET, _abi.EX_FOV | _abi.EX_MASS, 11
     if getattr(parameters, "SIZE_GRID", False):
         raise NotImplementedError("SIZE_GRID observations are not implemented")
-    if getattr(parameters, "CNN_REPR", False):
-        raise NotImplementedError("CNN observations are not implemented (grid view only)")
+    if getattr(parameters, "CNN_REPR", False) and not getattr(parameters, "CNN_P_REPR", False):
+        # bot.py:284: a CNN over getGridStateRepresentation() with CNN_INPUT_DIM_* (42 / 84) squares per side
+        raise NotImplementedError("CNN over the grid view (CNN_REPR without CNN_P_REPR) needs more than 16 grid "
+                                  "squares per side, beyond the device observation; the pixel CNN path "
+                                  "(CNN_P_REPR) is supported")
     ch = 0
     for name, bit in _CHANNEL_FLAGS:
         if getattr(parameters, name, False):
@@ -457,11 +460,26 @@ class Field:
     def getReward(player):
         return player.getTotalMass()
 
-    # observation for the bots: one device call per tick, rows served per bot
-    def _observation(self):
-        if "obs" not in self._cache:
-            self._cache["obs"] = self.stepper.observe()
-        return self._cache["obs"]
+    # observation for the NN bots: getStateRepresentation advances a bot's last-frame
+    # history only when that bot computes its state (bot.py:195-202), so the device
+    # observes exactly the bots asked for (aigar_observe_masked); Model.takeBotActions
+    # asks for all NN bots of a tick in one call
+    def _prefetch_states(self, indices):
+        idx = [i for i in indices if i not in self._cache.get("obs_rows", {})]
+        if not idx:
+            return
+        mask = np.zeros(len(self.players), np.uint8)
+        mask[idx] = 1
+        if "obs_buf" not in self._cache:
+            self._cache["obs_buf"] = np.zeros((len(self.players), self.stepper.obs_len))
+            self._cache["obs_rows"] = {}
+        buf = self.stepper.observe(self._cache["obs_buf"], mask=mask)
+        for i in idx:
+            self._cache["obs_rows"][i] = buf[i].copy()
+
+    def _state_row(self, index):
+        self._prefetch_states([index])
+        return self._cache["obs_rows"][index]
 
     def _greedy_moves(self, mask, greedy_split):
         """make_greedy_bot_move + set_command_point on the device for the masked players;
@@ -498,36 +516,134 @@ class Field:
 class Bot:
     """bot.py:23-710.  Greedy bots move on the device (k_policy_greedy, batched
     over all Greedy bots by Model.takeBotActions); Random bots draw from numpy
-    like the reference; NN bots get their actions from the caller
-    (`currentAction` / `set_command_point`), as the reference's learners supply them."""
+    like the reference; NN bots run the reference's move_NN (bot.py:194-233):
+    cumulative reward over the frame-skip window, frame skipping, the state from
+    the device (grid view, or the pixel frame for CNN_P_REPR), the learner's
+    decideMove(state), the experience tuples."""
 
-    def __init__(self, player, field, bot_type, learningAlg=None, parameters=None):
+    def __init__(self, player, field, bot_type, learningAlg=None, parameters=None, rgbGenerator=None):
         if bot_type not in ("Greedy", "Random", "NN"):
             raise NotImplementedError("bot type %r is not one of Greedy, Random, NN" % bot_type)
         self.player, self.field, self.type = player, field, bot_type
         self.learningAlg = learningAlg
         self.parameters = parameters
+        self.rgbGenerator = rgbGenerator
+        self.gatherExperiences = self._param("GATHER_EXP", True)
+        self.experiences = []
+        self.memories = []
+        self.lastMass = None
+        self.lastReward = None
+        self.lastAction = None
+        self.fovSize = None
+        self.lastFovSize = None
+        self.currentAction = None
+        self.lastPixelGrid = None
         self.time = 0
         self.totalMasses = []
-        self.currentAction = [0, 0, 0, 0] if bot_type == "Random" else None
-        self.lastAction = None
-        self.currentlySkipping = False
         self.reset()
 
     def __repr__(self):
         return "%s bot (%s)" % (self.type, self.player)
 
-    def reset(self):  # bot.py:125-164
+    def _param(self, name, default):
+        return getattr(self.parameters, name, default) if self.parameters is not None else default
+
+    def reset(self):  # bot.py:125-164 (the NN bot's history grids are the device's, cleared by the world reset)
         if self.learningAlg is not None and hasattr(self.learningAlg, "reset"):
             self.learningAlg.reset()
         self.lastMass = None
+        self.oldState = None
+        self.lastMemory = None
+        self.skipFrames = 0
         self.cumulativeReward = 0
         self.lastReward = 0
+        self.rewardAvgOfEpisode = 0
+        self.rewardLenOfEpisode = 0
+        self.currentlySkipping = False
         if self.type == "NN":
+            self.currentActionIdx = None
             self.currentAction = None
+            if len(self.memories) > 0:
+                self.memories[-1][-1] = True
+            self.fovSize = 0
+            self.lastFovSize = 0
+        else:
+            self.currentAction = [0, 0, 0, 0]
+        self.experiences = []
 
-    def _param(self, name, default):
-        return getattr(self.parameters, name, default) if self.parameters is not None else default
+    # ---- NN bots (bot.py:166-233)
+    def getReward(self):  # bot.py:654-667
+        p = self.parameters
+        if getattr(p, "MASS_AS_REWARD", False):
+            if self.player.getIsAlive():
+                return self.player.getTotalMass() - p.REWARD_TERM
+            return p.DEATH_TERM - p.REWARD_TERM
+        if self.lastMass is None:
+            return None
+        if not self.player.getIsAlive():
+            reward = -1 * self.lastMass * p.DEATH_FACTOR + p.DEATH_TERM
+        else:
+            reward = self.player.getTotalMass() - self.lastMass
+        return reward * p.REWARD_SCALE - p.REWARD_TERM
+
+    def updateRewards(self):  # bot.py:166-168
+        self.cumulativeReward += self.getReward() if self.lastMass else 0
+        self.lastReward = self.cumulativeReward
+
+    def updateFrameSkip(self):  # bot.py:171-178
+        if self.skipFrames > 0:
+            self.skipFrames -= 1
+            self.latestTDerror = None
+            if self.player.getIsAlive():
+                return True
+        return False
+
+    def updateValues(self, extraInfo, newAction, newState, newLastMemory=None):  # bot.py:180-192
+        if newLastMemory is not None:
+            self.lastMemory = newLastMemory
+        self.cumulativeReward = 0
+        self.skipFrames = self._param("FRAME_SKIP_RATE", 0)
+        self.oldState = newState
+        self.lastAction = self.currentAction
+        self.currentAction = newAction
+        if str(self.learningAlg) == "Q-learning":
+            self.currentActionIdx = extraInfo
+        else:
+            self.currentRawAction = extraInfo
+
+    def _move_nn_pre(self):  # bot.py:196-199
+        self.currentlySkipping = False
+        if self.learningAlg is None:
+            return
+        if self.currentAction is not None:
+            self.updateRewards()
+            self.currentlySkipping = self.updateFrameSkip()
+
+    def _move_nn_post(self):  # bot.py:201-229
+        if self.learningAlg is None:  # (facade: an NN bot without a learner steers by the
+            return                    #  currentAction its caller sets -- the reference would raise)
+        if self.currentlySkipping:
+            return
+        newState = self.getStateRepresentation()
+        if self.gatherExperiences and self.oldState is not None:
+            self.time += 1
+            action = self.currentActionIdx if getattr(self.learningAlg, "discrete", False) else self.currentAction
+            if str(self.learningAlg) != "Q-learning" and self._param("ALGORITHM", "") == "CACLA":
+                self.experiences.append((self.oldState, action, self.lastReward, newState, self.currentRawAction))
+            else:
+                self.experiences.append((self.oldState, action, self.lastReward, newState, None))
+            self.lastMemory = ([self.oldState], [action], [self.lastReward], [newState], [newState is not None])
+            if self.player.getSelected():
+                print("Reward: ", self.cumulativeReward)
+        if self.player.getIsAlive():
+            extraInfo, new_action = self.learningAlg.decideMove(newState)
+            self.updateValues(extraInfo, new_action, newState)
+        if self.player.getIsAlive():
+            self.lastMass = self.player.getTotalMass()
+
+    def move_NN(self):  # bot.py:194-233
+        self._move_nn_pre()
+        self._move_nn_post()
 
     def make_random_bot_move(self):  # bot.py:243-249
         if self.time % self._param("FRAME_SKIP_RATE", 7) == 0:
@@ -537,8 +653,13 @@ class Bot:
             self.currentAction[3] = np.random.random() if self._param("ENABLE_EJECT", False) else False
         self.time += 1
 
-    def makeMove(self):  # bot.py:252-269
-        self.totalMasses.append(self.player.getTotalMass())
+    def makeMove(self, _prepared=False):  # bot.py:252-269
+        if not _prepared:
+            self.totalMasses.append(self.player.getTotalMass())
+            if self.type == "NN":
+                self._move_nn_pre()
+        if self.type == "NN":
+            self._move_nn_post()
         if not self.player.getIsAlive():
             return
         if self.type == "Greedy":  # one bot at a time (Model.takeBotActions batches them)
@@ -573,10 +694,22 @@ class Bot:
                 split, eject = action[2] > 0.5, action[3] > 0.5
         self.player.setCommands(left + action[0] * size, top + action[1] * size, split, eject)
 
-    def getStateRepresentation(self):  # bot.py:272-299 (grid view, MLP layout)
+    def getStateRepresentation(self):  # bot.py:272-299
         if not self.player.getIsAlive():
             return None
-        row = self.field._observation()[self.player.index]
+        if not self._param("GRID_VIEW_ENABLED", True):
+            raise NotImplementedError("getSimpleStateRepresentation (GRID_VIEW_ENABLED = False) is not implemented")
+        if self._param("CNN_REPR", False):
+            if not self._param("CNN_P_REPR", False):
+                raise NotImplementedError("CNN over the grid view is not implemented (see obs_masks)")
+            rgb_values = self.rgbGenerator.get_cnn_inputRGB(self.player)
+            stateRepr = (rgb_values - 255) / 100  # bot.py:279
+            if self._param("CNN_LAST_GRID", False):
+                # bot.py:281 (lastPixelGrid starts as None: the reference raises here on the first frame)
+                stateRepr = np.concatenate((stateRepr, self.lastPixelGrid), axis=2)
+                self.lastPixelGrid = stateRepr
+            return stateRepr
+        row = self.field._state_row(self.player.index)  # grid view + extras, flattened (bot.py:286-295)
         return row.reshape(1, -1).copy()
 
     def getPlayer(self): return self.player
@@ -584,6 +717,12 @@ class Bot:
     def getLearningAlg(self): return self.learningAlg
     def getCurrentAction(self): return self.currentAction
     def getMassOverTime(self): return self.totalMasses
+    def getLastReward(self): return self.lastReward
+    def getCumulativeReward(self): return self.cumulativeReward
+    def getLastState(self): return self.oldState
+    def getLastMemory(self): return self.lastMemory
+    def getExperiences(self): return self.experiences
+    def getFrameSkipRate(self): return self._param("FRAME_SKIP_RATE", 0)
 
 
 class RGBGenerator:
@@ -644,6 +783,10 @@ class Model:
         self.players, self.bots, self.humans = [], [], []
         self.field = Field(self.virusEnabled, parameters, seed=seed, device=device, **field_kw)
         self.counter = 0
+        # model.py:67-71: the pixel generator exists when the CNN reads pixels
+        self.rgbGenerator = RGBGenerator(self.field, parameters) if (
+            parameters is not None and getattr(parameters, "CNN_REPR", False) and
+            getattr(parameters, "CNN_P_REPR", False)) else None
 
     def createPlayer(self, name):  # model.py:149-152
         p = Player(name)
@@ -653,7 +796,8 @@ class Model:
     def createBot(self, botType, learningAlg=None, parameters=None):  # model.py:154-162
         name = botType + str(len(self.bots))
         p = self.createPlayer(name)
-        bot = Bot(p, self.field, botType, learningAlg, parameters if parameters is not None else self.parameters)
+        bot = Bot(p, self.field, botType, learningAlg, parameters if parameters is not None else self.parameters,
+                  self.rgbGenerator)
         self.addBot(bot)
         return bot
 
@@ -673,16 +817,27 @@ class Model:
         self.counter = 0
 
     def takeBotActions(self):  # model.py:113-115
+        """Every bot's makeMove, in list order for the ones that draw from numpy
+        (Random bots, and learners that may); the world does not change between the
+        moves, so the parts that read it are batched: every Greedy bot's move in one
+        device launch, every NN bot's state in one masked observation."""
+        for bot in self.bots:
+            bot.totalMasses.append(bot.player.getTotalMass())
+            if bot.type == "NN":
+                bot._move_nn_pre()
+        need = [b.player.index for b in self.bots if b.type == "NN" and b.learningAlg is not None and
+                not b.currentlySkipping and b.player.getIsAlive() and not b._param("CNN_REPR", False)]
+        if need:
+            self.field._prefetch_states(need)
         greedy = [b for b in self.bots if b.type == "Greedy"]
-        if greedy:  # every Greedy bot in one device launch (their moves are independent)
+        if greedy:  # (their moves are independent of each other and of the other bots')
             mask = np.zeros(len(self.players), np.uint8)
             for b in greedy:
-                b.totalMasses.append(b.player.getTotalMass())
                 mask[b.player.index] = 1
             self.field._greedy_moves(mask, bool(getattr(self.parameters, "ENABLE_GREEDY_SPLIT", False)))
         for bot in self.bots:
             if bot.type != "Greedy":
-                bot.makeMove()
+                bot.makeMove(_prepared=True)
 
     def resetBots(self):
         for bot in self.bots:

@@ -218,6 +218,10 @@ int aigar_step(aigar_handle *h, int n_ticks);
  * aigar_policy_random(p_split, p_eject, seed);
  * GREEDY is aigar_policy_greedy for every player.  With AIGAR_FLAG_EVENTS the
  * event log holds the events of all n_steps of the call. */
+/* player roles of a batched population (aigar_set_roles) */
+#define AIGAR_ROLE_NN     0  /* actions from the caller (learner): aigar_apply_actions / aigar_env_step */
+#define AIGAR_ROLE_GREEDY 1  /* Greedy bot on the device (bot.py:579-633)                              */
+#define AIGAR_ROLE_RANDOM 2  /* Random bot on the device (bot.py:243-249)                              */
 #define AIGAR_POLICY_NONE   0
 #define AIGAR_POLICY_RANDOM 1
 #define AIGAR_POLICY_GREEDY 2
@@ -235,6 +239,29 @@ int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p, void *obs
  * Updates each bot's last-frame history grids like the reference does. */
 int aigar_obs_len(aigar_handle *h);
 int aigar_observe(aigar_handle *h, void *out, int dtype, int on_device);
+/* The same for the players whose mask byte is non-zero only (mask on the host, or on
+ * the device when mask_on_device): the others' rows stay as they are in out and
+ * their last-frame history does not advance -- the reference computes a state only
+ * for the NN bots that are not skipping a frame (bot.py:195-202). */
+int aigar_observe_masked(aigar_handle *h, void *out, int dtype, int on_device, const uint8_t *mask,
+                         int mask_on_device);
+
+/* Mixed populations (aigar.py:767-780: NN bots trained among Greedy and Random
+ * bots): roles[A*B] of AIGAR_ROLE_* (NULL: every player NN).  aigar_env_step then
+ * moves the Greedy and Random bots itself every tick (the learner's actions apply to
+ * the NN players only) and observes the NN players only. */
+int aigar_set_roles(aigar_handle *h, const uint8_t *roles, int on_device);
+typedef struct aigar_env_params {
+  int32_t greedy_split;   /* ENABLE_GREEDY_SPLIT (networkParameters.py:17)            */
+  int32_t random_skip;    /* Random bots draw a new action every FRAME_SKIP_RATE moves */
+  int32_t random_split;   /* ENABLE_SPLIT: Random bots draw a split value             */
+  int32_t random_eject;   /* ENABLE_EJECT: Random bots draw an eject value            */
+  uint64_t salt;          /* Philox salt of the Random bots' draws                    */
+} aigar_env_params;
+int aigar_env_config(aigar_handle *h, const aigar_env_params *p);
+/* One Model.takeBotActions for the Random bots only (make_random_bot_move +
+ * set_command_point, bot.py:243-269), with the aigar_env_config parameters. */
+int aigar_policy_random_bots(aigar_handle *h);
 /* RGBGenerator.get_cnn_inputRGB (rgbGenerator.py:95-110) for every player: a
  * side x side frame (side <= 84; CNN_INPUT_DIM_* of networkParameters.py) of
  * the player's FOV, objects drawn in stable mass order with SDL_gfx circle

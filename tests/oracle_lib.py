@@ -42,6 +42,7 @@ def lib():
         L.oracle_step.argtypes = [vp, C.c_int]
         L.oracle_observe.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_obs_len.argtypes = [vp]
+        L.oracle_observe_one.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
         L.oracle_pixels.argtypes = [vp, C.c_int, C.c_uint64, C.POINTER(C.c_uint8)]
         L.oracle_player_stats.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_get_events.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.c_int]
@@ -136,6 +137,12 @@ class Oracle:
     def observe(self):
         out = np.zeros((self.n_total, self.obs_len), np.float64)
         self._chk(self.L.oracle_observe(self.h, _dp(out)))
+        return out
+
+    def observe_one(self, player, arena=0):
+        """One bot's getStateRepresentation (its last-frame history advances, no other's)."""
+        out = np.zeros(self.obs_len, np.float64)
+        self._chk(self.L.oracle_observe_one(self.h, arena, player, _dp(out)))
         return out
 
     def pixels(self, side=42, color_seed=0):
