@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "k_observe|k_scan_lb|k_pgrid|k_food" --output-format csv \
-    -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --steps 30 --warmup 10 --no-cpu-baseline --batched-arenas 0 "$@" \
+    -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --profile-run --steps 30 --warmup 10 "$@" \
     > $R/gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "pmc $C failed rc=$?"; exit 1; }
 done
 echo done
