@@ -83,6 +83,17 @@ def obs_masks(parameters):
     return ch, ex, int(getattr(parameters, "GRID_SQUARES_PER_FOV", 11))
 
 
+def reference_parameters():
+    """The reference's networkParameters module when its code is loaded in this
+    process (model.py imports it, then builds Field(virusEnabled) without passing
+    it), else None (the single-NN-bot defaults of obs_masks)."""
+    import sys
+    for name, mod in list(sys.modules.items()):
+        if name.split(".")[-1] == "networkParameters" and hasattr(mod, "GRID_SQUARES_PER_FOV"):
+            return mod
+    return None
+
+
 def _mix(v):
     """splitmix64 finaliser: the hash behind the (deterministic) colours."""
     v = (v + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
@@ -306,6 +317,8 @@ class Field:
         self.players.append(player)
 
     def _config(self):
+        if self.parameters is None:  # the reference's model.py builds Field(virusEnabled) without them
+            self.parameters = reference_parameters()
         ch, ex, g = obs_masks(self.parameters)
         if not self.virusEnabled:
             ch &= ~_abi.OBS_VIRUS
