@@ -138,10 +138,15 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   if (gi >= kMaxCells * NP) return;
   const int gp = gi % NP;
   const size_t ci = (size_t)gi;
+  const bool live = d.c_flags[ci] & F_ALIVE;
+  if (!d.p_alive[gp] || (!live && !(rp.on && gi < NP))) return;  // (dead players keep their command: makeMove)
+  // every load of the cell up front, before any store: one memory round trip,
+  // not one per store the compiler cannot prove disjoint
+  double m = d.c_m[ci], r = d.c_r[ci], svx = d.c_svx[ci], svy = d.c_svy[ci], mt = d.c_mt[ci];
+  const double x = d.c_x[ci], y = d.c_y[ci];
+  int svc = d.c_svc[ci];
   double cmdx, cmdy;
   if (rp.on) {
-    const bool live = d.c_flags[ci] & F_ALIVE;
-    if ((!live && gi >= NP) || !d.p_alive[gp]) return;  // (dead players keep their command: makeMove)
     const Command c = random_command(d, gp, rp);  // (the player's live cells and slot 0 only)
     if (gi < NP) {  // slot 0 stores the player's command
       d.p_cmdx[gp] = c.x;
@@ -153,27 +158,22 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
     cmdx = c.x;
     cmdy = c.y;
   } else {
-    if (!(d.c_flags[ci] & F_ALIVE) || !d.p_alive[gp]) return;
     cmdx = d.p_cmdx[gp];
     cmdy = d.p_cmdy[gp];
   }
-  double m = d.c_m[ci], r = d.c_r[ci];
   if (m >= 4) {  // Cell.decayMass (cell.py:123-126)
     m = m * kDecay;
     r = radius_of(m);
     d.c_m[ci] = m;
     d.c_r[ci] = r;
   }
-  int svc = d.c_svc[ci];
-  double svx = d.c_svx[ci], svy = d.c_svy[ci];
   update_momentum(svc, svx, svy);
   d.c_svc[ci] = svc;
   d.c_svx[ci] = svx;
   d.c_svy[ci] = svy;
-  double mt = d.c_mt[ci];
   if (mt > 0) d.c_mt[ci] = mt - 1;
   double vx, vy;
-  set_move_direction(d.c_x[ci], d.c_y[ci], m, r, cmdx, cmdy, vx, vy);
+  set_move_direction(x, y, m, r, cmdx, cmdy, vx, vy);
   d.c_vx[ci] = vx;
   d.c_vy[ci] = vy;
 }

@@ -2,7 +2,9 @@
 // precision (libquadmath, 113 bits) value rounded to double, on inputs shaped
 // like the stepper's (move directions from coordinate differences, split
 // angles in [-pi, pi], explosion angles deg2rad(0..359)).  Also reports how
-// often glibc differs from that rounding.  Prints "mismatches=<n>" for ours.
+// often glibc differs from that rounding.  Adversarial sets too: arguments at
+// the j/64 table seams, next to multiples of pi/2, ratios at the seams, and
+// huge / tiny / subnormal atan2 operands.  Prints "mismatches=<n>" for ours.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,6 +46,21 @@ int main(int argc, char **argv) {
   const double edge[] = {0.0, -0.0, 1.0, -1.0, 1e-300, -1e-300, 5e-324, 1000.0, -1000.0};
   for (double y : edge)
     for (double x : edge) check_at(y, x);
+  std::uniform_real_distribution<double> unit(-1.0, 1.0);
+  for (long i = 0; i < n / 8; i++) {
+    const int j = (int)(i % 52), k = (int)(i % 6) - 1;
+    const double e = unit(rng) * 0x1p-9;
+    check_sc(j / 64.0 + 1 / 128.0 + e * 0x1p-20);  // the seam between table rows
+    check_sc(k * 1.5707963267948966 + e);           // near k pi/2
+    check_sc(k * 1.5707963267948966 + j / 64.0 + e);
+    const double den = coord(rng);
+    check_at((j / 64.0 + 1 / 128.0 + e * 0x1p-20) * den, den);  // ratio at a seam
+    check_at(den, (j / 64.0 + e) * den);
+    check_at(ldexp(unit(rng), -1060), ldexp(unit(rng), -1050));  // subnormal operands
+    check_at(ldexp(unit(rng), 1020), ldexp(unit(rng), 1023));    // near overflow
+    check_at(ldexp(unit(rng), -700), ldexp(unit(rng), 300));     // tiny ratio
+    check_at(ldexp(unit(rng), 200), ldexp(unit(rng), -950));
+  }
   for (long i = 0; i < n; i++) {
     check_at(coord(rng), coord(rng));
     check_at(small(rng), coord(rng));
