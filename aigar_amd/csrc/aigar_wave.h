@@ -9,6 +9,22 @@
 
 namespace aigar {
 
+// a wave-uniform value moved to SGPRs (the compiler keeps a uniform value that
+// came from a vector load in VGPRs; in a register-bound kernel that costs waves)
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni(int64_t v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double uni(double v) { return __longlong_as_double(uni((int64_t)__double_as_longlong(v))); }
+__device__ __forceinline__ Rect uni(Rect r) {
+  r.x0 = uni(r.x0);
+  r.x1 = uni(r.x1);
+  r.y0 = uni(r.y0);
+  r.y1 = uni(r.y1);
+  return r;
+}
+
 __device__ __forceinline__ void atomic_max_pos(double *addr, double v) {  // v >= 0
   atomicMax((unsigned long long *)addr, (unsigned long long)__double_as_longlong(v));
 }

@@ -195,7 +195,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   aigar_handle *h = new aigar_handle();
   h->cfg = *cfg;
   if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
-  if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(1, std::min(16, atoi(r)));  // tuning knob
+  // tuning knob; >= 2: the player-cell grid counts ride on round 1, its scatter on round 2
+  if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(2, std::min(16, atoi(r)));
   Dev &d = h->d;
   d.A = cfg->n_arenas;
   d.B = cfg->bots_per_arena;

@@ -32,7 +32,65 @@ namespace aigar {
 
 #define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
 
+// Diagnostics build only (-DAIGAR_PHASE_TIMING, tools/phase_timing.py): per
+// wave, its start time (slot 0, low 32 bits of the 100 MHz wall clock) and the
+// time from its start to each mark, after its outstanding loads have landed
+// (plain stores to the wave's own slots: no contention).  The product build
+// compiles these to nothing.
+#ifdef AIGAR_PHASE_TIMING
+constexpr int kPtWaves = 8192;
+__device__ unsigned int g_ptw[8][kPtWaves][8];
+__device__ unsigned int g_ptid[8][kPtWaves][2];  // HW_ID, XCC_ID of the wave
+__device__ __forceinline__ void pt_ids(unsigned *o) {
+  unsigned a, b;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(a));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(b));
+  o[0] = a;
+  o[1] = b;
+}
+#define PT_BEGIN(PT_K)                                                                              \
+  const unsigned long long pt0_ = wall_clock64();                                                   \
+  const int pt_w_ = (blockIdx.x + blockIdx.y * gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+  if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) {                                                \
+    g_ptw[PT_K][pt_w_][0] = (unsigned)pt0_;                                                         \
+    pt_ids(g_ptid[PT_K][pt_w_]);                                                                    \
+  }
+#define PT_MARK(k, m)                                                                               \
+  do {                                                                                              \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                     \
+    if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[k][pt_w_][m] = (unsigned)(wall_clock64() - pt0_); \
+  } while (0)
+#else
+#define PT_BEGIN(k)
+#define PT_MARK(k, m)
+#endif
+
 __device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { atomicOr(&d.ctl[a].err, bit); }
+
+// Last-block ticket (cdna_hip_programming.md, the in-launch reduction recipe):
+// each of the nblocks participating blocks publishes its writes (every wave's
+// stores drained, one agent-scope release) and takes a ticket; the block that
+// draws the last one returns true in all its threads and, after its acquire,
+// sees every participant's writes.  The last block resets the counter, so it is
+// 0 between launches (dalloc zeroes it).  Correct for any block placement.
+__device__ bool last_block(int *ticket, int nblocks) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == nblocks - 1;
+    if (t == nblocks - 1) {
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return s_last;
+}
 
 __device__ __forceinline__ void tile_out(const Dev &d, int32_t kind, int32_t idx, int64_t seq, double x, double y) {
   const int i = atomicAdd(&d.ctl[0].n_out, 1);
@@ -315,9 +373,11 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
 // updateViruses + updateBlobs + the per-cell part of updatePlayers in one
 // launch: thread ranges [cell slots | viruses | blobs] (independent, field.py:94-119)
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
+  PT_BEGIN(2);
   int gi = GTID;
   if (gi < kMaxCells * d.NP) {
     update_cell(d, gi, rp);
+    PT_MARK(2, 1);
     return;
   }
   gi -= kMaxCells * d.NP;
@@ -407,6 +467,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
   __shared__ int s_ps, s_pb, s_ts, s_tb, s_blob0;
   __shared__ int64_t s_seq0;
   __shared__ uint32_t s_epoch;
+  PT_BEGIN(1);
   const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ntiles = gridDim.x, NP = d.NP;
   ArenaCtl &c = d.ctl[a];
@@ -427,6 +488,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     nn = d.p_newc[gp];
     nb = d.p_newb[gp];
   }
+  PT_MARK(1, 1);
   const int vs = nn + nb, vb = nb;
   int is = vs, ib = vb;
 #pragma unroll
@@ -502,6 +564,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     }
   }
   __syncthreads();
+  PT_MARK(1, 2);
   const int64_t seq0 = s_seq0;
   const int blob0 = s_blob0;
   if (tile == ntiles - 1 && tid == 0) {  // arena totals are known: advance the bases
@@ -544,6 +607,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
       d.b_flags[g] = F_ALIVE;
     }
   }
+  PT_MARK(1, 3);
   if (tid == 0 && atomicAdd(&c.pl_ticket, 1) == ntiles - 1) {  // last block of the arena bumps the epoch
     c.pl_ticket = 0;
     __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -655,9 +719,10 @@ __device__ __forceinline__ int cgrid_bucket(const Dev &d, double x, double y) {
 __device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int parity) {
   return d.cgcnt + ((size_t)a * 2 + parity) * CG_STRIDE;
 }
-// block bodies; they run as extra blocks of the food-phase kernels (k_food_prep,
-// k_food_commit round 1): eating changes masses and radii, never positions, and
-// the player-cell grid is first read by playerPlayerOverlap
+// block bodies, run as extra blocks of k_food_commit rounds 1 (counts) and 2
+// (scatter): eating changes masses and radii, never positions (a radius read
+// while its cell eats still bounds the grid: the eating cell reports its grown
+// radius itself), and the player-cell grid is first read by playerPlayerOverlap
 __device__ __forceinline__ int cgrid_blocks(const Dev &d) {  // per arena, count and scatter alike
   const int cc = cgrid_cols(d);
   return (int)((std::max((long)kMaxCells * d.B, (long)cc * cc + 1) + 255) / 256);
@@ -1085,9 +1150,11 @@ __device__ __forceinline__ void vb_active(const Dev &d, int gi) {
     else set_err(d, a, ERR_WORK_CAP);
   }
 }
-__global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
-  int a = blockIdx.x;
-  if (threadIdx.x != 0) return;
+// the serial passes are device bodies run by one wavefront per arena: as their
+// own launches (k_*_serial) or in the tail / head of a neighbouring kernel
+// (launch_tick: fold), which saves a dependent launch per idle pass
+__device__ void vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
+  if ((threadIdx.x & 63) != 0) return;
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
@@ -1174,10 +1241,13 @@ __global__ void k_vb_serial(Dev d, int64_t *scr_k, int *scr_v) {
 
 // mergePlayerCells (per player) and the virus<-blob activity test (per virus)
 // in one launch: merging touches only player cells, the test only viruses/blobs
-__global__ void __launch_bounds__(256) k_merge_vb(Dev d) {
-  int gi = GTID;
-  if (gi < d.NP) return merge_player(d, gi);
-  if (d.virus_enabled) vb_active(d, gi - d.NP);
+// fold: virusBlobOverlap's serial pass runs in the last block (one wave per arena)
+__global__ void __launch_bounds__(256) k_merge_vb(Dev d, int64_t *scr_k, int *scr_v, int fold) {
+  const int gi = GTID;
+  if (gi < d.NP) merge_player(d, gi);
+  else if (d.virus_enabled) vb_active(d, gi - d.NP);
+  if (fold && last_block(d.ticket + 0, gridDim.x))
+    for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) vb_serial_body(d, a, scr_k, scr_v);
 }
 
 // ------------------------------------------------------------ T12 cell <- virus
@@ -1253,9 +1323,8 @@ __global__ void __launch_bounds__(256) k_pv_active(Dev d) {
     else set_err(d, a, ERR_WORK_CAP);
   }
 }
-__global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
-  int a = blockIdx.x;
-  if (threadIdx.x != 0) return;
+__device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
+  if ((threadIdx.x & 63) != 0) return;
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
@@ -1358,6 +1427,9 @@ __global__ void k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
     for (int k = 0; k < d.p_ncells[gp]; k++) d.c_flags[(size_t)d.p_list[k * NP + gp] * NP + gp] &= ~F_NEW;
   }
 }
+__global__ void __launch_bounds__(64) k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
+  pv_serial_body(d, blockIdx.x, scr_k, scr_v);
+}
 
 // ------------------------------------------------------------ T14/T15 food
 // playerPelletOverlap then playerBlobOverlap (field.py:200-222) as ONE
@@ -1454,16 +1526,12 @@ constexpr int PREP_WAVES = 1;  // wavefronts per player (wave h takes cells h, h
 // pass once the owners' outcomes arrived).  Cells that cannot touch a held food
 // are skipped.  resume: only cells not yet final (f_done != 1) are prepared.
 __device__ __forceinline__ double tile_rall() { return sqrt(kMaxMass / kPi) * (1 + 1e-9); }  // any cell's radius bound
-__global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume) {
-  const int nprep = (d.NP * PREP_WAVES + 3) / 4;
-  if ((int)blockIdx.x >= nprep) {  // extra blocks: player-cell grid counts
-    const int e = blockIdx.x - nprep, nb = cgrid_blocks(d);
-    return cgrid_count_block(d, e / nb, e % nb);
-  }
+__global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int resume) {
   __shared__ int64_t s_seq[4][PREP_CAND];
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
   __shared__ int s_idx[4][PREP_CAND];
   __shared__ uint8_t s_sel[4][PREP_CAND];
+  PT_BEGIN(0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wi = blockIdx.x * 4 + w, gp = wi / PREP_WAVES, h = wi - gp * PREP_WAVES;
   if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
@@ -1471,14 +1539,16 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   Food F(d, a);
   const uint32_t base = d.ctl[a].food_round;
-  int n = d.p_ncells[gp];
+  int n = uni(d.p_ncells[gp]);  // (wave-uniform values kept in SGPRs: 4 waves per SIMD fit in 128 VGPRs)
+  PT_MARK(0, 1);
   for (int k = h; k < n; k += PREP_WAVES) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    size_t ci = (size_t)uni((int)d.p_list[k * NP + gp]) * NP + gp;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
     if (resume && d.f_done[ci] == 1) continue;  // final (here or by its owner's message)
-    double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
-    int64_t cseq = d.c_seq[ci];
-    Rect q = footprint(x, y, r, d.size);
+    double x = uni(d.c_x[ci]), y = uni(d.c_y[ci]), m = uni(d.c_m[ci]), r = uni(d.c_r[ci]);
+    int64_t cseq = uni(d.c_seq[ci]);
+    PT_MARK(0, 2);
+    Rect q = uni(footprint(x, y, r, d.size));
     if (d.tiled && !tile_near_rect(d, rect_grow(footprint(x, y, fmax(r, tile_rall()), d.size), 1, d.cols), 2)) {
       if (lane == 0) {  // cannot compete for any held food: its owner decides it
         d.f_cnt[ci] = 0;
@@ -1512,11 +1582,12 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume
       cnt += __popcll(bal);
     };
     F.walk_pellets(q, visit);
+    PT_MARK(0, 3);
     // The blob turn's candidates are the blobs hashed in the buckets of the
     // cell's box AFTER its pellet turn (field.py:215-222): walk the box of the
     // largest radius the pellets can give (the eat loop applies the exact box).
     const double Rp = fmax(r, radius_of(py_min(kMaxMass, (m + wave_sum(lsum)) * (1 + 1e-9))) * (1 + 1e-9));
-    const Rect qb = footprint(x, y, Rp, d.size);
+    const Rect qb = uni(footprint(x, y, Rp, d.size));
     auto visit_b = [&](bool valid, int j) {  // as visit, against the blob-turn box bound
       bool keep = false;
       double fx = 0, fy = 0, fm = 0;
@@ -1541,11 +1612,12 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume
       cnt += __popcll(bal);
     };
     F.walk_blobs(qb, visit_b);
+    PT_MARK(0, 4);
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
     double sum = wave_sum(lsum);
-    double M = py_min(kMaxMass, (m + sum) * (1 + 1e-9));
-    double Rm = fmax(r, radius_of(M)) * (1 + 1e-9);
+    double M = uni(py_min(kMaxMass, (m + sum) * (1 + 1e-9)));
+    double Rm = uni(fmax(r, radius_of(M)) * (1 + 1e-9));
     wave_sync_lds();
     if (d.tiled && (!(tile_holds_rect(d, rect_grow(q, 1, d.cols)) && tile_holds_rect(d, rect_grow(qb, 1, d.cols))) ||
                     ((d.tile_flags & AIGAR_TILE_OWNED_ONLY) && !tile_owns(d, x, y)))) {
@@ -1581,6 +1653,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume
       ovf = nsel > FCAP;
     }
     wave_sync_lds();
+    PT_MARK(0, 5);
     if (ovf) {  // reserve everything the cell may touch, resolved serially in priority order
       uint64_t key = food_key(base + rounds + 1, prio);
       if (lane == 0) {
@@ -1621,6 +1694,7 @@ __global__ void __launch_bounds__(256) k_food_prep(Dev d, int rounds, int resume
       d.f_done[ci] = (nsel == 0);
     }
     wave_sync_lds();
+    PT_MARK(0, 6);
   }
 }
 // one eaten food: the event (in its reference phase), kill, growth
@@ -1718,26 +1792,35 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last) 
   }
   return rgrow;
 }
-__global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last) {
+__device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, int rounds);
+// fold (last round only): the serial pass runs in the last of the player blocks
+// (wave 0, arena after arena; the grid's extra blocks do not take part)
+__global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last, int64_t *scr_k, int *scr_v,
+                                                     int rounds, int fold) {
   const int ncommit = (d.NP + 255) / 256;
-  if ((int)blockIdx.x >= ncommit) {  // extra blocks (round 1): player-cell grid scatter
+  if ((int)blockIdx.x >= ncommit) {  // extra blocks: player-cell grid counts (round 1), scatter (round 2)
     const int e = blockIdx.x - ncommit, nb = cgrid_blocks(d);
+    if (round == 1) return cgrid_count_block(d, e / nb, e % nb);
     return cgrid_scatter_block(d, e / nb, e % nb);
   }
+  PT_BEGIN(4);
   const int gp = GTID;
   const double rg = gp < d.NP ? food_commit_player(d, gp, round, last) : 0.0;
+  PT_MARK(4, round < 7 ? round : 7);
   wave_atomic_max_pos(&d.ctl[min(gp, d.NP - 1) / d.B].rmax_cell, rg);
+  if (fold && last_block(d.ticket + 1, ncommit) && threadIdx.x < 64)
+    for (int a = 0; a < d.A; a++) food_serial_body(d, a, scr_k, scr_v, rounds);
 }
 // Cells the reservation rounds could not settle, in priority order (player,
 // list position), one wavefront per arena.  The sequential eat loop runs on
 // all lanes uniformly; each cell's candidates are gathered lane-parallel with
 // their state into LDS (within one cell's turn only that cell changes them).
 constexpr int FS_CAP = 512;
-__global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
+__device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, int rounds) {
   __shared__ int64_t s_key[FS_CAP];
   __shared__ int s_val[FS_CAP], s_srt[FS_CAP];
   __shared__ double s_x[FS_CAP], s_y[FS_CAP], s_m[FS_CAP], s_r[FS_CAP];
-  const int a = blockIdx.x, lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   ArenaCtl &c = d.ctl[a];
   const int nw = min(c.n_pend, d.Wcap);
   const uint32_t excl_round = c.food_round + rounds + 2;  // tiles: excluded / tainted keys (k_food_prep)
@@ -1882,12 +1965,16 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
     wave_fence();  // kills and the new mass are read by the next cell's gather
   }
 }
+__global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
+  food_serial_body(d, blockIdx.x, scr_k, scr_v, rounds);
+}
 
 // ------------------------------------------------------------ T16 player <- player
 __device__ __forceinline__ Rect cell_rect(const Dev &d, size_t ci) { return footprint(d.c_x[ci], d.c_y[ci], d.c_r[ci], d.size); }
 
 // one wavefront per player: cells with an overlapping enemy cell at phase start
 __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
+  PT_BEGIN(3);
   const int lane = threadIdx.x & 63;
   const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gp >= d.NP || !d.p_alive[gp]) return;
@@ -1897,9 +1984,11 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   int E = expand_for(d.ctl[a].rmax_cell);
   int n = d.p_ncells[gp];
   bool anyp = false;
+  PT_MARK(3, 1);
   for (int k = 0; k < n; k++) {
     size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    PT_MARK(3, 2);
     Rect q = footprint(x, y, r, d.size);
     bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int e) {
       // only the LOWER-index player of a pair is marked: its turn comes first
@@ -1915,6 +2004,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
     }, d.cshift_c);
     if (lane == 0) d.c_active[ci] = any;
     anyp |= any;
+    PT_MARK(3, 3);
   }
   if (anyp && lane == 0) {
     int w = atomicAdd(&d.ctl[a].n_pend, 1);
@@ -1962,14 +2052,14 @@ __device__ __forceinline__ void active_st(const Dev &d, size_t i, uint8_t v) {
 // (candidate gathering, re-activation after growth) are spread over the lanes.
 // Cross-lane data: the LDS candidate lists, the pending bitmap and c_active.
 constexpr int PP_LCAP = 512;
-__global__ void __launch_bounds__(64) k_pp_serial(Dev d, int64_t *scr_k, int *scr_v) {
-  extern __shared__ uint32_t pend[];  // pending-player bitmap (B bits)
+__device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend) {
+  // pend: pending-player bitmap (B bits, LDS)
   // candidates of the current turn, with their state at turn start (only the
   // turn's own cell changes them: what it eats dies, and it stops when eaten)
   __shared__ int64_t s_key[PP_LCAP];
   __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
   __shared__ double s_x[PP_LCAP], s_y[PP_LCAP], s_m[PP_LCAP], s_r[PP_LCAP];
-  const int a = blockIdx.x, lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   ArenaCtl &c = d.ctl[a];
   const int B = d.B, NW = (B + 31) / 32;
   const int nw = min(c.n_pend, d.Wcap);
@@ -2177,11 +2267,18 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
 
 __device__ void spawn_counts(const Dev &d, int a, int init);
 constexpr int OCC_LDS = 4096;  // occupancy words kept in LDS (32 KiB: fields up to 10240 units)
-__global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init) {
+// pp (tick only): playerPlayerOverlap's serial pass first, by wave 0 of the
+// arena's block (its pending bitmap in the dynamic LDS)
+__global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *scr_k, int *scr_v, int pp) {
   __shared__ int sflag[1024];
   __shared__ int gcnt[SG_CAP + 1];
   __shared__ unsigned long long s_occ[OCC_LDS];
   int a = blockIdx.x;
+  if (pp) {
+    extern __shared__ uint32_t pend[];
+    if (threadIdx.x < 64) pp_serial_body(d, a, scr_k, scr_v, pend);
+    __syncthreads();
+  }
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
   // order-preserving compaction of viruses and blobs (list order == creation order),
@@ -2495,20 +2592,23 @@ void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
 }
 
 
-// playerPelletOverlap + playerBlobOverlap: prep, reservation rounds, serial rest;
-// the player-cell grid (counts, scatter) rides along as extra blocks of the
-// prep and of the first round
+// playerPelletOverlap + playerBlobOverlap: prep, reservation rounds (>= 2),
+// serial rest; the player-cell grid rides along as extra blocks of rounds 1
+// (counts) and 2 (scatter).  (As extra blocks of the prep they made a fifth
+// block per CU beside its four, which waited for a free slot: ~+10 us.)
 // (resume: a further eat pass of a tiled tick -- the cell grid is built already)
-static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr, int resume = 0) {
+static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr, int resume = 0, int fold = 0) {
+  rounds = std::max(rounds, 2);  // (the cell grid's scatter rides on round 2)
   const int g = nblk(d.NP, 256);
   const long per = (long)kMaxCells * d.B;
   const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
   const int ncg = resume ? 0 : nblk(std::max(per, (long)cc * cc + 1), 256) * d.A;
-  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4) + ncg), dim3(256), 0, s, d, rounds, resume);
+  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4)), dim3(256), 0, s, d, rounds, resume);
   for (int r = 1; r <= rounds; r++) {
-    hipLaunchKernelGGL(k_food_commit, dim3(g + (r == 1 ? ncg : 0)), dim3(256), 0, s, d, r, r == rounds ? 1 : 0);
+    hipLaunchKernelGGL(k_food_commit, dim3(g + (r <= 2 ? ncg : 0)), dim3(256), 0, s, d, r, r == rounds ? 1 : 0, scr.k,
+                       scr.v, rounds, fold && r == rounds ? 1 : 0);
   }
-  hipLaunchKernelGGL(k_food_serial, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
+  if (!fold) hipLaunchKernelGGL(k_food_serial, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
 }
 
 void launch_player_fov(const Dev &d, hipStream_t s);
@@ -2523,9 +2623,8 @@ void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, co
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
-                     dim3(256), 0, s, d);
+                     dim3(256), 0, s, d, scr_k, scr_v, d.virus_enabled ? 1 : 0);  // + virusBlobOverlap's serial pass
   if (d.virus_enabled) {
-    hipLaunchKernelGGL(k_vb_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
     hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
   }
@@ -2533,8 +2632,9 @@ void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, co
 // the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_pp_serial, dim3(d.A), dim3(64), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, scr_k, scr_v);
-  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 0);  // + end-of-tick virus grid
+  // playerPlayerOverlap's serial pass + spawnStuff's plan + the end-of-tick virus grid
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, 0, scr_k,
+                     scr_v, 1);
   const long n_spawn = (long)d.NP + (long)d.A * d.Pcap + (d.virus_enabled ? (long)d.A * d.Vcap : 0) +
                        (long)d.A * d.H;
   hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d);
@@ -2547,7 +2647,7 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
 }
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   launch_tick_pre(d, s, scr_k, scr_v, rp);
-  launch_food(d, s, rounds, Scratch{scr_k, scr_v});
+  launch_food(d, s, rounds, Scratch{scr_k, scr_v}, 0, 1);
   launch_tick_post(d, s, scr_k, scr_v);
 }
 
@@ -2678,7 +2778,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.pl_state, 0, sizeof(unsigned long long) * (size_t)d.A * d.pl_tiles, s);
   hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
   (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
-  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1);
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1, (int64_t *)nullptr, (int *)nullptr, 0);
   hipLaunchKernelGGL(k_spawn_players, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, 1);
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
@@ -2687,4 +2787,20 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   launch_player_fov(d, s);
 }
 
+#ifdef AIGAR_PHASE_TIMING
+// out: [8][kPtWaves][8] wave records, ids: [8][kPtWaves][2] (see PT_BEGIN); *khz: the wall clock's rate
+extern "C" int aigar_debug_phase_times(unsigned int *out, unsigned int *ids, int *khz, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptw), sizeof(g_ptw)) != hipSuccess) return -1;
+  if (ids && hipMemcpyFromSymbol(ids, HIP_SYMBOL(g_ptid), sizeof(g_ptid)) != hipSuccess) return -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return -1;
+  if (reset) {
+    void *p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ptw)) != hipSuccess || hipMemset(p, 0, sizeof(g_ptw)) != hipSuccess)
+      return -1;
+  }
+  return 0;
+}
+#endif
 }  // namespace aigar
