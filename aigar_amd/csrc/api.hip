@@ -257,7 +257,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.bm_words = (int)(((size_t)kMaxCells * d.NP + 255) / 256 * 4);  // 16 * NP bits, whole TileRecs
   h->box_recs = 1 + d.tcap + d.bm_words / 4;
   for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_glibc((double)k, 0.32);
-  d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (k_grid_small)
+  d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (grid_small_build)
   while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
     d.cshift++;
   d.cshift_c = 0;  // player-cell grid: as fine as one block's LDS histogram allows

@@ -5,23 +5,29 @@
 //                             field.py:94-110, player.py:39-44
 //   k_players                 rest of updatePlayers (split, eject, move, push-apart) +
 //                             creation-sequence numbers (canonical order) + blob append
-//                             field.py:112-181, player.py:30-72
-//   k_grid_small              updateHashTables for blobs and viruses (field.py:121-132;
-//                             centre-bucket counting sort, membership tested exactly per query)
-//   k_merge_vb                mergePlayerCells + virus<-blob activity  field.py:183-198
-//   k_vb_serial               virusBlobOverlap         field.py:246-253, 316-325
-//   k_pv_active/serial        playerVirusOverlap       field.py:225-231, 333-370
-//   k_food_prep/commit/serial playerPelletOverlap + playerBlobOverlap field.py:207-222 as one
+//                             field.py:112-181, player.py:30-72; + updateHashTables for
+//                             blobs and viruses (field.py:121-132; centre-bucket counting
+//                             sort, membership tested exactly per query)
+//   k_merge_vb                mergePlayerCells + virus<-blob activity  field.py:183-198;
+//                             its last block: virusBlobOverlap's serial pass
+//                             field.py:246-253, 316-325
+//   k_pv_active               playerVirusOverlap       field.py:225-231, 333-370 (activity per
+//                             player; the serial pass in the last block)
+//   k_food_prep/commit        playerPelletOverlap + playerBlobOverlap field.py:207-222 as one
 //                             "deterministic reservations" pass: each cell reserves the foods
 //                             it could ever eat; a cell commits once it owns them all (=> every
 //                             earlier conflicting cell has committed); leftovers run serially
-//                             in priority order.  Extra blocks build the player-cell grid.
-//   k_pp_active/serial        playerPlayerOverlap      field.py:233-244
-//                             parallel activity test, then one wavefront per arena walks
-//                             the active players in order (live-list semantics incl.
-//                             skip-after-removal), re-activating neighbours on growth.
+//                             in priority order in the last commit round's last block.  Extra
+//                             blocks of rounds 1 / 2 build the player-cell grid.
+//   k_pp_active               playerPlayerOverlap      field.py:233-244
+//                             parallel activity test; its serial pass (one wavefront per
+//                             arena walks the active players in order: live-list semantics
+//                             incl. skip-after-removal, re-activating neighbours on growth)
+//                             opens k_spawn_plan
 //   k_spawn_plan/all          spawnStuff               field.py:256-313
 //   k_scan_lb, k_pgrid_scatter closing pellet rebuild; extra blocks refresh the FOV cache
+// "last block" = the block that draws the last ticket (last_block): an idle
+// serial pass then costs a ticket, not a dependent launch.
 #include <hip/hip_runtime.h>
 
 #include "aigar_dev.h"
@@ -66,6 +72,11 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
 #endif
 
 __device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { atomicOr(&d.ctl[a].err, bit); }
+
+constexpr int SG_CAP = 4096;           // cells of a coarse grid (small entity sets, player cells)
+constexpr int CG_STRIDE = SG_CAP + 4;  // per-arena, per-parity stride of Dev::cgcnt (16-byte aligned rows)
+template <int KIND>
+__device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh);
 
 // Last-block ticket (cdna_hip_programming.md, the in-launch reduction recipe):
 // each of the nblocks participating blocks publishes its writes (every wave's
@@ -462,24 +473,29 @@ __device__ __forceinline__ unsigned long long pl_word(unsigned long long st, uin
   return st | ((unsigned long long)(ep & 0x3FFFu) << 48) | ((unsigned long long)(vs & 0xFFFFFFu) << 24) |
          (unsigned long long)(vb & 0xFFFFFFu);
 }
+// updateHashTables for viruses and blobs rides along (the virus grid as one
+// extra block per arena -- viruses are final after k_tick_begin -- the blob
+// grid in the arena's last block, once every tile's blobs are appended).
 __global__ void __launch_bounds__(256) k_players(Dev d) {
   __shared__ int ws[4], wb[4];
   __shared__ int s_ps, s_pb, s_ts, s_tb, s_blob0;
   __shared__ int64_t s_seq0;
   __shared__ uint32_t s_epoch;
+  __shared__ int g_cnt[SG_CAP + 1], g_sh[32];  // (the small grids' counting sort)
   PT_BEGIN(1);
   const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ntiles = gridDim.x, NP = d.NP;
+  const int ntiles = d.pl_tiles, NP = d.NP;
+  if (tile == ntiles) {  // the virus grid (+ its radius bound and lightest mass)
+    grid_small_build<2>(d, a, g_cnt, g_sh);
+    return;
+  }
   ArenaCtl &c = d.ctl[a];
   unsigned long long *st = d.pl_state + (size_t)a * ntiles;
   if (tid == 0) {
     s_epoch = __hip_atomic_load(&c.pl_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_seq0 = c.seq_next;
     s_blob0 = c.n_blob;
-    if (tile == 0) {  // grid radius bounds restart (re-maxed by every grid build)
-      c.rmax_cell = 0;
-      c.rmax_virus = 0;
-    }
+    if (tile == 0) c.rmax_cell = 0;  // the cell grid's radius bound restarts (re-maxed by its build)
   }
   const int p = tile * 256 + tid, gp = a * d.B + p;
   int nn = 0, nb = 0;
@@ -608,9 +624,9 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     }
   }
   PT_MARK(1, 3);
-  if (tid == 0 && atomicAdd(&c.pl_ticket, 1) == ntiles - 1) {  // last block of the arena bumps the epoch
-    c.pl_ticket = 0;
-    __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (last_block(&c.pl_ticket, ntiles)) {  // the arena's last block: look-back epoch, blob grid
+    if (tid == 0) __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    grid_small_build<1>(d, a, g_cnt, g_sh);
   }
 }
 
@@ -643,16 +659,15 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
 }
 
 
-// Grids of the small entity sets (blobs, viruses): one 1024-thread block per
-// arena runs the whole counting sort in LDS on a grid coarsened by
-// 2^cshift (<= SG_CAP cells, chosen at create): LDS-atomic ranks, block scan,
-// coalesced start[] store, scatter.  One launch instead of count/scan/scatter.
-constexpr int SG_CAP = 4096;
-constexpr int CG_STRIDE = SG_CAP + 4;  // per-arena, per-parity stride of Dev::cgcnt (16-byte aligned rows)
+// Grids of the small entity sets (blobs, viruses): one block per arena (any
+// multiple of 64 threads) runs the whole counting sort in LDS on a grid
+// coarsened by 2^cshift (<= SG_CAP cells, chosen at create): LDS-atomic ranks,
+// block scan, coalesced start[] store, scatter.  The virus grid also sets the
+// radius bound and the lightest mass (the block is their only writer then).
 template <int KIND>
 __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
-  __shared__ double vmin_w[16];
-  const int tid = threadIdx.x, s = d.cshift;
+  __shared__ double vmin_w[32];  // per wave (<= 16): lightest mass, then largest radius
+  const int tid = threadIdx.x, T = blockDim.x, s = d.cshift;
   const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
   ArenaCtl &c = d.ctl[a];
   const int per = KIND == 1 ? d.Ecap : d.Vcap;
@@ -661,10 +676,10 @@ __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
   int *start = (KIND == 1 ? d.bstart : d.vstart) + (size_t)a * (d.H + 1);
   int *items = (KIND == 1 ? d.bitems : d.vitems) + (size_t)a * per;
   int *rank = (KIND == 1 ? d.b_rank : d.v_rank) + (size_t)a * per;
-  for (int i = tid; i <= Hc; i += 1024) cnt[i] = 0;
+  for (int i = tid; i <= Hc; i += T) cnt[i] = 0;
   __syncthreads();
   double rloc = 0;
-  for (int i = tid; i < n; i += 1024) {
+  for (int i = tid; i < n; i += T) {
     size_t g = (size_t)a * per + i;
     bool ok = (KIND == 1 ? d.b_flags[g] : d.v_flags[g]) & F_ALIVE;
     int rk = -1;
@@ -677,26 +692,35 @@ __device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
     rank[i] = rk;
   }
   if (KIND == 2) {
-    wave_atomic_max_pos(&c.rmax_virus, rloc);
     // lightest virus (bounds who can eat one in playerVirusOverlap)
     double mn = __builtin_inf();
-    for (int i = tid; i < n; i += 1024) {
+    for (int i = tid; i < n; i += T) {
       size_t g = (size_t)a * per + i;
       if (d.v_flags[g] & F_ALIVE) mn = fmin(mn, d.v_m[g]);
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off));
-    if ((tid & 63) == 0) vmin_w[tid >> 6] = mn;
+    for (int off = 32; off > 0; off >>= 1) {
+      mn = fmin(mn, __shfl_xor(mn, off));
+      rloc = fmax(rloc, __shfl_xor(rloc, off));
+    }
+    if ((tid & 63) == 0) {
+      vmin_w[tid >> 6] = mn;
+      vmin_w[16 + (tid >> 6)] = rloc;
+    }
   }
   __syncthreads();
   if (KIND == 2 && tid == 0) {
-    double mn = vmin_w[0];
-    for (int k = 1; k < (int)(blockDim.x >> 6); k++) mn = fmin(mn, vmin_w[k]);
+    double mn = vmin_w[0], rm = vmin_w[16];
+    for (int k = 1; k < T >> 6; k++) {
+      mn = fmin(mn, vmin_w[k]);
+      rm = fmax(rm, vmin_w[16 + k]);
+    }
     c.vmin_mass = mn;
+    c.rmax_virus = rm;
   }
   block_scan_excl(cnt, cnt, Hc + 1, sh);  // in place: bucket starts
-  for (int i = tid; i <= Hc; i += 1024) start[i] = cnt[i];
-  for (int i = tid; i < n; i += 1024) {
+  for (int i = tid; i <= Hc; i += T) start[i] = cnt[i];
+  for (int i = tid; i < n; i += T) {
     int rk = rank[i];
     if (rk < 0) continue;
     int b = rk >> 12, r = rk & 4095;
@@ -805,12 +829,6 @@ __device__ void cgrid_scatter_block(const Dev &d, int a, int bx) {
 }
 
 // blocks [0, A): blob grids; [A, 2A): virus grids (when enabled)
-__global__ void __launch_bounds__(1024) k_grid_small(Dev d) {
-  __shared__ int cnt[SG_CAP + 1];
-  __shared__ int sh[32];
-  if ((int)blockIdx.x < d.A) grid_small_build<1>(d, blockIdx.x, cnt, sh);
-  else grid_small_build<2>(d, blockIdx.x - d.A, cnt, sh);
-}
 
 // Single-pass multi-block exclusive scan with decoupled look-back.  Grid
 // (tiles, arenas), 256 threads, LB_TILE counts per block.  Each tile publishes
@@ -1286,42 +1304,50 @@ __device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items
   return false;
 }
 
-// one wavefront per player: cells that overlap an edible virus at phase start
-__global__ void __launch_bounds__(256) k_pv_active(Dev d) {
-  const int lane = threadIdx.x & 63;
-  const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gp >= d.NP || !d.p_alive[gp]) return;
+// one thread per player: its cells that overlap an edible virus at phase start
+// (c_active; the player joins the serial pass's work list).  Cells lighter than
+// 1.25 x the lightest virus have nothing to eat and skip the grid; the rest
+// walk the coarse virus grid serially (a few viruses per neighbourhood).  One
+// thread per player keeps the grid at NP/256 blocks, so the serial pass runs
+// in the last block (fold) for the price of a small ticket fan-in.
+__device__ void pv_player(const Dev &d, int gp) {
   const int NP = d.NP, a = gp / d.B;
-  int n = d.p_ncells[gp];
   const int *st = d.vstart + (size_t)a * (d.H + 1);
   const int *it = d.vitems + (size_t)a * d.Vcap;
-  int E = expand_for(d.ctl[a].rmax_virus);
-  // lightest virus at the grid build (k_grid_small); viruses split during
+  const int E = expand_for(d.ctl[a].rmax_virus);
+  // lightest virus at the grid build (k_players); viruses split during
   // virusBlobOverlap are >= (VIRUS_BASE_SIZE + 7 * 14.4) / 2, so VIRUS_BASE_SIZE bounds them
   const double vmin = fmin(d.ctl[a].vmin_mass, kVirusBase);
+  const int n = d.p_ncells[gp];
   bool anyp = false;
   for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
-    if (!(m > 1.25 * vmin)) {  // lighter than 1.25 x the lightest virus: nothing to eat
-      if (lane == 0) d.c_active[ci] = 0;
-      continue;
+    const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    const double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    bool any = false;
+    if (m > 1.25 * vmin) {
+      const Rect q = footprint(x, y, r, d.size);
+      grid_visit(st, it, d.cols, q, E, [&](int j) {
+        const size_t g = (size_t)a * d.Vcap + j;
+        if (any || (d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
+        if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return;
+        any = overlap(x, y, m, r, d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) && m > 1.25 * d.v_m[g];
+      }, d.cshift);
     }
-    Rect q = footprint(x, y, r, d.size);
-    bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int j) {
-      size_t g = (size_t)a * d.Vcap + j;
-      if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return false;
-      if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return false;
-      return overlap(x, y, m, r, d.v_x[g], d.v_y[g], d.v_m[g], d.v_r[g]) && m > 1.25 * d.v_m[g];
-    }, d.cshift);
-    if (lane == 0) d.c_active[ci] = any;
+    d.c_active[ci] = any;
     anyp |= any;
   }
-  if (anyp && lane == 0) {
-    int w = atomicAdd(&d.ctl[a].n_pend, 1);
+  if (anyp) {
+    const int w = atomicAdd(&d.ctl[a].n_pend, 1);
     if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
     else set_err(d, a, ERR_WORK_CAP);
   }
+}
+__device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
+__global__ void __launch_bounds__(256) k_pv_active(Dev d, int64_t *scr_k, int *scr_v, int fold) {
+  const int gp = GTID;
+  if (gp < d.NP && d.p_alive[gp]) pv_player(d, gp);
+  if (fold && last_block(d.ticket + 2, gridDim.x))
+    for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) pv_serial_body(d, a, scr_k, scr_v);
 }
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
   if ((threadIdx.x & 63) != 0) return;
@@ -1426,9 +1452,6 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
     }
     for (int k = 0; k < d.p_ncells[gp]; k++) d.c_flags[(size_t)d.p_list[k * NP + gp] * NP + gp] &= ~F_NEW;
   }
-}
-__global__ void __launch_bounds__(64) k_pv_serial(Dev d, int64_t *scr_k, int *scr_v) {
-  pv_serial_body(d, blockIdx.x, scr_k, scr_v);
 }
 
 // ------------------------------------------------------------ T14/T15 food
@@ -2620,13 +2643,13 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
-  hipLaunchKernelGGL(k_players, dim3(d.pl_tiles, d.A), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_grid_small, dim3(d.virus_enabled ? 2 * d.A : d.A), dim3(1024), 0, s, d);
+  // + the virus grid (extra block) and the blob grid (last block) of updateHashTables
+  hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + (d.virus_enabled ? 1 : 0), d.A), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
                      dim3(256), 0, s, d, scr_k, scr_v, d.virus_enabled ? 1 : 0);  // + virusBlobOverlap's serial pass
   if (d.virus_enabled) {
-    hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_pv_serial, dim3(d.A), dim3(64), 0, s, d, scr_k, scr_v);
+    // playerVirusOverlap: activity test + its serial pass in the last block
+    hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, scr_k, scr_v, 1);
   }
 }
 // the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
