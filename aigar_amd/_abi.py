@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 RNG_PHILOX = 0
 RNG_MT19937 = 1
@@ -80,6 +80,7 @@ class State(C.Structure):
         ("players_f", _PD), ("players_i", _PI), ("cells_f", _PD), ("cells_i", _PI),
         ("pellets_f", _PD), ("pellets_seq", _PI), ("blobs_f", _PD), ("blobs_i", _PI),
         ("viruses_f", _PD), ("viruses_i", _PI), ("dead", _PI),
+        ("pellets_col", _PI), ("blobs_col", _PI),
     ]
 
 
@@ -91,7 +92,10 @@ LAYOUT = {
     "blobs_f": ("n_blobs", 8, np.float64), "blobs_i": ("n_blobs", 3, np.int64),
     "viruses_f": ("n_viruses", 8, np.float64), "viruses_i": ("n_viruses", 3, np.int64),
     "dead": ("n_dead", 0, np.int64),
+    # optional: colour owners (player index, -1: own colour); absent from older snapshots
+    "pellets_col": ("n_pellets", 0, np.int64), "blobs_col": ("n_blobs", 0, np.int64),
 }
+OPTIONAL = ("pellets_col", "blobs_col")
 SCALARS = ("n_players", "field_size", "virus_enabled", "rng_mode", "seq_next", "tick",
            "max_pellets", "max_viruses", "ctr_pellet", "ctr_virus", "mt_pos")
 
@@ -105,6 +109,8 @@ def state_to_struct(d):
     st = State()
     keep = []
     for name, (cnt, cols, dt) in LAYOUT.items():
+        if name in OPTIONAL and name not in d:
+            continue  # (NULL: the library takes -1)
         a = np.ascontiguousarray(d[name], dtype=dt)
         n = a.shape[0] if a.ndim else 0
         if cols:

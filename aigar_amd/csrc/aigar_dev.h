@@ -131,8 +131,10 @@ struct Dev {
   // pellets: two record buffers + staging
   double *pel_x[2], *pel_y[2], *pel_m[2];
   int64_t *pel_seq[2];
+  int *pel_col[2];  // colour owner: the player whose colour a blob-made pellet carries, -1: its own
   double *pn_x, *pn_y, *pn_m;
   int64_t *pn_seq;
+  int *pn_col;
   uint8_t *pel_dead;  // [A*Pcap] for the eat-phase buffer
   int *pel_rank;      // scratch [A*(Pcap)]
   int *pcnt, *pstart; // [A*(H+1)] survivor counts / bucket starts (pellets)
@@ -142,6 +144,7 @@ struct Dev {
   double *b_x, *b_y, *b_m, *b_r, *b_vx, *b_vy, *b_svx, *b_svy;
   int *b_svc;
   int64_t *b_seq, *b_ej;
+  int *b_col;  // the ejecting player (field.py:141 blob.setColor(player.getColor()))
   uint32_t *b_flags;
   uint64_t *b_owner;
   int *bcnt, *bstart, *bitems, *b_rank;

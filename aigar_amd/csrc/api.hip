@@ -285,14 +285,15 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   const size_t P = A * d.Pcap;
   for (int b = 0; b < 2; b++) {
     AL(pel_x[b], double, P); AL(pel_y[b], double, P); AL(pel_m[b], double, P); AL(pel_seq[b], int64_t, P);
+    AL(pel_col[b], int, P);
   }
-  AL(pn_x, double, P); AL(pn_y, double, P); AL(pn_m, double, P); AL(pn_seq, int64_t, P);
+  AL(pn_x, double, P); AL(pn_y, double, P); AL(pn_m, double, P); AL(pn_seq, int64_t, P); AL(pn_col, int, P);
   AL(pel_dead, uint8_t, P); AL(pel_rank, int, 2 * P); AL(pcnt, int, A * H1); AL(pncnt, int, A * H1); AL(pstart, int, A * H1);
   AL(pel_owner, uint64_t, P);
   const size_t E = A * d.Ecap, V = A * d.Vcap;
   AL(b_x, double, E); AL(b_y, double, E); AL(b_m, double, E); AL(b_r, double, E); AL(b_vx, double, E);
   AL(b_vy, double, E); AL(b_svx, double, E); AL(b_svy, double, E); AL(b_svc, int, E); AL(b_seq, int64_t, E);
-  AL(b_ej, int64_t, E); AL(b_flags, uint32_t, E); AL(b_owner, uint64_t, E);
+  AL(b_ej, int64_t, E); AL(b_flags, uint32_t, E); AL(b_owner, uint64_t, E); AL(b_col, int, E);
   AL(bcnt, int, A * H1); AL(bstart, int, A * H1); AL(bitems, int, E); AL(b_rank, int, E);
   AL(v_x, double, V); AL(v_y, double, V); AL(v_m, double, V); AL(v_r, double, V); AL(v_vx, double, V);
   AL(v_vy, double, V); AL(v_svx, double, V); AL(v_svy, double, V); AL(v_svc, int, V); AL(v_seq, int64_t, V);
@@ -917,18 +918,19 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
   const size_t po = (size_t)arena * d.Pcap, bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;
   std::vector<double> px, py, pm, bf[8], vf[8];
   std::vector<int64_t> ps, bseq, bej, vseq;
-  std::vector<int> bsvc, vsvc;
+  std::vector<int> bsvc, vsvc, pcol, bcol;
   std::vector<uint32_t> bfl, vfl;
   const int pb = c.pcur;
   if (d2h(h, px, d.pel_x[pb] + po, c.n_pel) || d2h(h, py, d.pel_y[pb] + po, c.n_pel) ||
-      d2h(h, pm, d.pel_m[pb] + po, c.n_pel) || d2h(h, ps, d.pel_seq[pb] + po, c.n_pel))
+      d2h(h, pm, d.pel_m[pb] + po, c.n_pel) || d2h(h, ps, d.pel_seq[pb] + po, c.n_pel) ||
+      d2h(h, pcol, d.pel_col[pb] + po, c.n_pel))
     return -1;
   double *bfs[8] = {d.b_x, d.b_y, d.b_m, d.b_r, d.b_vx, d.b_vy, d.b_svx, d.b_svy};
   double *vfs[8] = {d.v_x, d.v_y, d.v_m, d.v_r, d.v_vx, d.v_vy, d.v_svx, d.v_svy};
   for (int f = 0; f < 8; f++)
     if (d2h(h, bf[f], bfs[f] + bo, c.n_blob) || d2h(h, vf[f], vfs[f] + vo, c.n_vir)) return -1;
   if (d2h(h, bsvc, d.b_svc + bo, c.n_blob) || d2h(h, bseq, d.b_seq + bo, c.n_blob) ||
-      d2h(h, bej, d.b_ej + bo, c.n_blob) || d2h(h, bfl, d.b_flags + bo, c.n_blob) ||
+      d2h(h, bej, d.b_ej + bo, c.n_blob) || d2h(h, bfl, d.b_flags + bo, c.n_blob) || d2h(h, bcol, d.b_col + bo, c.n_blob) ||
       d2h(h, vsvc, d.v_svc + vo, c.n_vir) || d2h(h, vseq, d.v_seq + vo, c.n_vir) ||
       d2h(h, vfl, d.v_flags + vo, c.n_vir))
     return -1;
@@ -992,11 +994,13 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
     double *f = st->pellets_f + 4 * i;
     f[0] = px[j]; f[1] = py[j]; f[2] = pm[j]; f[3] = pm[j] > 0 ? std::sqrt(pm[j] / 3.141592653589793) : 0.0;
     st->pellets_seq[i] = ps[j];
+    if (st->pellets_col) st->pellets_col[i] = pcol[j];
   }
   for (size_t i = 0; i < bl.size(); i++) {
     int j = bl[i];
     for (int f = 0; f < 8; f++) st->blobs_f[8 * i + f] = bf[f][j];
     st->blobs_i[3 * i] = bsvc[j]; st->blobs_i[3 * i + 1] = bseq[j]; st->blobs_i[3 * i + 2] = bej[j];
+    if (st->blobs_col) st->blobs_col[i] = bcol[j];
   }
   for (size_t i = 0; i < vl.size(); i++) {
     int j = vl[i];
@@ -1108,6 +1112,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   // (tiles: only the pellets in the held range)
   std::vector<double> px, py, pm;
   std::vector<int64_t> ps;
+  std::vector<int> pc;
   for (int i = 0; i < st->n_pellets; i++) {
     const double x = st->pellets_f[4 * i], y = st->pellets_f[4 * i + 1];
     const int bx = std::min(d.cols - 1, std::max(0, (int)(x / kBucket)));
@@ -1117,17 +1122,19 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
     py.push_back(y);
     pm.push_back(st->pellets_f[4 * i + 2]);
     ps.push_back(st->pellets_seq[i]);
+    pc.push_back(st->pellets_col ? (int)st->pellets_col[i] : -1);
   }
   host_grid(d.cols, px, py, start, order);
   {
     std::vector<double> sx(order.size()), sy(order.size()), sm(order.size());
     std::vector<int64_t> ss(order.size());
+    std::vector<int> sc(order.size());
     for (size_t i = 0; i < order.size(); i++) {
-      sx[i] = px[order[i]]; sy[i] = py[order[i]]; sm[i] = pm[order[i]]; ss[i] = ps[order[i]];
+      sx[i] = px[order[i]]; sy[i] = py[order[i]]; sm[i] = pm[order[i]]; ss[i] = ps[order[i]]; sc[i] = pc[order[i]];
     }
     const size_t po = (size_t)arena * d.Pcap;
     if (h2d(h, d.pel_x[0] + po, sx) || h2d(h, d.pel_y[0] + po, sy) || h2d(h, d.pel_m[0] + po, sm) ||
-        h2d(h, d.pel_seq[0] + po, ss))
+        h2d(h, d.pel_seq[0] + po, ss) || h2d(h, d.pel_col[0] + po, sc))
       return -1;
     HIPCHK(hipMemcpyAsync(d.pstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
   }
@@ -1141,13 +1148,14 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
     for (int i = 0; i < st->n_viruses; i++) vv[i] = st->viruses_f[8 * i + f];
     if (h2d(h, bfs[f] + bo, bv) || h2d(h, vfs[f] + vo, vv)) return -1;
   }
-  std::vector<int> bsvc(st->n_blobs), vsvc(st->n_viruses);
+  std::vector<int> bsvc(st->n_blobs), vsvc(st->n_viruses), bcol(st->n_blobs);
   std::vector<int64_t> bseq(st->n_blobs), bej(st->n_blobs), vseq(st->n_viruses);
   std::vector<uint32_t> bfl(d.Ecap, 0), vfl(d.Vcap, 0);
   std::vector<double> vgx, vgy;
   double rmax_v = 0;
   for (int i = 0; i < st->n_blobs; i++) {
     bsvc[i] = (int)st->blobs_i[3 * i]; bseq[i] = st->blobs_i[3 * i + 1]; bej[i] = st->blobs_i[3 * i + 2];
+    bcol[i] = st->blobs_col ? (int)st->blobs_col[i] : -1;
     bfl[i] = F_ALIVE;
   }
   std::vector<int> vg_ids;
@@ -1158,7 +1166,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
     vgy.push_back(st->viruses_f[8 * i + 1]);
     rmax_v = std::max(rmax_v, st->viruses_f[8 * i + 3]);
   }
-  if (h2d(h, d.b_svc + bo, bsvc) || h2d(h, d.b_seq + bo, bseq) || h2d(h, d.b_ej + bo, bej) ||
+  if (h2d(h, d.b_svc + bo, bsvc) || h2d(h, d.b_seq + bo, bseq) || h2d(h, d.b_ej + bo, bej) || h2d(h, d.b_col + bo, bcol) ||
       h2d(h, d.b_flags + bo, bfl) || h2d(h, d.v_svc + vo, vsvc) || h2d(h, d.v_seq + vo, vseq) ||
       h2d(h, d.v_flags + vo, vfl))
     return -1;

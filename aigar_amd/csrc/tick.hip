@@ -66,9 +66,13 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                     \
     if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[k][pt_w_][m] = (unsigned)(wall_clock64() - pt0_); \
   } while (0)
+#define PT_PARAMS , unsigned long long pt0_, int pt_w_
+#define PT_ARGS , pt0_, pt_w_
 #else
 #define PT_BEGIN(k)
 #define PT_MARK(k, m)
+#define PT_PARAMS
+#define PT_ARGS
 #endif
 
 __device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { atomicOr(&d.ctl[a].err, bit); }
@@ -180,6 +184,7 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
     d.pn_y[pj] = d.b_y[gi];
     d.pn_m[pj] = d.b_m[gi];
     d.pn_seq[pj] = d.b_seq[gi];
+    d.pn_col[pj] = d.b_col[gi];  // (addPellet(blob): the same object, its colour kept)
     d.b_flags[gi] = 0;
     atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
     return;
@@ -202,7 +207,7 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
 // rp.on: the synthetic population's policy is evaluated here (every cell of a
 // player computes the same command; slot 0 stores it for k_players), which
 // saves the policy launch of aigar_run's step
-__device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPolicy &rp) {
+__device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPolicy &rp PT_PARAMS) {
   const int NP = d.NP;
   if (gi >= kMaxCells * NP) return;
   const int gp = gi % NP;
@@ -215,8 +220,10 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   const double x = d.c_x[ci], y = d.c_y[ci];
   int svc = d.c_svc[ci];
   double cmdx, cmdy;
+  PT_MARK(2, 2);
   if (rp.on) {
     const Command c = random_command(d, gp, rp);  // (the player's live cells and slot 0 only)
+    PT_MARK(2, 3);
     if (gi < NP) {  // slot 0 stores the player's command
       d.p_cmdx[gp] = c.x;
       d.p_cmdy[gp] = c.y;
@@ -242,7 +249,9 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   d.c_svy[ci] = svy;
   if (mt > 0) d.c_mt[ci] = mt - 1;
   double vx, vy;
+  PT_MARK(2, 4);
   set_move_direction(x, y, m, r, cmdx, cmdy, vx, vy);
+  PT_MARK(2, 5);
   d.c_vx[ci] = vx;
   d.c_vy[ci] = vy;
 }
@@ -387,7 +396,7 @@ __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   PT_BEGIN(2);
   int gi = GTID;
   if (gi < kMaxCells * d.NP) {
-    update_cell(d, gi, rp);
+    update_cell(d, gi, rp PT_ARGS);
     PT_MARK(2, 1);
     return;
   }
@@ -620,6 +629,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
       d.b_svc[g] = 15;
       d.b_seq[g] = s0 + nn + j;
       d.b_ej[g] = d.c_seq[(size_t)d.sb_slot[si] * NP + gp];
+      d.b_col[g] = p;
       d.b_flags[g] = F_ALIVE;
     }
   }
@@ -1024,7 +1034,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
   const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
   double x, y, m;
   int64_t s;
-  int pos;
+  int pos, col;
   if (i < d.Pcap) {
     if (i >= c.src_n_pel) return;
     size_t g = (size_t)a * d.Pcap + i;
@@ -1036,6 +1046,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
     y = d.pel_y[src][g];
     m = d.pel_m[src][g];
     s = d.pel_seq[src][g];
+    col = d.pel_col[src][g];
     int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
     pos = d.pstart[H1 + b] + d.pel_rank[R0 + i];
   } else {
@@ -1055,6 +1066,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
     y = d.pn_y[g];
     m = d.pn_m[g];
     s = d.pn_seq[g];
+    col = d.pn_col[g];
     int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
     pos = d.pstart[H1 + b + 1] - 1 - rk;
   }
@@ -1067,6 +1079,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
   d.pel_y[dst][o] = y;
   d.pel_m[dst][o] = m;
   d.pel_seq[dst][o] = s;
+  d.pel_col[dst][o] = col;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
 // fov_blocks > 0 (the tick's closing rebuild): the last fov_blocks blocks
@@ -2317,7 +2330,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
       size_t g = (size_t)a * cap + i;
       bool alive = i < n && ((kind == 0 ? d.v_flags[g] : d.b_flags[g]) & F_ALIVE);
       double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, f6 = 0, f7 = 0;
-      int svc = 0;
+      int svc = 0, col = -1;
       int64_t s = 0, e = 0;
       uint32_t fl = 0;
       if (alive) {
@@ -2327,6 +2340,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
         } else {
           f0 = d.b_x[g]; f1 = d.b_y[g]; f2 = d.b_m[g]; f3 = d.b_r[g]; f4 = d.b_vx[g]; f5 = d.b_vy[g];
           f6 = d.b_svx[g]; f7 = d.b_svy[g]; svc = d.b_svc[g]; s = d.b_seq[g]; e = d.b_ej[g]; fl = d.b_flags[g];
+          col = d.b_col[g];
         }
       }
       int chunk;
@@ -2339,6 +2353,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
         } else {
           d.b_x[o] = f0; d.b_y[o] = f1; d.b_m[o] = f2; d.b_r[o] = f3; d.b_vx[o] = f4; d.b_vy[o] = f5;
           d.b_svx[o] = f6; d.b_svy[o] = f7; d.b_svc[o] = svc; d.b_seq[o] = s; d.b_ej[o] = e; d.b_flags[o] = fl;
+          d.b_col[o] = col;
         }
       }
       out += chunk;
@@ -2473,6 +2488,7 @@ __device__ __forceinline__ void spawn_pellet(const Dev &d, int gi, bool rank_sta
   d.pn_y[o] = (double)y;
   d.pn_m[o] = m;
   d.pn_seq[o] = c.seq_base_spawn + j;
+  d.pn_col[o] = -1;  // Cell(..., None): a colour of its own
   if (rank_staged) pgrid_rank_staged(d, a, c.n_pnew + j);  // rebuild ranks taken at spawn time
 }
 __global__ void k_spawn_pellets(Dev d) { spawn_pellet(d, GTID, false); }

@@ -392,18 +392,18 @@ class Field:
         st = self._snapshot()
         per_player = [[] for _ in self.players]
         cells = []
-        owner_of = {}  # cell seq -> player index (an ejected blob takes its player's colour)
         pcol = [p.getColor() for p in self.players]
         for f, i in zip(st["cells_f"], st["cells_i"]):
             c = Cell("player", f[:8], i[2], i[1], self.players[int(i[0])], f[8], pcol[int(i[0])])
             per_player[int(i[0])].append(c)
             cells.append(c)
-            owner_of[int(i[2])] = int(i[0])
-        pel = [Cell("pellet", f, s, 0, color=pellet_color(s, self.seed))
-               for f, s in zip(st["pellets_f"], st["pellets_seq"])]
-        blobs = [Cell("blob", f, i[1], i[0], color=(pcol[owner_of[int(i[2])]] if int(i[2]) in owner_of
-                                                    else pellet_color(i[1], self.seed)))
-                 for f, i in zip(st["blobs_f"], st["blobs_i"])]
+        # an ejected blob carries its player's colour (field.py:141, cell.py:219), and so
+        # does the pellet it becomes (addPellet(blob), field.py:110): the state's colour owners
+        colour = lambda owner, seq: pcol[int(owner)] if owner >= 0 else pellet_color(seq, self.seed)  # noqa: E731
+        pel = [Cell("pellet", f, s, 0, color=colour(c, s))
+               for f, s, c in zip(st["pellets_f"], st["pellets_seq"], st["pellets_col"])]
+        blobs = [Cell("blob", f, i[1], i[0], color=colour(c, i[1]))
+                 for f, i, c in zip(st["blobs_f"], st["blobs_i"], st["blobs_col"])]
         vir = [Cell("virus", f, i[1], i[0], color=VIRUS_COLOR) for f, i in zip(st["viruses_f"], st["viruses_i"])]
         v = {"per_player": per_player, "cells": cells, "pellets": pel, "blobs": blobs, "viruses": vir,
              "cell_hashed": np.asarray(st["cells_i"])[:, 3] != 0 if len(cells) else np.zeros(0, bool),

@@ -62,6 +62,8 @@ def merge_states(states):
     ps = np.concatenate([s["pellets_seq"] for s in states])
     o = np.argsort(ps, kind="stable")
     d["pellets_f"], d["pellets_seq"] = pf[o], ps[o]
+    if all("pellets_col" in s for s in states):
+        d["pellets_col"] = np.concatenate([s["pellets_col"] for s in states])[o]
     d["n_pellets"] = len(ps)
     return d
 

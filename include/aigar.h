@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AIGAR_ABI_VERSION 2
+#define AIGAR_ABI_VERSION 3
 
 /* random number stream of the world (spawns, explosion angles) */
 #define AIGAR_RNG_PHILOX 0   /* Philox4x64-10 keyed by (seed, site, index): device + oracle */
@@ -139,6 +139,12 @@ typedef struct aigar_state {
   double *viruses_f;
   int64_t *viruses_i;
   int64_t *dead;
+  /* optional (NULL: not exported / -1 on import): the player whose colour the
+   * object carries -- an ejected blob its ejecting player's (field.py:141,
+   * cell.py:219), a pellet made from a blob the blob's (field.py:110) -- or -1
+   * for a pellet's / orphan blob's colour of its own (cell.py:31) */
+  int64_t *pellets_col;  /* [n_pellets], in pellets_seq order */
+  int64_t *blobs_col;    /* [n_blobs] */
 } aigar_state;
 
 const char *aigar_last_error(void);

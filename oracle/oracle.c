@@ -219,6 +219,8 @@ typedef struct Cell {
   int alive;
   int blob_to_eject;
   int64_t ejecter_seq;
+  int col;  /* colour owner: the player whose colour an ejected blob (and the
+               pellet it becomes) carries (field.py:141, cell.py:219), else -1 */
   int mark; /* scratch for snapshot hash membership */
 } Cell;
 
@@ -314,6 +316,7 @@ static Cell *new_cell(Arena *A, double x, double y, double mass, int player) {
   c->merge_time = 0;
   c->alive = 1;
   c->ejecter_seq = -1;
+  c->col = -1;
   return c;
 }
 
@@ -748,6 +751,7 @@ static void update_players(Arena *A) { /* field.py:112-119 */
       add_momentum(b, P->cmdx, P->cmdy, A->size, A->size, c);
       cv_push(&A->blobs, b);
       b->ejecter_seq = c->seq;
+      b->col = c->player; /* blob.setColor(player.getColor()); setEjecterCell (field.py:141-146) */
     }
     for (int i = 0; i < P->cells.n; i++) { /* handlePlayerCollisions field.py:149-159 */
       Cell *c = P->cells.a[i];
@@ -1380,6 +1384,7 @@ static void pixels_one(Arena *A, int p, int L, uint64_t seed, uint8_t *out) {
     uint8_t col[3], rim[3];
     if (objs[i].kind == 3) player_rgb(c->player, seed, col);
     else if (objs[i].kind == 2) { col[0] = 0; col[1] = 255; col[2] = 0; }
+    else if (c->col >= 0) player_rgb(c->col, seed, col); /* a blob / blob-made pellet: its player's */
     else pellet_rgb(c->seq, seed, col);
     int rad = (int)(c->radius * scale);
     int x = (int)(int64_t)(((c->x - fx) + fs / 2) * scale), y = (int)(int64_t)(((c->y - fy) + fs / 2) * scale);
@@ -1670,6 +1675,7 @@ int oracle_get_state(void *h, int arena, aigar_state *st) {
     double *f = st->pellets_f + 4 * i;
     f[0] = ps[i]->x; f[1] = ps[i]->y; f[2] = ps[i]->mass; f[3] = ps[i]->radius;
     st->pellets_seq[i] = ps[i]->seq;
+    if (st->pellets_col) st->pellets_col[i] = ps[i]->col;
   }
   free(ps);
   for (int i = 0; i < A->blobs.n; i++) {
@@ -1678,6 +1684,7 @@ int oracle_get_state(void *h, int arena, aigar_state *st) {
     f[0] = c->x; f[1] = c->y; f[2] = c->mass; f[3] = c->radius; f[4] = c->vx; f[5] = c->vy; f[6] = c->svx; f[7] = c->svy;
     int64_t *q = st->blobs_i + 3 * i;
     q[0] = c->svc; q[1] = c->seq; q[2] = c->ejecter_seq;
+    if (st->blobs_col) st->blobs_col[i] = c->col;
   }
   for (int i = 0; i < A->viruses.n; i++) {
     Cell *c = A->viruses.a[i];
@@ -1741,6 +1748,7 @@ int oracle_load_state(void *h, int arena, const aigar_state *st) {
     Cell *c = (Cell *)calloc(1, sizeof(Cell));
     c->x = f[0]; c->y = f[1]; c->mass = f[2]; c->radius = f[3]; c->seq = st->pellets_seq[i];
     c->player = -1; c->alive = 1; c->ejecter_seq = -1;
+    c->col = st->pellets_col ? (int)st->pellets_col[i] : -1;
     cv_push(&A->pellets, c);
     hash_insert(&A->ph, c);
   }
@@ -1750,6 +1758,7 @@ int oracle_load_state(void *h, int arena, const aigar_state *st) {
     Cell *c = (Cell *)calloc(1, sizeof(Cell));
     c->x = f[0]; c->y = f[1]; c->mass = f[2]; c->radius = f[3]; c->vx = f[4]; c->vy = f[5]; c->svx = f[6]; c->svy = f[7];
     c->svc = (int)q[0]; c->seq = q[1]; c->ejecter_seq = q[2]; c->player = -1; c->alive = 1;
+    c->col = st->blobs_col ? (int)st->blobs_col[i] : -1;
     cv_push(&A->blobs, c);
     hash_insert(&A->bh, c);
   }

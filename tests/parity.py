@@ -49,7 +49,9 @@ def diff_states(a, b, ftol=FTOL):
             out.append("%s: %s != %s" % (k, a[k], b[k]))
     if out:
         return out
-    for k in ("players_i", "cells_i", "pellets_seq", "blobs_i", "viruses_i", "dead"):
+    for k in ("players_i", "cells_i", "pellets_seq", "blobs_i", "viruses_i", "dead", "pellets_col", "blobs_col"):
+        if k not in a or k not in b:  # (colour owners: optional)
+            continue
         if not np.array_equal(a[k], b[k]):
             idx = np.argwhere(np.asarray(a[k]) != np.asarray(b[k]))
             out.append("%s differs at %s: %s vs %s" % (k, idx[:3].tolist(), np.asarray(a[k])[tuple(idx[0])],

@@ -129,3 +129,48 @@ def test_rgb_generator_facade():
     gray = M.RGBGenerator(field, params).get_cnn_inputRGB(mdl.getPlayers()[0])
     assert gray.shape == (42, 42, 1)
     orc.close()
+
+
+def test_blob_colours_follow_the_ejecting_player():
+    """Ejected blobs carry their player's colour (field.py:141, cell.py:219) and
+    keep it as the pellets they become (addPellet(blob), field.py:110): the
+    colour owners in the state equal the oracle's and the ejecting player's
+    index, and the frames that show them equal the oracle's."""
+    cfg = make_config(bots=4, virus=False, channels=CH, extras=0, field_size=300, max_pellets=50)
+    g, o = pair(cfg, 3)
+    st = g.get_state()
+    cf = np.array(st["cells_f"])
+    ci = np.array(st["cells_i"])
+    k = int(np.argmax(ci[:, 0] == 1))  # player 1's first cell: heavy enough to eject for a while
+    cf[k, 2] = 400.0
+    cf[k, 3] = np.sqrt(400.0 / np.pi)
+    st["cells_f"] = cf
+    g.load_state(st)
+    o.load_state(st)
+    n = cfg.bots_per_arena
+    ejected = pelleted = False
+    for t in range(40):
+        cmd = np.zeros((n, 4))
+        cmd[:, 0] = cmd[:, 1] = 150.0
+        cmd[1, 0], cmd[1, 3] = 10.0, 1.0 if t < 8 else 0.0  # player 1 ejects towards the left wall
+        g.set_commands(cmd)
+        o.set_commands(cmd)
+        g.step(1)
+        o.step(1)
+        sg, so = g.get_state(), o.get_state()
+        dif = parity.diff_states(sg, so)
+        assert not dif, (t, dif)
+        if len(sg["blobs_col"]):
+            assert set(np.asarray(sg["blobs_col"]).tolist()) <= {1}, sg["blobs_col"]
+            ejected = True
+        if 1 in set(np.asarray(sg["pellets_col"]).tolist()):
+            pelleted = True
+        if ejected and t % 5 == 0:
+            for cseed in (0, 7):
+                assert_frames_equal(g.observe_pixels(42, cseed), o.pixels(42, cseed))
+    assert ejected and pelleted
+    assert set(np.asarray(sg["pellets_col"]).tolist()) <= {-1, 1}
+    for cseed in (0, 7):
+        assert_frames_equal(g.observe_pixels(42, cseed), o.pixels(42, cseed))
+    g.close()
+    o.close()

@@ -57,6 +57,8 @@ def test_oracle_reproduces_reference(name, golden_dir):
             st = o.get_state()
             pre = "ck%d/" % (t + 1)
             for k in _abi.LAYOUT:
+                if k in _abi.OPTIONAL and pre + k not in z.files:
+                    continue  # (colour owners: the fixtures predate them; colours are unpinned)
                 assert _same(st[k], z[pre + k]), "%s differs at tick %d" % (k, t + 1)
             assert np.array_equal(st["mt_key"], z[pre + "mt_key"]) and st["mt_pos"] == z[pre + "mt_pos"]
             assert st["seq_next"] == z[pre + "seq_next"]

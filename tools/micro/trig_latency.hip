@@ -48,6 +48,24 @@ float run(const double *x, const double *y, const double *m, double *o, int n, i
   return ms * 1000.0f / reps;
 }
 
+// A, B alternating: with B's code in between, A starts from a cold instruction cache
+template <int A, int B>
+float run_pair(const double *x, const double *y, const double *m, double *o, int n, int reps) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  for (int r = 0; r < reps; r++) {
+    hipLaunchKernelGGL(k<A>, dim3((n + 255) / 256), dim3(256), 0, 0, x, y, m, o, n);
+    hipLaunchKernelGGL(k<B>, dim3((n + 255) / 256), dim3(256), 0, 0, x, y, m, o, n);
+  }
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1000.0f / reps;
+}
+
 int main() {
   const int n = 6144, reps = 500;
   std::mt19937_64 g(1);
@@ -74,5 +92,9 @@ int main() {
   printf("atan2+sincos    %.2f\n", run<4>(dx, dy, dm, dout, n, reps));
   printf("move direction  %.2f\n", run<5>(dx, dy, dm, dout, n, reps));
   printf("ocml            %.2f\n", run<8>(dx, dy, dm, dout, n, reps));
+  const float p58 = run_pair<5, 8>(dx, dy, dm, dout, n, reps), p88 = run_pair<8, 8>(dx, dy, dm, dout, n, reps);
+  const float p55 = run_pair<5, 5>(dx, dy, dm, dout, n, reps);
+  printf("pairs: move+ocml %.2f, ocml+ocml %.2f, move+move %.2f -> move direction after other code %.2f vs warm %.2f\n",
+         p58, p88, p55, p58 - p88 / 2, p55 / 2);
   return 0;
 }
