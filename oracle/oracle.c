@@ -1602,7 +1602,8 @@ int oracle_player_stats(void *h, double *out) {
 }
 int oracle_get_events(void *h, int arena, int64_t *out, int cap) {
   Arena *A = &((Oracle *)h)->ar[arena];
-  if (out) memcpy(out, A->ev, sizeof(int64_t) * 4 * (size_t)(A->n_ev < cap ? A->n_ev : cap));
+  const int n = A->n_ev < cap ? A->n_ev : cap;
+  if (out && n > 0) memcpy(out, A->ev, sizeof(int64_t) * 4 * (size_t)n);  /* (no events: A->ev may be NULL) */
   return A->n_ev;
 }
 int oracle_reset_obs_state(void *h) {
