@@ -49,6 +49,9 @@ struct ArenaCtl {
   int scan_ticket[2];      // slot 0: pellet rebuilds, slot 1: cell grid (may run concurrently)
   int src_n_pel, src_n_stage;
   int src_n_conv;  // blob conversions among the staged records (eaten ones are dropped)
+  int n_kill;      // buffer pellets killed this tick (kill_list; sorted + unique after k_spawn_plan)
+  int n_stg;       // staged records joining the buffer at the closing update (stg_key)
+  int pu_src, pu_n0, pu_nconv;  // the closing update's source buffer, its count, blob conversions
   int pcur;           // pellet buffer holding the current (end-of-tick) pellets
   int peat;           // pellet buffer of this tick's eat phase (pcur when nothing was converted)
   uint32_t dirty;     // DIRTY_*: a virus / blob died this tick (k_spawn_plan compacts)
@@ -99,6 +102,12 @@ struct Dev {
   TileRec *outbox;       // [1 + tcap] records + bitmap
   const TileRec *inbox;  // [ntiles] outboxes (the transport fills it)
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
+  // closing pellet update (k_pel_update): killed buffer indices, staged (bucket << 32 | index)
+  // keys -- both sorted by k_spawn_plan -- and the per-bucket counts that go with pstart
+  int *kill_list;     // [A][Pcap]
+  int64_t *stg_key;   // [A][2 Pcap] (second half: padding of a global-memory sort)
+  int64_t *pu_tmp;    // [A][2 Pcap] (kills sorted in global memory when LDS is too small)
+  int *pbc;           // [A][H] pellets per bucket of the current buffer
   double pow_n032[17];  // pow_glibc(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)
   int cshift_c;  // player-cell grid: smallest shift with <= 4096 cells (k_cgrid_count / k_cgrid_scatter)

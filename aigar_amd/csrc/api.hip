@@ -312,7 +312,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.OBcap = (int)std::min<size_t>(std::max<size_t>(1u << 20, 64 * NP), (size_t)1 << 24);
   AL(scan_state, unsigned long long, 2 * A * d.scan_tiles);
   AL(pl_state, unsigned long long, A * d.pl_tiles);
-  AL(ticket, int, 4);
+  AL(ticket, int, 16);
+  AL(kill_list, int, P); AL(stg_key, int64_t, 2 * P); AL(pu_tmp, int64_t, 2 * P); AL(pbc, int, A * d.H);
   AL(ob_used, unsigned long long, 1);
   AL(ob_epoch, uint32_t, 1);
   AL(p_split_lh, int, NP);
@@ -1137,6 +1138,9 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
         h2d(h, d.pel_seq[0] + po, ss) || h2d(h, d.pel_col[0] + po, sc))
       return -1;
     HIPCHK(hipMemcpyAsync(d.pstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
+    std::vector<int> cnt(d.H);  // per-bucket counts (the closing update keeps them with pstart)
+    for (int b = 0; b < d.H; b++) cnt[b] = start[b + 1] - start[b];
+    if (h2d(h, d.pbc + (size_t)arena * d.H, cnt)) return -1;
   }
   // blobs and viruses in list order; blob grid for completeness, virus grid for observations
   const size_t bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;

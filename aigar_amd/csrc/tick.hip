@@ -106,6 +106,36 @@ __device__ bool last_block(int *ticket, int nblocks) {
   __syncthreads();
   return s_last;
 }
+// The same for a wide grid: the tickets are sharded by blockIdx % 8 (tk[0..7]),
+// the last block of each shard takes a ticket of tk[8], so no counter sees more
+// than ~nblocks / 8 arrivals (one device-scope counter serialises them at
+// ~12 ns each, MI355X_MICROARCH.md row fanin).  Acquire / release between the
+// two levels chain the visibility from every block to the last one.
+__device__ bool last_block_sharded(int *tk, int nblocks) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int sh = blockIdx.x & 7, members = (nblocks - sh + 7) / 8, shards = min(8, nblocks);
+    int last = 0;
+    if (__hip_atomic_fetch_add(&tk[sh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __hip_atomic_store(&tk[sh], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (__hip_atomic_fetch_add(&tk[8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shards - 1) {
+        __hip_atomic_store(&tk[8], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = 1;
+      }
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last;
+}
 
 __device__ __forceinline__ void tile_out(const Dev &d, int32_t kind, int32_t idx, int64_t seq, double x, double y) {
   const int i = atomicAdd(&d.ctl[0].n_out, 1);
@@ -504,7 +534,10 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     s_epoch = __hip_atomic_load(&c.pl_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_seq0 = c.seq_next;
     s_blob0 = c.n_blob;
-    if (tile == 0) c.rmax_cell = 0;  // the cell grid's radius bound restarts (re-maxed by its build)
+    if (tile == 0) {
+      c.rmax_cell = 0;  // the cell grid's radius bound restarts (re-maxed by its build)
+      c.n_kill = 0;     // this tick's pellet kills (read by the last tick's closing update, done by now)
+    }
   }
   const int p = tile * 256 + tid, gp = a * d.B + p;
   int nn = 0, nb = 0;
@@ -875,6 +908,7 @@ __global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, in
   for (int j = 0; j < LB_PER; j++) {
     int i = base + j;
     v[j] = i < n ? c[i] + (c2 ? c2[i] : 0) : 0;
+    if (pfix && i < n) d.pbc[(size_t)a * d.H + i] = v[j];  // pellets: the bucket counts kept with pstart
     sum += v[j];
   }
 #pragma unroll
@@ -1090,6 +1124,112 @@ __global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode, int fov_
   if ((int)blockIdx.x >= nsc) return fov_cache_thread(d, (blockIdx.x - nsc) * 256 + threadIdx.x);
   pgrid_scatter_one(d, GTID, mode);
 }
+// step 2 of the closing pellet update (see pellet_close_prep): blocks
+// [arena][pellet blocks | bucket blocks] + the FOV cache as extra blocks.  A
+// pellet thread moves one buffer record (or drops an eaten one and clears its
+// flag); a bucket thread rewrites its bucket's start and count and moves its
+// staged records behind the survivors.  Every thread issues its own loads
+// before the block fetches K and S into LDS (short lists; long ones are
+// searched in global memory), so the launch is one round of loads.  No
+// epilogue: k_spawn_plan already closed the counts; block 0 advances the tick.
+constexpr int PU_SH = 2048;
+__device__ __forceinline__ int count_below_i32(const int *v, int n, int x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (v[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+__device__ __forceinline__ int count_below_i64(const int64_t *v, int n, int64_t x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (v[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
+  __shared__ int s_kill[PU_SH];
+  __shared__ int64_t s_stg[PU_SH];
+  const int per = nbP + nbB, nup = d.A * per;
+  if ((int)blockIdx.x >= nup) return fov_cache_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
+  const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
+  ArenaCtl &c = d.ctl[a];
+  const int nk = c.n_kill, ns = c.n_stg, n0 = c.pu_n0, nconv = c.pu_nconv;
+  const int src = c.pu_src, dst = src ^ 1;
+  const size_t P0 = (size_t)a * d.Pcap;
+  // this thread's record (pellet blocks) or bucket (bucket blocks), loaded first
+  const bool pel = blk < nbP;
+  const int i = pel ? blk * 256 + tid : (blk - nbP) * 256 + tid;
+  const size_t g = P0 + i;
+  bool dead = false;
+  double x = 0, y = 0, m = 0;
+  int64_t sq = 0;
+  int col = -1, s0 = 0, c0 = 0;
+  if (pel && i < n0) {
+    dead = d.pel_dead[g];
+    x = d.pel_x[src][g];
+    y = d.pel_y[src][g];
+    m = d.pel_m[src][g];
+    sq = d.pel_seq[src][g];
+    col = d.pel_col[src][g];
+  } else if (!pel && i < d.H) {
+    s0 = d.pstart[(size_t)a * (d.H + 1) + i];
+    c0 = d.pbc[(size_t)a * d.H + i];
+  }
+  const int *kl = d.kill_list + P0;
+  const int64_t *sk = d.stg_key + 2 * P0;
+  const bool kin = nk <= PU_SH, sin = ns <= PU_SH;
+  if (kin)
+    for (int t = tid; t < nk; t += 256) s_kill[t] = kl[t];
+  if (sin)
+    for (int t = tid; t < ns; t += 256) s_stg[t] = sk[t];
+  __syncthreads();
+  const int *K = kin ? s_kill : kl;
+  const int64_t *S = sin ? s_stg : sk;
+  if (pel) {
+    if (i < n0) {
+      if (dead) {
+        d.pel_dead[g] = 0;  // eaten: dropped (the flags stay clean for the next eat phase)
+      } else {
+        const int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+        const int pos = i - count_below_i32(K, nk, i) + count_below_i64(S, ns, (int64_t)b << 32);
+        if (pos < d.Pcap) {
+          const size_t o = P0 + pos;
+          d.pel_x[dst][o] = x;
+          d.pel_y[dst][o] = y;
+          d.pel_m[dst][o] = m;
+          d.pel_seq[dst][o] = sq;
+          d.pel_col[dst][o] = col;
+        }
+      }
+    } else if (i < n0 + nconv) {
+      d.pel_dead[g] = 0;  // (a blob conversion eaten in the eat phase)
+    }
+    if (blk == 0 && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
+  } else if (i < d.H) {
+    const int k0 = count_below_i32(K, nk, s0), k1 = count_below_i32(K, nk, s0 + c0);
+    const int j0 = count_below_i64(S, ns, (int64_t)i << 32), j1 = count_below_i64(S, ns, (int64_t)(i + 1) << 32);
+    const int start = s0 - k0 + j0, surv = c0 - (k1 - k0);
+    for (int r = j0; r < j1; r++) {
+      const size_t gs = P0 + (size_t)(S[r] & 0xFFFFFFFFll);
+      const int pos = start + surv + (r - j0);
+      if (pos >= d.Pcap) continue;
+      const size_t o = P0 + pos;
+      d.pel_x[dst][o] = d.pn_x[gs];
+      d.pel_y[dst][o] = d.pn_y[gs];
+      d.pel_m[dst][o] = d.pn_m[gs];
+      d.pel_seq[dst][o] = d.pn_seq[gs];
+      d.pel_col[dst][o] = d.pn_col[gs];
+    }
+    d.pstart[(size_t)a * (d.H + 1) + i] = start;
+    d.pbc[(size_t)a * d.H + i] = surv + (j1 - j0);
+  }
+}
+
 // ------------------------------------------------------------ T10 merge
 __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
   if (gp >= d.NP || !d.p_alive[gp]) return;
@@ -1484,6 +1624,13 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 // rebuild, so no rebuild runs before the eat phase); blobs kBlobBit | slot.
 // Pellet dead flags and reservation words are indexed by a * Pcap + j.
 constexpr int kBlobBit = 1 << 30;
+// a buffer pellet killed this tick, for the closing update (duplicates -- a tile
+// applying a kill its own eat phase made -- are dropped when the list is sorted)
+__device__ __forceinline__ void note_kill(const Dev &d, int a, int j) {
+  const int k = atomicAdd(&d.ctl[a].n_kill, 1);
+  if (k < d.Pcap) d.kill_list[(size_t)a * d.Pcap + k] = j;
+  else set_err(d, a, ERR_PELLET_CAP);
+}
 struct Food {
   const Dev &d;
   int a, pb;  // pb: the eat-phase pellet buffer (ArenaCtl::peat)
@@ -1506,6 +1653,7 @@ struct Food {
   __device__ void kill(int j) const {
     if (!blob(j)) {
       d.pel_dead[g(j)] = 1;
+      if (j < n0) note_kill(d, a, j);  // (a staged record is dropped by its flag)
     } else {
       d.b_flags[gb(j)] = 0;
       atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
@@ -2303,18 +2451,225 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
 
 __device__ void spawn_counts(const Dev &d, int a, int init);
 constexpr int OCC_LDS = 4096;  // occupancy words kept in LDS (32 KiB: fields up to 10240 units)
+// ---------------------------------------------------- closing pellet update
+// Pellets never move and only a few change per tick (eaten, spawned, converted
+// from blobs), so the end-of-tick pellet layout (bucket-sorted, double buffered)
+// is an update, not a re-sort: with K = the killed buffer indices and S = the
+// joining staged records' (bucket, index) keys, both sorted,
+//   survivor i of bucket b:  i - |K < i| + |S in buckets < b|
+//   bucket b's new start:    start(b) - |K < start(b)| + |S in buckets < b|
+// and bucket b's staged records follow its survivors.  k_spawn_plan builds and
+// sorts K and S; k_pel_update moves every record and rewrites every bucket's
+// start and count in one launch (no scan).
+__device__ void spawn_pellet_at(const Dev &d, int a, int j, double *px, double *py);
+// bitonic sort of v[0..n) ascending by the whole block (v: LDS or global, with
+// room for n rounded up to a power of two)
+__device__ void block_bitonic_i64(int64_t *v, int n) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int i = n + tid; i < np2; i += T) v[i] = INT64_MAX;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < np2 / 2; t += T) {
+        const int i = 2 * j * (t / j) + (t % j), l = i + j;
+        const int64_t x = v[i], y = v[l];
+        if ((x > y) == ((i & k) == 0)) {
+          v[i] = y;
+          v[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+__device__ __forceinline__ int pow2_at_least(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+// ascending bitonic sort of one value per lane across the wavefront (64 lanes)
+__device__ __forceinline__ int64_t wave_sort_i64(int64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int64_t o = __shfl_xor(v, j);
+      const bool lower = (lane & j) == 0, up = (lane & k) == 0;
+      v = (lower == up) ? (v < o ? v : o) : (v < o ? o : v);
+    }
+  return v;
+}
+// step 1, one block per arena after the spawn counts: this tick's pellet spawns
+// into the staging list (spawnPellets, field.py:258-265); the staged records that
+// join the buffer -- blob conversions nobody ate, spawns (tiles: those in the
+// held range) -- as sorted (bucket << 32 | staging index) keys; the killed
+// buffer indices sorted and made unique.  Then the tick's pellet bookkeeping
+// closes here (the update reads pu_*): new count, staging emptied, the buffer
+// the update builds made current.  The tick counter advances in k_pel_update
+// (k_spawn_all's respawns and events still key on it).  lds: 4096 free int64.
+constexpr int PU_LDS = 4096;
+__device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
+  ArenaCtl &c = d.ctl[a];
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int n0 = c.n_pel, nconv = c.n_pnew, nsp = c.n_spawn_p, nst = nconv + nsp;
+  const int nk_raw = min(c.n_kill, d.Pcap);
+  int *kl = d.kill_list + (size_t)a * d.Pcap;
+  int64_t *key = d.stg_key + (size_t)a * 2 * d.Pcap;
+  __shared__ int s_n[2];
+  if (nst <= 64 && nk_raw <= 64) {
+    // the usual tick (a few dozen changes): wave 0 alone, sorts in registers, no
+    // block barriers
+    if (tid < 64) {
+      bool live = false;
+      int64_t k = INT64_MAX;
+      if (tid < nst) {
+        double x, y;
+        if (tid < nconv) {
+          const size_t g = (size_t)a * d.Pcap + tid;
+          x = d.pn_x[g];
+          y = d.pn_y[g];
+          live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
+        } else {
+          spawn_pellet_at(d, a, tid - nconv, &x, &y);
+          live = true;
+        }
+        const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
+        live = live && tile_holds_bucket(d, bx, by);
+        if (live) k = ((int64_t)(by * d.cols + bx) << 32) | tid;
+      }
+      const int64_t kv = wave_sort_i64(tid < nk_raw ? (int64_t)kl[tid] : INT64_MAX);
+      k = wave_sort_i64(k);  // (dead / absent keys sort last)
+      const int ns = __popcll(__ballot(live));
+      if (tid < ns) key[tid] = k;
+      const int64_t prev = __shfl_up(kv, 1);
+      const bool keep = tid < nk_raw && (tid == 0 || kv != prev);
+      const unsigned long long kb = __ballot(keep);
+      if (keep) kl[__popcll(kb & ((1ull << tid) - 1))] = (int)kv;
+      if (tid == 0) {
+        s_n[0] = ns;
+        s_n[1] = __popcll(kb);
+      }
+    }
+  } else if (nst <= T && nk_raw <= T && nk_raw <= PU_LDS / 2) {
+    // one round of loads: the thread's staged record (a spawn is made here, in
+    // registers) and killed index; keys into LDS, both lists sorted there
+    int64_t *ks = lds, *kk = lds + PU_LDS / 2;
+    bool live = false;
+    int64_t k = 0, kv = INT64_MAX;
+    if (tid < nst) {
+      double x, y;
+      if (tid < nconv) {
+        const size_t g = (size_t)a * d.Pcap + tid;
+        x = d.pn_x[g];
+        y = d.pn_y[g];
+        live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
+      } else {
+        spawn_pellet_at(d, a, tid - nconv, &x, &y);
+        live = true;
+      }
+      const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
+      live = live && tile_holds_bucket(d, bx, by);
+      k = ((int64_t)(by * d.cols + bx) << 32) | tid;
+    }
+    if (tid < nk_raw) kv = kl[tid];
+    int chunk;
+    const int pos = block_rank(live, sh, &chunk);
+    if (live) ks[pos] = k;
+    if (tid < nk_raw) kk[tid] = kv;
+    const int ns = chunk;
+    block_bitonic_i64(ks, ns);
+    block_bitonic_i64(kk, nk_raw);
+    const bool keep = tid < nk_raw && (tid == 0 || kk[tid] != kk[tid - 1]);
+    int nu;
+    const int upos = block_rank(keep, sh, &nu);
+    if (keep) kl[upos] = (int)kk[tid];
+    if (tid < ns) key[tid] = ks[tid];
+    if (tid == 0) {
+      s_n[0] = ns;
+      s_n[1] = nu;
+    }
+  } else {  // many changes this tick: the same in passes, sorts in global memory when large
+    for (int j = tid; j < nsp; j += T) spawn_pellet_at(d, a, j, nullptr, nullptr);
+    __syncthreads();
+    int ns = 0;
+    for (int j0 = 0; j0 < nst; j0 += T) {
+      const int j = j0 + tid;
+      bool live = false;
+      int64_t k = 0;
+      if (j < nst) {
+        const size_t g = (size_t)a * d.Pcap + j;
+        const int bx = center_bucket_coord(d.pn_x[g], d.cols), by = center_bucket_coord(d.pn_y[g], d.cols);
+        live = !(j < nconv && d.pel_dead[(size_t)a * d.Pcap + n0 + j]) && tile_holds_bucket(d, bx, by);
+        k = ((int64_t)(by * d.cols + bx) << 32) | j;
+      }
+      int chunk;
+      const int pos = ns + block_rank(live, sh, &chunk);
+      if (live) key[pos] = k;
+      ns += chunk;
+    }
+    __syncthreads();
+    if (pow2_at_least(ns) <= PU_LDS) {
+      for (int i = tid; i < ns; i += T) lds[i] = key[i];
+      block_bitonic_i64(lds, ns);
+      for (int i = tid; i < ns; i += T) key[i] = lds[i];
+    } else {
+      block_bitonic_i64(key, ns);
+    }
+    __syncthreads();
+    int64_t *kb = pow2_at_least(nk_raw) <= PU_LDS ? lds : d.pu_tmp + (size_t)a * 2 * d.Pcap;
+    for (int i = tid; i < nk_raw; i += T) kb[i] = kl[i];
+    block_bitonic_i64(kb, nk_raw);
+    int nu = 0;
+    for (int i0 = 0; i0 < nk_raw; i0 += T) {
+      const int i = i0 + tid;
+      const bool keep = i < nk_raw && (i == 0 || kb[i] != kb[i - 1]);
+      int chunk;
+      const int pos = nu + block_rank(keep, sh, &chunk);
+      if (keep) kl[pos] = (int)kb[i];
+      nu += chunk;
+    }
+    if (tid == 0) {
+      s_n[0] = ns;
+      s_n[1] = nu;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int ns = s_n[0], nu = s_n[1], nn = n0 - nu + ns;
+    c.n_stg = ns;
+    c.n_kill = nu;
+    c.pu_src = c.peat;
+    c.pu_n0 = n0;
+    c.pu_nconv = nconv;
+    if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
+    c.n_pel = min(nn, d.Pcap);
+    d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
+    c.n_pnew = 0;
+    c.n_pel_eaten = 0;
+    c.pcur = c.peat ^ 1;
+    c.peat = c.pcur;  // the next eat phase reads the buffer built by the update
+  }
+  __syncthreads();
+}
+
 // pp (tick only): playerPlayerOverlap's serial pass first, by wave 0 of the
 // arena's block (its pending bitmap in the dynamic LDS)
-__global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *scr_k, int *scr_v, int pp) {
+// close (tick only): then the closing pellet update's step 1 (pellet_close_prep)
+__global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *scr_k, int *scr_v, int pp,
+                                                     int close) {
   __shared__ int sflag[1024];
   __shared__ int gcnt[SG_CAP + 1];
   __shared__ unsigned long long s_occ[OCC_LDS];
+  PT_BEGIN(5);
   int a = blockIdx.x;
   if (pp) {
     extern __shared__ uint32_t pend[];
     if (threadIdx.x < 64) pp_serial_body(d, a, scr_k, scr_v, pend);
     __syncthreads();
   }
+  PT_MARK(5, 1);
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
   // order-preserving compaction of viruses and blobs (list order == creation order),
@@ -2376,7 +2731,9 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   // (membership stays the F_INHASH flag; the viruses spawned below are not hashed)
   // (unchanged otherwise: viruses do not move after updateViruses, and the ones
   // appended by splits or spawns are not hashed this tick)
+  PT_MARK(5, 2);
   if (d.virus_enabled && (dirty & DIRTY_VIRUS)) grid_small_build<2>(d, a, gcnt, sflag);
+  PT_MARK(5, 3);
   __shared__ int s_spawn;
   if (tid == 0) {
     spawn_counts(d, a, init);
@@ -2411,6 +2768,12 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
     if (lds)
       for (int i = tid; i < W; i += T) gocc[i] = s_occ[i];
   }
+  PT_MARK(5, 4);
+  if (close) {  // (s_occ is free again: its 32 KiB hold the sorts)
+    __syncthreads();
+    pellet_close_prep(d, a, (int64_t *)s_occ, sflag);
+  }
+  PT_MARK(5, 5);
 }
 
 // spawnStuff's counts (field.py:227-280): pellets and viruses to add, players to respawn
@@ -2473,6 +2836,34 @@ __global__ void k_pnew_commit(Dev d) {
   d.ctl[a].n_pnew += d.ctl[a].n_spawn_p;
 }
 
+// spawn j of this tick (j < n_spawn_p): its record, a function of (key, counter) only
+__device__ __forceinline__ void spawn_pellet_rec(const Dev &d, const ArenaCtl &c, int j, double &x, double &y,
+                                                 double &m, int64_t &seq) {
+  uint64_t u[4];
+  philox(c.ctr_pellet_base + j, ST_PELLET, 0, 0, c.key0, c.key1, u);
+  x = (double)(int64_t)mulhi(u[0], (uint64_t)d.size);
+  y = (double)(int64_t)mulhi(u[1], (uint64_t)d.size);
+  const int64_t sr = (int64_t)mulhi(u[2], 50);
+  m = (sr > 50 - 4) ? (double)(50 - sr) : 1.0;  // randomSize (field.py:20-26)
+  seq = c.seq_base_spawn + j;
+}
+// ... into the staging list; its position also to *px, *py
+__device__ void spawn_pellet_at(const Dev &d, int a, int j, double *px, double *py) {
+  const ArenaCtl &c = d.ctl[a];
+  double x, y, m;
+  int64_t seq;
+  spawn_pellet_rec(d, c, j, x, y, m, seq);
+  size_t o = (size_t)a * d.Pcap + c.n_pnew + j;
+  d.pn_x[o] = x;
+  d.pn_y[o] = y;
+  d.pn_m[o] = m;
+  d.pn_seq[o] = seq;
+  d.pn_col[o] = -1;  // Cell(..., None): a colour of its own
+  if (px) {
+    *px = x;
+    *py = y;
+  }
+}
 __device__ __forceinline__ void spawn_pellet(const Dev &d, int gi, bool rank_staged) {
   if (gi >= d.A * d.Pcap) return;
   int a = gi / d.Pcap, j = gi - a * d.Pcap;
@@ -2562,10 +2953,16 @@ __global__ void k_spawn_players(Dev d, int init) { spawn_player(d, GTID, init); 
 // | viruses | pellet buckets]: the three spawn lists are independent (their
 // counts and sequence bases come from k_spawn_plan), and the survivor counts of
 // the closing pellet rebuild only read the eat-phase buffer.
-__global__ void __launch_bounds__(256) k_spawn_all(Dev d) {
+// inc (the tick): the pellets are spawned and joined by the closing update
+// (k_spawn_plan, k_pel_update): only players and viruses here
+__global__ void __launch_bounds__(256) k_spawn_all(Dev d, int inc) {
   int gi = GTID;
   if (gi < d.NP) return spawn_player(d, gi, 0);
   gi -= d.NP;
+  if (inc) {
+    if (d.virus_enabled && gi < d.A * d.Vcap) spawn_virus(d, gi);
+    return;
+  }
   if (gi < d.A * d.Pcap) {
     const int a = gi / d.Pcap, j = gi - a * d.Pcap;
     const ArenaCtl &c = d.ctl[a];
@@ -2598,6 +2995,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.n_dead = 0;
   c.n_ev = 0;
   c.n_pend = c.n_pend2 = 0;
+  c.n_kill = c.n_stg = 0;
   c.err = c.warn = 0;
   c.rmax_cell = radius_of(kStartMass);
   c.rmax_virus = radius_of(kVirusBase);
@@ -2671,18 +3069,18 @@ void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, co
 // the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
-  // playerPlayerOverlap's serial pass + spawnStuff's plan + the end-of-tick virus grid
+  // playerPlayerOverlap's serial pass + spawnStuff's plan + the end-of-tick virus
+  // grid + the closing pellet update's sorted kill / join lists (and the pellet spawns)
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, 0, scr_k,
-                     scr_v, 1);
-  const long n_spawn = (long)d.NP + (long)d.A * d.Pcap + (d.virus_enabled ? (long)d.A * d.Vcap : 0) +
-                       (long)d.A * d.H;
-  hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d);
-  // closing pellet rebuild (eat-phase survivors U spawns -> the new current
-  // buffer; the scan's epilogue closes the tick); the FOV cache runs as extra
-  // blocks of its scatter (player state is final by then).  Fused into the
-  // scatter's own threads it stretched that kernel ~5x; as separate blocks it
-  // only adds them to the grid.
-  launch_pellet_rebuild(d, s, PR_CLOSE);
+                     scr_v, 1, 1);
+  const long n_spawn = (long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0);
+  hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d, 1);  // players, viruses
+  // the closing pellet update (survivors U joining staged records -> the new
+  // current buffer, the last block closes the tick); the FOV cache runs as extra
+  // blocks (player state is final by then: fused into the pellet threads it
+  // stretched the kernel, as separate blocks it only adds them to the grid)
+  const int nbP = nblk(d.Pcap, 256), nbB = nblk(d.H, 256);
+  hipLaunchKernelGGL(k_pel_update, dim3(d.A * (nbP + nbB) + nblk(d.NP, 256)), dim3(256), 0, s, d, nbP, nbB);
 }
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   launch_tick_pre(d, s, scr_k, scr_v, rp);
@@ -2765,6 +3163,7 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
       for (int t = lo; t < hi; t++)
         if (d.pel_seq[F.pb][F.g(t)] == r.seq) {
           d.pel_dead[F.g(t)] = 1;
+          note_kill(d, 0, t);
           return;
         }
       for (int j = F.n0; j < F.n0 + F.nst; j++)  // this tick's blob conversions (staged)
@@ -2817,7 +3216,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.pl_state, 0, sizeof(unsigned long long) * (size_t)d.A * d.pl_tiles, s);
   hipLaunchKernelGGL(k_init_ctl, dim3(nblk(d.A, 64)), dim3(64), 0, s, d, seed);
   (void)hipMemsetAsync(d.occ, 0, sizeof(unsigned long long) * (size_t)d.A * d.occ_words, s);
-  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1, (int64_t *)nullptr, (int *)nullptr, 0);
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), 0, s, d, 1, (int64_t *)nullptr, (int *)nullptr, 0, 0);
   hipLaunchKernelGGL(k_spawn_players, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, 1);
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
