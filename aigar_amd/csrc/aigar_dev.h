@@ -52,6 +52,7 @@ struct ArenaCtl {
   int n_kill;      // buffer pellets killed this tick (kill_list; sorted + unique after k_spawn_plan)
   int n_stg;       // staged records joining the buffer at the closing update (stg_key)
   int pu_src, pu_n0, pu_nconv;  // the closing update's source buffer, its count, blob conversions
+  int pu_small;  // a usual tick: k_pel_update builds the short lists (n_kill raw) and closes the counts
   int pcur;           // pellet buffer holding the current (end-of-tick) pellets
   int peat;           // pellet buffer of this tick's eat phase (pcur when nothing was converted)
   uint32_t dirty;     // DIRTY_*: a virus / blob died this tick (k_spawn_plan compacts)
@@ -105,6 +106,7 @@ struct Dev {
   // closing pellet update (k_pel_update): killed buffer indices, staged (bucket << 32 | index)
   // keys -- both sorted by k_spawn_plan -- and the per-bucket counts that go with pstart
   int *kill_list;     // [A][Pcap]
+  double *spec_x, *spec_y, *spec_m;  // [A][64] this tick's first pellet spawns, drawn ahead (k_tick_begin)
   int64_t *stg_key;   // [A][2 Pcap] (second half: padding of a global-memory sort)
   int64_t *pu_tmp;    // [A][2 Pcap] (kills sorted in global memory when LDS is too small)
   int *pbc;           // [A][H] pellets per bucket of the current buffer
@@ -168,7 +170,8 @@ struct Dev {
   int *ccnt, *cstart, *citems, *c_rank;
   int *cgcnt;  // [A][2][4100] coarse cell-grid counts (<= 4096 cells), by tick parity
   // occupancy bitmap of the player hash [A][ceil(H/64)]
-  unsigned long long *occ;
+  unsigned long long *occ;  // getSpawnPos occupancy: one bit per fine bucket a live player cell touches
+  int *occ_cnt;             // ... and the number of such cells per bucket (k_pp_active, kept by the pp pass)
   int occ_words;
   // dead list [NP], worklists [A*Wcap]
   int *dead;

@@ -301,7 +301,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(vcnt, int, A * H1); AL(vstart, int, A * H1); AL(vitems, int, V); AL(v_rank, int, V);
   AL(ccnt, int, A * H1); AL(cstart, int, A * H1); AL(citems, int, C); AL(c_rank, int, C);
   AL(cgcnt, int, A * 2 * 4100);
-  AL(occ, unsigned long long, A * d.occ_words);
+  AL(occ, unsigned long long, A * d.occ_words); AL(occ_cnt, int, A * d.H);
   AL(dead, int, NP); AL(work, int, A * d.Wcap); AL(work2, int, A * d.Wcap);
   AL(f_list, int, C * FCAP); AL(f_cnt, uint8_t, C); AL(f_done, uint8_t, C);
   AL(respawn_list, int, NP);
@@ -313,7 +313,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(scan_state, unsigned long long, 2 * A * d.scan_tiles);
   AL(pl_state, unsigned long long, A * d.pl_tiles);
   AL(ticket, int, 16);
-  AL(kill_list, int, P); AL(stg_key, int64_t, 2 * P); AL(pu_tmp, int64_t, 2 * P); AL(pbc, int, A * d.H);
+  AL(kill_list, int, P); AL(spec_x, double, A * 64); AL(spec_y, double, A * 64); AL(spec_m, double, A * 64); AL(stg_key, int64_t, 2 * P); AL(pu_tmp, int64_t, 2 * P); AL(pbc, int, A * d.H);
   AL(ob_used, unsigned long long, 1);
   AL(ob_epoch, uint32_t, 1);
   AL(p_split_lh, int, NP);

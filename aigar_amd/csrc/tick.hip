@@ -422,9 +422,28 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
 
 // updateViruses + updateBlobs + the per-cell part of updatePlayers in one
 // launch: thread ranges [cell slots | viruses | blobs] (independent, field.py:94-119)
+// the first kSpawnAhead pellet spawns of this tick, drawn now: their counter
+// (ctr_pellet) is fixed before spawnStuff counts them, and a 64-bit Philox on the
+// closing update's path would cost more than all its loads
+constexpr int kSpawnAhead = 64;
+__device__ void spawn_ahead(const Dev &d, int a, int j) {
+  const ArenaCtl &c = d.ctl[a];
+  uint64_t u[4];
+  philox(c.ctr_pellet + j, ST_PELLET, 0, 0, c.key0, c.key1, u);
+  const int64_t sr = (int64_t)mulhi(u[2], 50);
+  const size_t o = (size_t)a * kSpawnAhead + j;
+  d.spec_x[o] = (double)(int64_t)mulhi(u[0], (uint64_t)d.size);
+  d.spec_y[o] = (double)(int64_t)mulhi(u[1], (uint64_t)d.size);
+  d.spec_m[o] = (sr > 50 - 4) ? (double)(50 - sr) : 1.0;  // randomSize (field.py:20-26)
+}
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   PT_BEGIN(2);
   int gi = GTID;
+  {  // the spawn occupancy restarts (k_pp_active rebuilds it; the last reader was the previous tick's spawns)
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = gi; i < (long)d.A * d.H; i += stride) d.occ_cnt[i] = 0;
+    for (long i = gi; i < (long)d.A * d.occ_words; i += stride) d.occ[i] = 0;
+  }
   if (gi < kMaxCells * d.NP) {
     update_cell(d, gi, rp PT_ARGS);
     PT_MARK(2, 1);
@@ -438,7 +457,9 @@ __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
     }
     gi -= d.A * d.Vcap;
   }
-  if (gi < d.A * d.Ecap) update_blob(d, gi);
+  if (gi < d.A * d.Ecap) return update_blob(d, gi);
+  gi -= d.A * d.Ecap;
+  if (gi < d.A * kSpawnAhead) spawn_ahead(d, gi / kSpawnAhead, gi % kSpawnAhead);
 }
 
 // rank of this thread among the flagged threads of the block (thread order);
@@ -1124,112 +1145,6 @@ __global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode, int fov_
   if ((int)blockIdx.x >= nsc) return fov_cache_thread(d, (blockIdx.x - nsc) * 256 + threadIdx.x);
   pgrid_scatter_one(d, GTID, mode);
 }
-// step 2 of the closing pellet update (see pellet_close_prep): blocks
-// [arena][pellet blocks | bucket blocks] + the FOV cache as extra blocks.  A
-// pellet thread moves one buffer record (or drops an eaten one and clears its
-// flag); a bucket thread rewrites its bucket's start and count and moves its
-// staged records behind the survivors.  Every thread issues its own loads
-// before the block fetches K and S into LDS (short lists; long ones are
-// searched in global memory), so the launch is one round of loads.  No
-// epilogue: k_spawn_plan already closed the counts; block 0 advances the tick.
-constexpr int PU_SH = 2048;
-__device__ __forceinline__ int count_below_i32(const int *v, int n, int x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int m = (lo + hi) >> 1;
-    if (v[m] < x) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
-}
-__device__ __forceinline__ int count_below_i64(const int64_t *v, int n, int64_t x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int m = (lo + hi) >> 1;
-    if (v[m] < x) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
-}
-__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
-  __shared__ int s_kill[PU_SH];
-  __shared__ int64_t s_stg[PU_SH];
-  const int per = nbP + nbB, nup = d.A * per;
-  if ((int)blockIdx.x >= nup) return fov_cache_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
-  const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
-  ArenaCtl &c = d.ctl[a];
-  const int nk = c.n_kill, ns = c.n_stg, n0 = c.pu_n0, nconv = c.pu_nconv;
-  const int src = c.pu_src, dst = src ^ 1;
-  const size_t P0 = (size_t)a * d.Pcap;
-  // this thread's record (pellet blocks) or bucket (bucket blocks), loaded first
-  const bool pel = blk < nbP;
-  const int i = pel ? blk * 256 + tid : (blk - nbP) * 256 + tid;
-  const size_t g = P0 + i;
-  bool dead = false;
-  double x = 0, y = 0, m = 0;
-  int64_t sq = 0;
-  int col = -1, s0 = 0, c0 = 0;
-  if (pel && i < n0) {
-    dead = d.pel_dead[g];
-    x = d.pel_x[src][g];
-    y = d.pel_y[src][g];
-    m = d.pel_m[src][g];
-    sq = d.pel_seq[src][g];
-    col = d.pel_col[src][g];
-  } else if (!pel && i < d.H) {
-    s0 = d.pstart[(size_t)a * (d.H + 1) + i];
-    c0 = d.pbc[(size_t)a * d.H + i];
-  }
-  const int *kl = d.kill_list + P0;
-  const int64_t *sk = d.stg_key + 2 * P0;
-  const bool kin = nk <= PU_SH, sin = ns <= PU_SH;
-  if (kin)
-    for (int t = tid; t < nk; t += 256) s_kill[t] = kl[t];
-  if (sin)
-    for (int t = tid; t < ns; t += 256) s_stg[t] = sk[t];
-  __syncthreads();
-  const int *K = kin ? s_kill : kl;
-  const int64_t *S = sin ? s_stg : sk;
-  if (pel) {
-    if (i < n0) {
-      if (dead) {
-        d.pel_dead[g] = 0;  // eaten: dropped (the flags stay clean for the next eat phase)
-      } else {
-        const int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-        const int pos = i - count_below_i32(K, nk, i) + count_below_i64(S, ns, (int64_t)b << 32);
-        if (pos < d.Pcap) {
-          const size_t o = P0 + pos;
-          d.pel_x[dst][o] = x;
-          d.pel_y[dst][o] = y;
-          d.pel_m[dst][o] = m;
-          d.pel_seq[dst][o] = sq;
-          d.pel_col[dst][o] = col;
-        }
-      }
-    } else if (i < n0 + nconv) {
-      d.pel_dead[g] = 0;  // (a blob conversion eaten in the eat phase)
-    }
-    if (blk == 0 && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
-  } else if (i < d.H) {
-    const int k0 = count_below_i32(K, nk, s0), k1 = count_below_i32(K, nk, s0 + c0);
-    const int j0 = count_below_i64(S, ns, (int64_t)i << 32), j1 = count_below_i64(S, ns, (int64_t)(i + 1) << 32);
-    const int start = s0 - k0 + j0, surv = c0 - (k1 - k0);
-    for (int r = j0; r < j1; r++) {
-      const size_t gs = P0 + (size_t)(S[r] & 0xFFFFFFFFll);
-      const int pos = start + surv + (r - j0);
-      if (pos >= d.Pcap) continue;
-      const size_t o = P0 + pos;
-      d.pel_x[dst][o] = d.pn_x[gs];
-      d.pel_y[dst][o] = d.pn_y[gs];
-      d.pel_m[dst][o] = d.pn_m[gs];
-      d.pel_seq[dst][o] = d.pn_seq[gs];
-      d.pel_col[dst][o] = d.pn_col[gs];
-    }
-    d.pstart[(size_t)a * (d.H + 1) + i] = start;
-    d.pbc[(size_t)a * d.H + i] = surv + (j1 - j0);
-  }
-}
-
 // ------------------------------------------------------------ T10 merge
 __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
   if (gp >= d.NP || !d.p_alive[gp]) return;
@@ -2156,7 +2071,45 @@ __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *
 // ------------------------------------------------------------ T16 player <- player
 __device__ __forceinline__ Rect cell_rect(const Dev &d, size_t ci) { return footprint(d.c_x[ci], d.c_y[ci], d.c_r[ci], d.size); }
 
+// getSpawnPos's occupancy (field.py:283-301: the buckets of the player hash that
+// hold a cell) as a per-bucket cell count plus the bit words spawn_pos scans.
+// k_pp_active adds every live cell's footprint; the pp pass keeps it exact
+// (a removed cell leaves its buckets, a grown one adds the buckets it reached),
+// so it describes the cells left when spawnStuff runs.  One bucket per lane.
+__device__ __forceinline__ void occ_add(const Dev &d, int a, Rect q) {
+  int *cnt = d.occ_cnt + (size_t)a * d.H;
+  unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
+  const int w = q.x1 - q.x0 + 1, n = w * (q.y1 - q.y0 + 1);
+  for (int t = threadIdx.x & 63; t < n; t += 64) {
+    const int b = (q.y0 + t / w) * d.cols + q.x0 + t % w;
+    atomicAdd(&cnt[b], 1);
+    atomicOr(&occ[b >> 6], 1ull << (b & 63));
+  }
+}
+// the buckets of q that old does not hold (old inside q: a radius grew in place)
+__device__ __forceinline__ void occ_grow(const Dev &d, int a, Rect old, Rect q) {
+  int *cnt = d.occ_cnt + (size_t)a * d.H;
+  unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
+  const int w = q.x1 - q.x0 + 1, n = w * (q.y1 - q.y0 + 1);
+  for (int t = threadIdx.x & 63; t < n; t += 64) {
+    const int bx = q.x0 + t % w, by = q.y0 + t / w;
+    if (bx >= old.x0 && bx <= old.x1 && by >= old.y0 && by <= old.y1) continue;
+    const int b = by * d.cols + bx;
+    if (atomicAdd(&cnt[b], 1) == 0) atomicOr(&occ[b >> 6], 1ull << (b & 63));
+  }
+}
+__device__ __forceinline__ void occ_remove(const Dev &d, int a, Rect q) {
+  int *cnt = d.occ_cnt + (size_t)a * d.H;
+  unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
+  const int w = q.x1 - q.x0 + 1, n = w * (q.y1 - q.y0 + 1);
+  for (int t = threadIdx.x & 63; t < n; t += 64) {
+    const int b = (q.y0 + t / w) * d.cols + q.x0 + t % w;
+    if (atomicSub(&cnt[b], 1) == 1) atomicAnd(&occ[b >> 6], ~(1ull << (b & 63)));
+  }
+}
+
 // one wavefront per player: cells with an overlapping enemy cell at phase start
+// (+ the player's cells into the spawn occupancy)
 __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   PT_BEGIN(3);
   const int lane = threadIdx.x & 63;
@@ -2174,6 +2127,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     PT_MARK(3, 2);
     Rect q = footprint(x, y, r, d.size);
+    occ_add(d, a, q);
     bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int e) {
       // only the LOWER-index player of a pair is marked: its turn comes first
       // and resolves the pair ("the one that can eat does", field.py:238-243).
@@ -2346,6 +2300,11 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         const double mr = radius_of(m);
         d.c_m[g] = m;
         d.c_r[g] = mr;
+        // the spawn occupancy follows: the eaten cell leaves, the eater's footprint grows
+        occ_remove(d, a, pc_eats ? footprint(ox, oy, orr, d.size) : footprint(px, py, pr, d.size));
+        wave_fence();
+        if (pc_eats) occ_grow(d, a, footprint(px, py, pr, d.size), footprint(px, py, mr, d.size));
+        else occ_grow(d, a, footprint(ox, oy, orr, d.size), footprint(ox, oy, mr, d.size));
         if (pc_eats) {
           pm = m;
           pr = mr;
@@ -2393,26 +2352,6 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
   c.rmax_cell = rmax;
 }
 
-// ------------------------------------------------------------ T17 occupancy
-__global__ void k_occupancy(Dev d) {
-  int gi = GTID;
-  int per = kMaxCells * d.B;
-  bool in = gi < d.A * per;
-  int a = in ? gi / per : 0, i = in ? gi - a * per : 0;
-  int slot = i / d.B, p = i - slot * d.B;
-  size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-  bool ok = in && (d.c_flags[g] & F_ALIVE);
-  wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? d.c_r[g] : 0.0);
-  if (!ok) return;
-  Rect r = cell_rect(d, g);
-  unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
-  for (int by = r.y0; by <= r.y1; by++)
-    for (int bx = r.x0; bx <= r.x1; bx++) {
-      int b = by * d.cols + bx;
-      atomicOr(&occ[b >> 6], 1ull << (b & 63));
-    }
-}
-
 // ------------------------------------------------------------ T18 spawn
 // getSpawnPos (field.py:283-301) with the player-hash occupancy bitmap
 __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4], double &ox, double &oy) {
@@ -2450,7 +2389,6 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
 }
 
 __device__ void spawn_counts(const Dev &d, int a, int init);
-constexpr int OCC_LDS = 4096;  // occupancy words kept in LDS (32 KiB: fields up to 10240 units)
 // ---------------------------------------------------- closing pellet update
 // Pellets never move and only a few change per tick (eaten, spawned, converted
 // from blobs), so the end-of-tick pellet layout (bucket-sorted, double buffered)
@@ -2507,7 +2445,8 @@ __device__ __forceinline__ int64_t wave_sort_i64(int64_t v) {
 // held range) -- as sorted (bucket << 32 | staging index) keys; the killed
 // buffer indices sorted and made unique.  Then the tick's pellet bookkeeping
 // closes here (the update reads pu_*): new count, staging emptied, the buffer
-// the update builds made current.  The tick counter advances in k_pel_update
+// the update builds made current.  A usual tick (<= 64 staged, <= 64 kills)
+// only hands over pu_*: k_pel_update's blocks sort the short lists themselves.  The tick counter advances in k_pel_update
 // (k_spawn_all's respawns and events still key on it).  lds: 4096 free int64.
 constexpr int PU_LDS = 4096;
 __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
@@ -2518,41 +2457,18 @@ __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
   int *kl = d.kill_list + (size_t)a * d.Pcap;
   int64_t *key = d.stg_key + (size_t)a * 2 * d.Pcap;
   __shared__ int s_n[2];
-  if (nst <= 64 && nk_raw <= 64) {
-    // the usual tick (a few dozen changes): wave 0 alone, sorts in registers, no
-    // block barriers
-    if (tid < 64) {
-      bool live = false;
-      int64_t k = INT64_MAX;
-      if (tid < nst) {
-        double x, y;
-        if (tid < nconv) {
-          const size_t g = (size_t)a * d.Pcap + tid;
-          x = d.pn_x[g];
-          y = d.pn_y[g];
-          live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
-        } else {
-          spawn_pellet_at(d, a, tid - nconv, &x, &y);
-          live = true;
-        }
-        const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
-        live = live && tile_holds_bucket(d, bx, by);
-        if (live) k = ((int64_t)(by * d.cols + bx) << 32) | tid;
-      }
-      const int64_t kv = wave_sort_i64(tid < nk_raw ? (int64_t)kl[tid] : INT64_MAX);
-      k = wave_sort_i64(k);  // (dead / absent keys sort last)
-      const int ns = __popcll(__ballot(live));
-      if (tid < ns) key[tid] = k;
-      const int64_t prev = __shfl_up(kv, 1);
-      const bool keep = tid < nk_raw && (tid == 0 || kv != prev);
-      const unsigned long long kb = __ballot(keep);
-      if (keep) kl[__popcll(kb & ((1ull << tid) - 1))] = (int)kv;
-      if (tid == 0) {
-        s_n[0] = ns;
-        s_n[1] = __popcll(kb);
-      }
+  if (nst <= 64 && nsp <= kSpawnAhead && nk_raw <= 64) {
+    // the usual tick (a few dozen changes): every k_pel_update block builds the
+    // short lists itself (pellet_lists_wave), which also closes the bookkeeping
+    if (tid == 0) {
+      c.pu_src = c.peat;
+      c.pu_n0 = n0;
+      c.pu_nconv = nconv;
+      c.pu_small = 1;
     }
-  } else if (nst <= T && nk_raw <= T && nk_raw <= PU_LDS / 2) {
+    return;
+  }
+  if (nst <= T && nk_raw <= T && nk_raw <= PU_LDS / 2) {
     // one round of loads: the thread's staged record (a spawn is made here, in
     // registers) and killed index; keys into LDS, both lists sorted there
     int64_t *ks = lds, *kk = lds + PU_LDS / 2;
@@ -2643,6 +2559,7 @@ __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
     c.pu_src = c.peat;
     c.pu_n0 = n0;
     c.pu_nconv = nconv;
+    c.pu_small = 0;
     if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
     c.n_pel = min(nn, d.Pcap);
     d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
@@ -2661,7 +2578,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
                                                      int close) {
   __shared__ int sflag[1024];
   __shared__ int gcnt[SG_CAP + 1];
-  __shared__ unsigned long long s_occ[OCC_LDS];
+  __shared__ int64_t s_sort[PU_LDS];
   PT_BEGIN(5);
   int a = blockIdx.x;
   if (pp) {
@@ -2734,44 +2651,13 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   PT_MARK(5, 2);
   if (d.virus_enabled && (dirty & DIRTY_VIRUS)) grid_small_build<2>(d, a, gcnt, sflag);
   PT_MARK(5, 3);
-  __shared__ int s_spawn;
-  if (tid == 0) {
-    spawn_counts(d, a, init);
-    s_spawn = !init && (c.n_spawn_pl > 0 || c.n_spawn_v > 0);
-  }
+  // (the spawn occupancy is built by k_pp_active and kept by the pp pass above)
+  if (tid == 0) spawn_counts(d, a, init);
   __syncthreads();
-  // player-hash occupancy for getSpawnPos (field.py:283-301): one bit per fine
-  // bucket a live player cell's footprint touches, built only when a player or
-  // a virus spawns this tick (in LDS when it fits, else with global atomics)
-  if (s_spawn) {
-    const int W = d.occ_words, NP = d.NP;
-    const bool lds = W <= OCC_LDS;
-    unsigned long long *gocc = d.occ + (size_t)a * W;
-    for (int i = tid; i < W; i += T) {
-      if (lds) s_occ[i] = 0;
-      else gocc[i] = 0;
-    }
-    __syncthreads();
-    for (int p = tid; p < d.B; p += T) {
-      const int gp = a * d.B + p, n = d.p_ncells[gp];
-      for (int k = 0; k < n; k++) {
-        const Rect r = cell_rect(d, (size_t)d.p_list[k * NP + gp] * NP + gp);
-        for (int by = r.y0; by <= r.y1; by++)
-          for (int bx = r.x0; bx <= r.x1; bx++) {
-            const int b = by * d.cols + bx;
-            if (lds) atomicOr(&s_occ[b >> 6], 1ull << (b & 63));
-            else atomicOr(&gocc[b >> 6], 1ull << (b & 63));
-          }
-      }
-    }
-    __syncthreads();
-    if (lds)
-      for (int i = tid; i < W; i += T) gocc[i] = s_occ[i];
-  }
   PT_MARK(5, 4);
-  if (close) {  // (s_occ is free again: its 32 KiB hold the sorts)
+  if (close) {
     __syncthreads();
-    pellet_close_prep(d, a, (int64_t *)s_occ, sflag);
+    pellet_close_prep(d, a, s_sort, sflag);
   }
   PT_MARK(5, 5);
 }
@@ -2949,6 +2835,194 @@ __device__ __forceinline__ void spawn_player(const Dev &d, int gi, int init) {
 }
 __global__ void k_spawn_players(Dev d, int init) { spawn_player(d, GTID, init); }
 
+// step 2 of the closing pellet update (see pellet_close_prep): blocks
+// [arena][pellet blocks | bucket blocks] + the FOV cache as extra blocks.  A
+// pellet thread moves one buffer record (or drops an eaten one and clears its
+// flag); a bucket thread rewrites its bucket's start and count and moves its
+// staged records behind the survivors.  Every thread issues its own loads
+// before the block fetches K and S into LDS (short lists; long ones are
+// searched in global memory), so the launch is one round of loads.  No
+// epilogue: k_spawn_plan already closed the counts; block 0 advances the tick.
+// A usual tick (pu_small): wave 0 of every block builds K and S itself from the
+// raw kill list, the blob conversions and this tick's spawns (drawn ahead by
+// k_tick_begin) -- a few dozen keys ranked in registers, the same in every
+// block -- and block 0 closes the bookkeeping.
+constexpr int PU_SH = 2048;
+// the short lists of a usual tick, by one wavefront: the staged keys (bucket <<
+// 32 | staging index) of the records that join, sorted, to S; the killed
+// indices sorted and unique to K; their counts to n[0], n[1]
+__device__ __forceinline__ void pellet_lists_wave(const Dev &d, const ArenaCtl &c, int a, int n0, int nconv, int nsp,
+                                                  int nk_raw, int *K, int64_t *S, int *n) {
+  const int tid = threadIdx.x;
+  const int nst = nconv + nsp;
+  const int *kl = d.kill_list + (size_t)a * d.Pcap;
+  const int kv = tid < nk_raw ? kl[tid] : INT_MAX;
+  bool live = false;
+  int bk = 0;
+  if (tid < nst) {
+    double x, y;
+    if (tid < nconv) {
+      const size_t g = (size_t)a * d.Pcap + tid;
+      x = d.pn_x[g];
+      y = d.pn_y[g];
+      live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
+    } else {  // (nsp <= kSpawnAhead)
+      const size_t o = (size_t)a * kSpawnAhead + tid - nconv;
+      x = d.spec_x[o];
+      y = d.spec_y[o];
+      live = true;
+    }
+    const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
+    live = live && tile_holds_bucket(d, bx, by);
+    bk = by * d.cols + bx;
+  }
+  // ranks by counting over the few live lanes (wave-uniform loops of lane reads:
+  // far shorter than a 64-wide sorting network of cross-lane permutes)
+  const unsigned long long lm = __ballot(live);
+  int rs = 0;
+  for (unsigned long long w = lm; w; w &= w - 1) {  // key order (bucket, staging index)
+    const int j = __ffsll((long long)w) - 1;
+    const int bj = __builtin_amdgcn_readlane(bk, j);
+    rs += bj < bk || (bj == bk && j < tid);
+  }
+  if (live) S[rs] = ((int64_t)bk << 32) | tid;
+  bool first = tid < nk_raw;
+  for (int j = 0; j < nk_raw; j++) first = first && !(j < tid && __builtin_amdgcn_readlane(kv, j) == kv);
+  const unsigned long long fm = __ballot(first);
+  int rk = 0;
+  for (unsigned long long w = fm; w; w &= w - 1) rk += __builtin_amdgcn_readlane(kv, __ffsll((long long)w) - 1) < kv;
+  if (first) K[rk] = kv;
+  if (tid == 0) {
+    n[0] = __popcll(lm);
+    n[1] = __popcll(fm);
+  }
+}
+__device__ __forceinline__ int count_below_i32(const int *v, int n, int x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (v[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+__device__ __forceinline__ int count_below_i64(const int64_t *v, int n, int64_t x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (v[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
+  __shared__ int s_kill[PU_SH];
+  __shared__ int64_t s_stg[PU_SH];
+  __shared__ int s_n[2];
+  const int per = nbP + nbB, nup = d.A * per;
+  if ((int)blockIdx.x >= nup) return fov_cache_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
+  const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
+  ArenaCtl &c = d.ctl[a];
+  const int small = c.pu_small, n0 = c.pu_n0, nconv = c.pu_nconv;
+  int nk = c.n_kill, ns = c.n_stg;
+  const int src = c.pu_src, dst = src ^ 1;
+  const size_t P0 = (size_t)a * d.Pcap;
+  // this thread's record (pellet blocks) or bucket (bucket blocks), loaded first
+  const bool pel = blk < nbP;
+  const int i = pel ? blk * 256 + tid : (blk - nbP) * 256 + tid;
+  const size_t g = P0 + i;
+  bool dead = false;
+  double x = 0, y = 0, m = 0;
+  int64_t sq = 0;
+  int col = -1, s0 = 0, c0 = 0;
+  if (pel && i < n0) {
+    dead = d.pel_dead[g];
+    x = d.pel_x[src][g];
+    y = d.pel_y[src][g];
+    m = d.pel_m[src][g];
+    sq = d.pel_seq[src][g];
+    col = d.pel_col[src][g];
+  } else if (!pel && i < d.H) {
+    s0 = d.pstart[(size_t)a * (d.H + 1) + i];
+    c0 = d.pbc[(size_t)a * d.H + i];
+  }
+  const int *kl = d.kill_list + P0;
+  const int64_t *sk = d.stg_key + 2 * P0;
+  if (small && tid < 64) pellet_lists_wave(d, c, a, n0, nconv, c.n_spawn_p, min(nk, d.Pcap), s_kill, s_stg, s_n);
+  const bool kin = small || nk <= PU_SH, sin = small || ns <= PU_SH;
+  if (!small) {
+    if (kin)
+      for (int t = tid; t < nk; t += 256) s_kill[t] = kl[t];
+    if (sin)
+      for (int t = tid; t < ns; t += 256) s_stg[t] = sk[t];
+  }
+  __syncthreads();
+  if (small) {
+    ns = s_n[0];
+    nk = s_n[1];
+    if (blk == 0 && tid == 0) {  // the tick's pellet bookkeeping (nothing in this launch reads it)
+      const int nn = n0 - nk + ns;
+      if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
+      c.n_pel = min(nn, d.Pcap);
+      d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
+      c.n_pnew = 0;
+      c.n_pel_eaten = 0;
+      c.pcur = dst;
+      c.peat = dst;  // the next eat phase reads the buffer built here
+    }
+  }
+  const int *K = kin ? s_kill : kl;
+  const int64_t *S = sin ? s_stg : sk;
+  if (pel) {
+    if (i < n0) {
+      if (dead) {
+        d.pel_dead[g] = 0;  // eaten: dropped (the flags stay clean for the next eat phase)
+      } else {
+        const int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
+        const int pos = i - count_below_i32(K, nk, i) + count_below_i64(S, ns, (int64_t)b << 32);
+        if (pos < d.Pcap) {
+          const size_t o = P0 + pos;
+          d.pel_x[dst][o] = x;
+          d.pel_y[dst][o] = y;
+          d.pel_m[dst][o] = m;
+          d.pel_seq[dst][o] = sq;
+          d.pel_col[dst][o] = col;
+        }
+      }
+    } else if (i < n0 + nconv) {
+      d.pel_dead[g] = 0;  // (a blob conversion eaten in the eat phase)
+    }
+    if (blk == 0 && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
+  } else if (i < d.H) {
+    const int k0 = count_below_i32(K, nk, s0), k1 = count_below_i32(K, nk, s0 + c0);
+    const int j0 = count_below_i64(S, ns, (int64_t)i << 32), j1 = count_below_i64(S, ns, (int64_t)(i + 1) << 32);
+    const int start = s0 - k0 + j0, surv = c0 - (k1 - k0);
+    for (int r = j0; r < j1; r++) {
+      const int js = (int)(S[r] & 0xFFFFFFFFll);
+      const int pos = start + surv + (r - j0);
+      if (pos >= d.Pcap) continue;
+      const size_t o = P0 + pos;
+      if (small && js >= nconv) {  // a spawn, drawn by k_tick_begin (k_spawn_plan did not stage it)
+        const size_t so = (size_t)a * kSpawnAhead + js - nconv;
+        d.pel_x[dst][o] = d.spec_x[so];
+        d.pel_y[dst][o] = d.spec_y[so];
+        d.pel_m[dst][o] = d.spec_m[so];
+        d.pel_seq[dst][o] = c.seq_base_spawn + (js - nconv);
+        d.pel_col[dst][o] = -1;
+        continue;
+      }
+      const size_t gs = P0 + js;
+      d.pel_x[dst][o] = d.pn_x[gs];
+      d.pel_y[dst][o] = d.pn_y[gs];
+      d.pel_m[dst][o] = d.pn_m[gs];
+      d.pel_seq[dst][o] = d.pn_seq[gs];
+      d.pel_col[dst][o] = d.pn_col[gs];
+    }
+    d.pstart[(size_t)a * (d.H + 1) + i] = start;
+    d.pbc[(size_t)a * d.H + i] = surv + (j1 - j0);
+  }
+}
+
 // spawnStuff (field.py:256-313) in one launch, thread ranges [players | pellets
 // | viruses | pellet buckets]: the three spawn lists are independent (their
 // counts and sequence bases come from k_spawn_plan), and the survivor counts of
@@ -3055,7 +3129,8 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 // overlap gains at this kernel size), so the graph stays linear.
 // the phases before the eat phase (field.py:94-198, 225-231, 246-253)
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
-  const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap;
+  const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap +
+                       (long)d.A * kSpawnAhead;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
   // + the virus grid (extra block) and the blob grid (last block) of updateHashTables
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + (d.virus_enabled ? 1 : 0), d.A), dim3(256), 0, s, d);
