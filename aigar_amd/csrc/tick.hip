@@ -1539,8 +1539,8 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 // rebuild, so no rebuild runs before the eat phase); blobs kBlobBit | slot.
 // Pellet dead flags and reservation words are indexed by a * Pcap + j.
 constexpr int kBlobBit = 1 << 30;
-// a buffer pellet killed this tick, for the closing update (duplicates -- a tile
-// applying a kill its own eat phase made -- are dropped when the list is sorted)
+// a buffer pellet killed this tick, for the closing update (each once: a tile
+// applying another tile's kill notes it only if its own eat phase did not)
 __device__ __forceinline__ void note_kill(const Dev &d, int a, int j) {
   const int k = atomicAdd(&d.ctl[a].n_kill, 1);
   if (k < d.Pcap) d.kill_list[(size_t)a * d.Pcap + k] = j;
@@ -2449,6 +2449,7 @@ __device__ __forceinline__ int64_t wave_sort_i64(int64_t v) {
 // only hands over pu_*: k_pel_update's blocks sort the short lists themselves.  The tick counter advances in k_pel_update
 // (k_spawn_all's respawns and events still key on it).  lds: 4096 free int64.
 constexpr int PU_LDS = 4096;
+constexpr int PU_SH = 2048;  // k_pel_update: kill / staged lists up to this length sit in LDS
 __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
@@ -2465,6 +2466,53 @@ __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
       c.pu_n0 = n0;
       c.pu_nconv = nconv;
       c.pu_small = 1;
+    }
+    return;
+  }
+  if (nst <= PU_SH && nk_raw <= PU_SH) {
+    // a busy tick (greedy crowds: hundreds of kills and spawns): the lists stay
+    // unsorted (the staged keys in staging order; kills are unique) and every
+    // k_pel_update block counts ranks over them in LDS -- no sorting network here
+    int ns = 0;
+    for (int j0 = 0; j0 < nst; j0 += T) {
+      const int j = j0 + tid;
+      bool live = false;
+      int64_t k = 0;
+      if (j < nst) {
+        double x, y;
+        if (j < nconv) {
+          const size_t g = (size_t)a * d.Pcap + j;
+          x = d.pn_x[g];
+          y = d.pn_y[g];
+          live = !d.pel_dead[(size_t)a * d.Pcap + n0 + j];
+        } else {
+          spawn_pellet_at(d, a, j - nconv, &x, &y);
+          live = true;
+        }
+        const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
+        live = live && tile_holds_bucket(d, bx, by);
+        k = ((int64_t)(by * d.cols + bx) << 32) | j;
+      }
+      int chunk;
+      const int pos = ns + block_rank(live, sh, &chunk);
+      if (live) key[pos] = k;
+      ns += chunk;
+    }
+    if (tid == 0) {
+      const int nn = n0 - nk_raw + ns;
+      c.n_stg = ns;
+      c.n_kill = nk_raw;
+      c.pu_src = c.peat;
+      c.pu_n0 = n0;
+      c.pu_nconv = nconv;
+      c.pu_small = 2;
+      if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
+      c.n_pel = min(nn, d.Pcap);
+      d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
+      c.n_pnew = 0;
+      c.n_pel_eaten = 0;
+      c.pcur = c.peat ^ 1;
+      c.peat = c.pcur;
     }
     return;
   }
@@ -2847,7 +2895,6 @@ __global__ void k_spawn_players(Dev d, int init) { spawn_player(d, GTID, init); 
 // raw kill list, the blob conversions and this tick's spawns (drawn ahead by
 // k_tick_begin) -- a few dozen keys ranked in registers, the same in every
 // block -- and block 0 closes the bookkeeping.
-constexpr int PU_SH = 2048;
 // the short lists of a usual tick, by one wavefront: the staged keys (bucket <<
 // 32 | staging index) of the records that join, sorted, to S; the killed
 // indices sorted and unique to K; their counts to n[0], n[1]
@@ -2915,6 +2962,112 @@ __device__ __forceinline__ int count_below_i64(const int64_t *v, int n, int64_t 
   }
   return lo;
 }
+// A busy tick's unsorted lists (pu_small == 2): a block's 256 queries are
+// monotone (pellet indices; buffer starts; buckets -- the buffer is sorted by
+// bucket), so each list entry is either below the block's query range (counted
+// once, block-wide) or inside it (a short LDS list every thread scans).
+__device__ __forceinline__ int block_sum(int v, int *red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int s = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); w++) s += red[w];
+  return s;
+}
+__device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel, int i, int n0, int nk, int ns,
+                                                   int src, int dst, bool dead, double x, double y, double m,
+                                                   int64_t sq, int col, int s0, int c0, int *lk, int64_t *ls,
+                                                   bool tick_block) {
+  __shared__ int s_lo[4], s_red[4], s_n[2];
+  const int tid = threadIdx.x;
+  const size_t P0 = (size_t)a * d.Pcap;
+  const int *kl = d.kill_list + P0;
+  const int64_t *sk = d.stg_key + 2 * P0;
+  const int i0 = i - tid;  // the block's first query
+  // the block's query range: pellets [i0, i0 + 256) of buckets [b_lo, b_hi];
+  // buckets [i0, i0 + 256) with buffer starts [s_lo, s_hi)
+  const int b = pel && i < n0 ? center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols) : 0;
+  const int last = pel ? min(i0 + 255, n0 - 1) : min(i0 + 255, d.H - 1);
+  if (tid == 0) {
+    s_lo[0] = pel ? b : s0;
+    s_n[0] = s_n[1] = 0;
+    if (last < i0) s_lo[1] = s_lo[0];  // (a pellet block past the buffer: no queries)
+  }
+  if (i == last) s_lo[1] = pel ? b : s0 + c0;
+  __syncthreads();
+  const int klo = pel ? i0 : s_lo[0], khi = pel ? i0 + 256 : s_lo[1];         // kills: [klo, khi)
+  const int blo = pel ? s_lo[0] : i0, bhi = pel ? s_lo[1] + 1 : i0 + 256;  // staged buckets: [blo, bhi)
+  int below_k = 0, below_s = 0;
+  for (int t = tid; t < nk; t += 256) {
+    const int v = kl[t];
+    below_k += v < klo;
+    if (v >= klo && v < khi) lk[atomicAdd(&s_n[0], 1)] = v;
+  }
+  for (int t = tid; t < ns; t += 256) {
+    const int64_t k = sk[t];
+    const int bk = (int)(k >> 32);
+    below_s += bk < blo;
+    if (bk >= blo && bk < bhi) ls[atomicAdd(&s_n[1], 1)] = k;
+  }
+  below_k = block_sum(below_k, s_red);  // (its barrier also publishes the short lists)
+  __syncthreads();
+  below_s = block_sum(below_s, s_red);
+  const int nlk = s_n[0], nls = s_n[1];
+  ArenaCtl &c = d.ctl[a];
+  if (tick_block && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
+  if (pel) {
+    if (i < n0) {
+      const size_t g = P0 + i;
+      if (dead) {
+        d.pel_dead[g] = 0;
+      } else {
+        int kb = below_k, sb = below_s;
+        for (int t = 0; t < nlk; t++) kb += lk[t] < i;
+        for (int t = 0; t < nls; t++) sb += (int)(ls[t] >> 32) < b;
+        const int pos = i - kb + sb;
+        if (pos < d.Pcap) {
+          const size_t o = P0 + pos;
+          d.pel_x[dst][o] = x;
+          d.pel_y[dst][o] = y;
+          d.pel_m[dst][o] = m;
+          d.pel_seq[dst][o] = sq;
+          d.pel_col[dst][o] = col;
+        }
+      }
+    } else if (i < n0 + d.ctl[a].pu_nconv) {
+      d.pel_dead[P0 + i] = 0;
+    }
+    return;
+  }
+  if (i >= d.H) return;
+  int k0 = below_k, k1 = below_k, j0 = below_s, nb = 0;
+  for (int t = 0; t < nlk; t++) {
+    k0 += lk[t] < s0;
+    k1 += lk[t] < s0 + c0;
+  }
+  for (int t = 0; t < nls; t++) {
+    const int bt = (int)(ls[t] >> 32);
+    j0 += bt < i;
+    nb += bt == i;
+  }
+  const int start = s0 - k0 + j0, surv = c0 - (k1 - k0);
+  // this bucket's staged records in staging order (the short list is unordered)
+  for (int t = 0; t < nls; t++) {
+    if ((int)(ls[t] >> 32) != i) continue;
+    int r = 0;
+    for (int u = 0; u < nls; u++) r += (int)(ls[u] >> 32) == i && ls[u] < ls[t];
+    const int pos = start + surv + r;
+    if (pos >= d.Pcap) continue;
+    const size_t o = P0 + pos, gs = P0 + (int)(ls[t] & 0xFFFFFFFFll);
+    d.pel_x[dst][o] = d.pn_x[gs];
+    d.pel_y[dst][o] = d.pn_y[gs];
+    d.pel_m[dst][o] = d.pn_m[gs];
+    d.pel_seq[dst][o] = d.pn_seq[gs];
+    d.pel_col[dst][o] = d.pn_col[gs];
+  }
+  d.pstart[(size_t)a * (d.H + 1) + i] = start;
+  d.pbc[(size_t)a * d.H + i] = surv + nb;
+}
 __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
   __shared__ int s_kill[PU_SH];
   __shared__ int64_t s_stg[PU_SH];
@@ -2923,7 +3076,8 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
   if ((int)blockIdx.x >= nup) return fov_cache_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
   const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
-  const int small = c.pu_small, n0 = c.pu_n0, nconv = c.pu_nconv;
+  const int mode = c.pu_small, n0 = c.pu_n0, nconv = c.pu_nconv;
+  const bool small = mode == 1, unsorted = mode == 2;  // (else: sorted lists from k_spawn_plan)
   int nk = c.n_kill, ns = c.n_stg;
   const int src = c.pu_src, dst = src ^ 1;
   const size_t P0 = (size_t)a * d.Pcap;
@@ -2950,6 +3104,8 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
   const int64_t *sk = d.stg_key + 2 * P0;
   if (small && tid < 64) pellet_lists_wave(d, c, a, n0, nconv, c.n_spawn_p, min(nk, d.Pcap), s_kill, s_stg, s_n);
   const bool kin = small || nk <= PU_SH, sin = small || ns <= PU_SH;
+  if (unsorted) return pel_update_blocked(d, a, pel, i, n0, nk, ns, src, dst, dead, x, y, m, sq, col, s0, c0, s_kill,
+                                         s_stg, blk == 0 && pel);
   if (!small) {
     if (kin)
       for (int t = tid; t < nk; t += 256) s_kill[t] = kl[t];
@@ -3237,8 +3393,10 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
       const int b = by * d.cols + bx, lo = min(d.pstart[b], F.n0), hi = min(d.pstart[b + 1], F.n0);
       for (int t = lo; t < hi; t++)
         if (d.pel_seq[F.pb][F.g(t)] == r.seq) {
-          d.pel_dead[F.g(t)] = 1;
-          note_kill(d, 0, t);
+          uint8_t *pd = d.pel_dead + F.g(t);  // (flag set through its 32-bit word: the first setter notes the kill)
+          unsigned *w = (unsigned *)((uintptr_t)pd & ~(uintptr_t)3);
+          const unsigned sh = (unsigned)((uintptr_t)pd & 3) * 8;
+          if (!((atomicOr(w, 1u << sh) >> sh) & 0xFFu)) note_kill(d, 0, t);
           return;
         }
       for (int j = F.n0; j < F.n0 + F.nst; j++)  // this tick's blob conversions (staged)

@@ -5,7 +5,7 @@ the time from the wave's first instruction to each mark.  Runs the bench's C3
 step (matured start, graph replays) and prints mean / max per mark in us.
 
   python tools/phase_timing.py build          # here: hipcc the diagnostics .so
-  python tools/phase_timing.py run [steps]    # GPU box
+  python tools/phase_timing.py run [steps] [random|greedy]   # GPU box
 """
 import ctypes as C
 import os
@@ -30,7 +30,7 @@ def build():
     print(SO)
 
 
-def run(steps):
+def run(steps, policy="random"):
     os.environ["AIGAR_SO"] = SO
     sys.path.insert(0, ROOT)
     import torch
@@ -41,7 +41,7 @@ def run(steps):
     stp = _lib.Stepper(bench.make_cfg(name, device=0, arenas=arenas))
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
     print(bench.start_world(stp, name, 1234, arenas))
-    stp.run(20, "random", obs, p_split=ps, p_eject=pe, seed=1234, greedy_split=True)
+    stp.run(20, policy, obs, p_split=ps, p_eject=pe, seed=1234, greedy_split=True)
     stp.sync()
     import numpy as np
     L = C.CDLL(SO)
@@ -55,7 +55,7 @@ def run(steps):
     placement = {}
     for _ in range(steps):  # one step per snapshot: every wave's slots are written once per step
         assert L.aigar_debug_phase_times(None, None, C.byref(khz), 1) == 0
-        stp.run(1, "random", obs, p_split=ps, p_eject=pe, seed=99, greedy_split=True)
+        stp.run(1, policy, obs, p_split=ps, p_eject=pe, seed=99, greedy_split=True)
         stp.sync()
         assert L.aigar_debug_phase_times(ptr, iptr, C.byref(khz), 0) == 0
         for k in KERNELS:
@@ -121,4 +121,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "build":
         build()
     else:
-        run(int(sys.argv[2]) if len(sys.argv) > 2 else 50)
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 50, sys.argv[3] if len(sys.argv) > 3 else "random")
