@@ -67,12 +67,37 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
     if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[k][pt_w_][m] = (unsigned)(wall_clock64() - pt0_); \
   } while (0)
 #define PT_PARAMS , unsigned long long pt0_, int pt_w_
+// accumulating buckets for a serial loop (g_ptw[6][a][k]: wall-clock ticks, [7][a][k]: counts)
+#define PA_DECL                                   \
+  unsigned long long pa_t_ = wall_clock64();      \
+  unsigned pa_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pa_cnt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PA_T(k)                                                         \
+  do {                                                                  \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");         \
+    const unsigned long long pa_n_ = wall_clock64();                    \
+    pa_acc_[k] += (unsigned)(pa_n_ - pa_t_);                            \
+    pa_t_ = pa_n_;                                                      \
+  } while (0)
+#define PA_C(k) (pa_cnt_[k]++)
+#define PA_ADD(k, v) (pa_cnt_[k] += (v))
+#define PA_STORE(a)                                                             \
+  if ((threadIdx.x & 63) == 0 && (a) < kPtWaves)                                \
+    for (int k_ = 0; k_ < 8; k_++) {                                            \
+      g_ptw[6][a][k_] += pa_acc_[k_];                                           \
+      g_ptw[7][a][k_] += pa_cnt_[k_];                                           \
+    }
+#define PT_ARGS , pt0_, pt_w_
 #define PT_ARGS , pt0_, pt_w_
 #else
 #define PT_BEGIN(k)
 #define PT_MARK(k, m)
 #define PT_PARAMS
 #define PT_ARGS
+#define PA_DECL
+#define PA_T(k)
+#define PA_C(k)
+#define PA_ADD(k, v)
+#define PA_STORE(a)
 #endif
 
 __device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { atomicOr(&d.ctl[a].err, bit); }
@@ -443,6 +468,13 @@ __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = gi; i < (long)d.A * d.H; i += stride) d.occ_cnt[i] = 0;
     for (long i = gi; i < (long)d.A * d.occ_words; i += stride) d.occ[i] = 0;
+    // the dead flags of the last closing update's blob conversions (its blocks
+    // read them while building their lists, so none of them may clear one)
+    for (long t = gi; t < (long)d.A * d.Ecap; t += stride) {
+      const int a = (int)(t / d.Ecap), j = (int)(t - (long)a * d.Ecap);
+      const ArenaCtl &c = d.ctl[a];
+      if (j < c.pu_nconv && c.pu_n0 + j < d.Pcap) d.pel_dead[(size_t)a * d.Pcap + c.pu_n0 + j] = 0;
+    }
   }
   if (gi < kMaxCells * d.NP) {
     update_cell(d, gi, rp PT_ARGS);
@@ -2198,6 +2230,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
   __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
   __shared__ double s_x[PP_LCAP], s_y[PP_LCAP], s_m[PP_LCAP], s_r[PP_LCAP];
   const int lane = threadIdx.x & 63;
+  PA_DECL;
   ArenaCtl &c = d.ctl[a];
   const int B = d.B, NW = (B + 31) / 32;
   const int nw = min(c.n_pend, d.Wcap);
@@ -2218,6 +2251,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
   const unsigned long long lt = (1ull << lane) - 1;
   uint64_t order = 0;
   double rmax = c.rmax_cell;
+  PA_T(0);
   int P = -1;
   for (;;) {
     // next pending player > P
@@ -2233,6 +2267,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
     if (lane == 0) pend[P >> 5] &= ~(1u << (P & 31));
     wave_fence();
     const int gp = a * B + P;
+    PA_C(0);
     if (!d.p_alive[gp]) continue;
     for (int i = 0; i < d.p_ncells[gp];) {  // for playerCell in player.getCells(): live list
       const size_t pc = (size_t)d.p_list[i * NP + gp] * NP + gp;
@@ -2240,6 +2275,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
       if (!active_ld(d, pc)) continue;
       active_st(d, pc, 0);
       const Rect q0 = cell_rect(d, pc);
+      PA_T(1);
       int nc = 0;
       wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
         double ex = 0, ey = 0, er = 0;
@@ -2266,6 +2302,9 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         set_err(d, a, ERR_CAND_CAP);
         nc = PP_LCAP;
       }
+      PA_T(2);
+      PA_C(1);
+      PA_ADD(4, nc);
       wave_fence();
       for (int x = lane; x < nc; x += 64) {  // rank by creation sequence (keys are unique)
         int64_t k = s_key[x];
@@ -2277,6 +2316,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
       const double px = d.c_x[pc], py = d.c_y[pc];
       const int64_t pseq = d.c_seq[pc];
       double pm = d.c_m[pc], pr = d.c_r[pc];
+      PA_T(3);
       for (int t = 0; t < nc; t++) {
         const int k = s_srt[t];
         const size_t o = (size_t)s_val[k];
@@ -2315,6 +2355,8 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         const int gpl = (int)(g % NP);
         const double gx = pc_eats ? px : ox, gy = pc_eats ? py : oy, gm = m, gr = mr;
         wave_fence();  // (the removal above is read by the re-activation walk)
+        PA_T(4);
+        PA_C(2);
         wave_grid_for(st, it, d.cols, cell_rect(d, g), expand_for(rmax), [&](bool valid, int e) {
           if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
           if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;
@@ -2325,6 +2367,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         active_st(d, g, 1);
         if (gpl - a * B > P && lane == 0) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
         wave_fence();
+        PA_T(5);
         if (!pc_eats) {
           // pc left the live list: the cell that moved into its place is skipped
           // this turn (field.py:236 + player.py:97).  Its pairs with later
@@ -2344,11 +2387,15 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
             }, d.cshift_c);
             wave_fence();
           }
+          PA_T(6);
+          PA_C(3);
           break;
         }
       }
     }
   }
+  PA_T(7);
+  PA_STORE(a);
   c.rmax_cell = rmax;
 }
 
@@ -3034,8 +3081,6 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
           d.pel_col[dst][o] = col;
         }
       }
-    } else if (i < n0 + d.ctl[a].pu_nconv) {
-      d.pel_dead[P0 + i] = 0;
     }
     return;
   }
@@ -3145,8 +3190,6 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
           d.pel_col[dst][o] = col;
         }
       }
-    } else if (i < n0 + nconv) {
-      d.pel_dead[g] = 0;  // (a blob conversion eaten in the eat phase)
     }
     if (blk == 0 && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
   } else if (i < d.H) {
@@ -3226,6 +3269,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.n_ev = 0;
   c.n_pend = c.n_pend2 = 0;
   c.n_kill = c.n_stg = 0;
+  c.pu_n0 = c.pu_nconv = c.pu_small = 0;
   c.err = c.warn = 0;
   c.rmax_cell = radius_of(kStartMass);
   c.rmax_virus = radius_of(kVirusBase);

@@ -58,6 +58,8 @@ def run(steps, policy="random"):
         stp.run(1, policy, obs, p_split=ps, p_eject=pe, seed=99, greedy_split=True)
         stp.sync()
         assert L.aigar_debug_phase_times(ptr, iptr, C.byref(khz), 0) == 0
+        pa_acc = pa_acc + buf[6, 0, :].astype(np.float64) if "pa_acc" in dir() else buf[6, 0, :].astype(np.float64)
+        pa_cnt = pa_cnt + buf[7, 0, :].astype(np.float64) if "pa_cnt" in dir() else buf[7, 0, :].astype(np.float64)
         for k in KERNELS:
             started = buf[k, :, 0] != 0
             if not started.any():
@@ -94,6 +96,12 @@ def run(steps, policy="random"):
             print("%-14s %-14s %9.1f %8.2f %8.2f %8.2f %8.2f %10.2f" % (
                 kn, marks[m] or "start", len(v) / steps, v.mean(), np.percentile(v, 50), np.percentile(v, 90),
                 v.max(), span.mean() if m else 0.0))
+    if "pa_acc" in dir():  # the pp serial pass, arena 0: accumulated buckets per step
+        names = ["setup", "turn start", "gather walk", "rank", "eat", "re-activation walk", "skip+reload", "rest"]
+        print("pp serial pass (arena 0, per step): " + ", ".join(
+            "%s %.2f us" % (nm, pa_acc[k] * us / steps) for k, nm in enumerate(names)))
+        print("pp serial pass counts per step: turns %.2f, gathers %.2f, eats %.2f, pc eaten %.2f, candidates %.2f" % tuple(
+            pa_cnt[k] / steps for k in (0, 1, 2, 3, 4)))
     khz_ = khz.value / 1e3
     for k in KERNELS:
         row = []
