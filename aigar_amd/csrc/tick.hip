@@ -461,21 +461,25 @@ __device__ void spawn_ahead(const Dev &d, int a, int j) {
   d.spec_y[o] = (double)(int64_t)mulhi(u[1], (uint64_t)d.size);
   d.spec_m[o] = (sr > 50 - 4) ? (double)(50 - sr) : 1.0;  // randomSize (field.py:20-26)
 }
+// per-tick resets, by extra threads at the end of k_tick_begin's grid (in the
+// update threads their loads delayed every cell's first round): the spawn
+// occupancy restarts (k_pp_active rebuilds it; its last reader was the previous
+// tick's spawns); the dead flags of the last closing update's blob conversions
+// (that update's blocks read them while building their lists, so none of them
+// may clear one) are cleared
+constexpr int kTickZero = 16 * 256;
+__device__ void tick_zero(const Dev &d, int gi) {
+  for (long i = gi; i < (long)d.A * d.H; i += kTickZero) d.occ_cnt[i] = 0;
+  for (long i = gi; i < (long)d.A * d.occ_words; i += kTickZero) d.occ[i] = 0;
+  for (long t = gi; t < (long)d.A * d.Ecap; t += kTickZero) {
+    const int a = (int)(t / d.Ecap), j = (int)(t - (long)a * d.Ecap);
+    const ArenaCtl &c = d.ctl[a];
+    if (j < c.pu_nconv && c.pu_n0 + j < d.Pcap) d.pel_dead[(size_t)a * d.Pcap + c.pu_n0 + j] = 0;
+  }
+}
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   PT_BEGIN(2);
   int gi = GTID;
-  {  // the spawn occupancy restarts (k_pp_active rebuilds it; the last reader was the previous tick's spawns)
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = gi; i < (long)d.A * d.H; i += stride) d.occ_cnt[i] = 0;
-    for (long i = gi; i < (long)d.A * d.occ_words; i += stride) d.occ[i] = 0;
-    // the dead flags of the last closing update's blob conversions (its blocks
-    // read them while building their lists, so none of them may clear one)
-    for (long t = gi; t < (long)d.A * d.Ecap; t += stride) {
-      const int a = (int)(t / d.Ecap), j = (int)(t - (long)a * d.Ecap);
-      const ArenaCtl &c = d.ctl[a];
-      if (j < c.pu_nconv && c.pu_n0 + j < d.Pcap) d.pel_dead[(size_t)a * d.Pcap + c.pu_n0 + j] = 0;
-    }
-  }
   if (gi < kMaxCells * d.NP) {
     update_cell(d, gi, rp PT_ARGS);
     PT_MARK(2, 1);
@@ -491,7 +495,9 @@ __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   }
   if (gi < d.A * d.Ecap) return update_blob(d, gi);
   gi -= d.A * d.Ecap;
-  if (gi < d.A * kSpawnAhead) spawn_ahead(d, gi / kSpawnAhead, gi % kSpawnAhead);
+  if (gi < d.A * kSpawnAhead) return spawn_ahead(d, gi / kSpawnAhead, gi % kSpawnAhead);
+  gi -= d.A * kSpawnAhead;
+  if (gi < kTickZero) tick_zero(d, gi);
 }
 
 // rank of this thread among the flagged threads of the block (thread order);
@@ -1582,8 +1588,9 @@ struct Food {
   const Dev &d;
   int a, pb;  // pb: the eat-phase pellet buffer (ArenaCtl::peat)
   int n0, nst;
+  int nblob;  // (the blob list's length is fixed during the eat phase: loaded with the rest, no round of its own)
   __device__ Food(const Dev &dd, int aa)
-      : d(dd), a(aa), pb(dd.ctl[aa].peat), n0(dd.ctl[aa].n_pel), nst(dd.ctl[aa].n_pnew) {}
+      : d(dd), a(aa), pb(dd.ctl[aa].peat), n0(dd.ctl[aa].n_pel), nst(dd.ctl[aa].n_pnew), nblob(dd.ctl[aa].n_blob) {}
   __device__ static bool blob(int j) { return (j & kBlobBit) != 0; }
   __device__ size_t g(int j) const { return (size_t)a * d.Pcap + j; }               // pellet j
   __device__ size_t gs(int j) const { return (size_t)a * d.Pcap + (j - n0); }       // staged pellet j
@@ -1607,7 +1614,7 @@ struct Food {
     }
   }
   __device__ uint64_t *owner(int j) const { return blob(j) ? d.b_owner + gb(j) : d.pel_owner + g(j); }
-  __device__ bool any_blobs() const { return d.ctl[a].n_blob > 0; }
+  __device__ bool any_blobs() const { return nblob > 0; }
   // every pellet / blob whose footprint may touch q: f(valid, j) on all lanes (wave-uniform calls)
   template <class Fn>
   __device__ void walk_pellets(Rect q, Fn f) const {
@@ -3330,7 +3337,7 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 // the phases before the eat phase (field.py:94-198, 225-231, 246-253)
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap +
-                       (long)d.A * kSpawnAhead;
+                       (long)d.A * kSpawnAhead + kTickZero;
   hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
   // + the virus grid (extra block) and the blob grid (last block) of updateHashTables
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + (d.virus_enabled ? 1 : 0), d.A), dim3(256), 0, s, d);
