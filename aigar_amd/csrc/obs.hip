@@ -204,7 +204,7 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
     for (int t0 = 0; t0 < total; t0 += 64) {
       const int t = t0 + lane;
       int rw = 0;
-      for (int k = 1; k < nr; k++) rw = (__shfl(excl, k) <= t) ? k : rw;
+      for (int k = 1; k < nr; k++) rw = (__builtin_amdgcn_readlane(excl, k) <= t) ? k : rw;  // (k uniform: v_readlane)
       const int idx = __shfl(lo, rw) + (t - __shfl(excl, rw));
       const int kd = __shfl(kind, rw);
       const bool valid = t < total;
@@ -253,6 +253,16 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
 #endif
   OBS_STAMP(0);
   OutT *row = out + (size_t)gp * L;
+  // the output row is written once and read by the host / learner, never by
+  // the next tick: non-temporal stores keep it from evicting the world state
+  // (the next tick's working set) out of the L2s
+  auto row_st = [&](int i, OutT v) __attribute__((always_inline)) {
+#ifdef AIGAR_OBS_NO_NT
+    row[i] = v;
+#else
+    __builtin_nontemporal_store(v, row + i);
+#endif
+  };
   // one round of independent loads: liveness, the FOV cache written at the end
   // of the tick (store_player_fov) and the own cells' slots
   const bool alive = d.p_alive[gp];
@@ -560,12 +570,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     double freeA = (rb - lb) * (bb - tb);
     // a square wholly inside the field: freeA / (gs*gs) is exactly 1 -> round(0, 3) = +0
     double vw = (freeA == gs * gs) ? 0.0 : py_round3(1 - (freeA / (gs * gs)));
-    if (o_pel >= 0) row[o_pel + t] = held ? (OutT)vp : (OutT)__builtin_nan("");
-    if (o_self >= 0) row[o_self + t] = (OutT)vs;
-    if (o_wall >= 0) row[o_wall + t] = (OutT)vw;
-    if (o_enemy >= 0) row[o_enemy + t] = (OutT)ve;
-    if (o_all >= 0) row[o_all + t] = (OutT)py_max(ve, vs);
-    if (o_vir >= 0) row[o_vir + t] = (OutT)vv;
+    if (o_pel >= 0) row_st(o_pel + t, held ? (OutT)vp : (OutT)__builtin_nan(""));
+    if (o_self >= 0) row_st(o_self + t, (OutT)vs);
+    if (o_wall >= 0) row_st(o_wall + t, (OutT)vw);
+    if (o_enemy >= 0) row_st(o_enemy + t, (OutT)ve);
+    if (o_all >= 0) row_st(o_all + t, (OutT)py_max(ve, vs));
+    if (o_vir >= 0) row_st(o_vir + t, (OutT)vv);
     double o_sl, o_ss, o_el, o_es;  // history before this frame
     if constexpr (decltype(hist_regs)::value) {
       o_sl = t < 64 ? h_slf0 : h_slf1;
@@ -579,19 +589,19 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       o_es = o_eslf >= 0 ? eslf[t] : 0.0;
     }
     if (o_sslf >= 0) {
-      row[o_sslf + t] = (OutT)o_ss;
+      row_st(o_sslf + t, (OutT)o_ss);
       sslf[t] = o_sl;
     }
     if (o_slf >= 0) {
-      row[o_slf + t] = (OutT)o_sl;
+      row_st(o_slf + t, (OutT)o_sl);
       slf[t] = vs;
     }
     if (o_eslf >= 0) {
-      row[o_eslf + t] = (OutT)o_es;
+      row_st(o_eslf + t, (OutT)o_es);
       eslf[t] = o_el;
     }
     if (o_elf >= 0) {
-      row[o_elf + t] = (OutT)o_el;
+      row_st(o_elf + t, (OutT)o_el);
       elf[t] = ve;
     }
   }

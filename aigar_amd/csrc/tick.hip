@@ -311,6 +311,109 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   d.c_vy[ci] = vy;
 }
 
+// adjustCellPositions (field.py:161-181) for the pair (a, b), a the bigger
+__device__ __forceinline__ void adjust_pair(double &bx, double &by, double bm, double &sx, double &sy, double sm,
+                                            double dist, double sr, double W) {
+  double ds = (sr - dist) / dist, mds = sm / bm;
+  double xd = (bx - sx) * ds, yd = (by - sy) * ds;
+  double nbx = bx + xd * mds, nby = by + yd * mds;
+  double nsx = sx - xd * (1 - mds), nsy = sy - yd * (1 - mds);
+  bx = py_min(W, py_max(0.0, nbx));
+  by = py_min(W, py_max(0.0, nby));
+  sx = py_min(W, py_max(0.0, nsx));
+  sy = py_min(W, py_max(0.0, nsy));
+}
+// The eject flags, updateCellsMovement, performEjections and
+// handlePlayerCollisions of update_player below for a player with n <= N
+// cells, on registers: every field of the n cells is loaded in ONE round
+// (fully unrolled, constant indices), the phases run in the same order on the
+// copies, and only what changed is stored.  The memory version re-loads
+// across each phase's stores (one dependent round per phase and cell).
+constexpr int kTailRegs = 4;
+template <int N>
+__device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint8_t *lst, int n, bool eject,
+                                                double cpx, double cpy, double W) {
+  const int NP = d.NP;
+  double x[N], y[N], vx[N], vy[N], svx[N], svy[N], m[N], r[N], mt[N];
+  int svc[N];
+  uint32_t fl[N];
+  bool ej[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    x[k] = y[k] = vx[k] = vy[k] = svx[k] = svy[k] = m[k] = r[k] = mt[k] = 0;
+    svc[k] = 0;
+    fl[k] = 0;
+    if (k < n) {
+      const size_t ci = (size_t)lst[k] * NP + gp;
+      x[k] = d.c_x[ci];
+      y[k] = d.c_y[ci];
+      vx[k] = d.c_vx[ci];
+      vy[k] = d.c_vy[ci];
+      svx[k] = d.c_svx[ci];
+      svy[k] = d.c_svy[ci];
+      m[k] = d.c_m[ci];
+      r[k] = d.c_r[ci];
+      mt[k] = d.c_mt[ci];
+      svc[k] = d.c_svc[ci];
+      fl[k] = d.c_flags[ci];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    if (eject && k < n && m[k] >= 35) fl[k] |= F_EJECT;  // Player.eject (player.py:54-58)
+    ej[k] = k < n && (fl[k] & F_EJECT);
+  }
+#pragma unroll
+  for (int k = 0; k < N; k++)  // updateCellsMovement
+    if (k < n) update_pos(x[k], y[k], vx[k], vy[k], svx[k], svy[k], svc[k], W, W);
+  int nb = 0;
+#pragma unroll
+  for (int k = 0; k < N; k++) {  // performEjections (field.py:134-146)
+    if (!ej[k]) continue;
+    m[k] = m[k] - kEjectMass;  // Cell.eject: radius stays stale (cell.py:90-94)
+    double bsvx, bsvy;
+    int bsvc;
+    add_momentum(x[k], y[k], cpx, cpy, W, W, r[k], bsvx, bsvy, bsvc);
+    const size_t si = (size_t)nb * NP + gp;
+    d.sb_x[si] = x[k];
+    d.sb_y[si] = y[k];
+    d.sb_svx[si] = bsvx;
+    d.sb_svy[si] = bsvy;
+    d.sb_slot[si] = lst[k];
+    nb++;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {  // handlePlayerCollisions (field.py:149-159)
+    if (i >= n || svc[i] > 0) continue;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j >= n || i == j || svc[j] > 0 || (mt[i] <= 0 && mt[j] <= 0)) continue;
+      double dist = sqrt((x[i] - x[j]) * (x[i] - x[j]) + (y[i] - y[j]) * (y[i] - y[j]));
+      double sr = r[i] + r[j];
+      if (dist < sr && dist != 0) {
+        if (m[i] > m[j])
+          adjust_pair(x[i], y[i], m[i], x[j], y[j], m[j], dist, sr, W);
+        else
+          adjust_pair(x[j], y[j], m[j], x[i], y[i], m[i], dist, sr, W);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    if (k >= n) continue;
+    const size_t ci = (size_t)lst[k] * NP + gp;
+    d.c_x[ci] = x[k];
+    d.c_y[ci] = y[k];
+    d.c_svx[ci] = svx[k];
+    d.c_svy[ci] = svy[k];
+    if (ej[k]) {
+      d.c_m[ci] = m[k];
+      d.c_flags[ci] = fl[k] & ~F_EJECT;
+    }
+  }
+  return nb;
+}
+
 // the rest of Player.update (split, eject, move) + performEjections +
 // handlePlayerCollisions, one thread per player (list order matters)
 __device__ __forceinline__ void update_player(const Dev &d, int gp) {
@@ -321,17 +424,22 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
   double *__restrict__ csvy = d.c_svy, *__restrict__ cmt = d.c_mt;
   int *__restrict__ csvc = d.c_svc;
   uint32_t *__restrict__ cfl = d.c_flags;
+  // the list's first rows are loaded with the player's fields (one round; the
+  // rows past the cell count are allocated and simply unused)
+  uint8_t lst[kMaxCells];
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) lst[k] = d.p_list[k * NP + gp];
+  const bool alive = d.p_alive[gp];
+  int n = d.p_ncells[gp];
   d.p_newc[gp] = 0;
   d.p_newb[gp] = 0;
-  if (!d.p_alive[gp]) {  // updateRespawnTime (player.py:74-75)
+  if (!alive) {  // updateRespawnTime (player.py:74-75)
     d.p_respawn[gp] -= 1;
     return;
   }
   const double W = (double)d.size;
   const double cpx = d.p_cmdx[gp], cpy = d.p_cmdy[gp];
-  int n = d.p_ncells[gp];
-  uint8_t lst[kMaxCells];
-  for (int k = 0; k < n; k++) lst[k] = d.p_list[k * NP + gp];
+  for (int k = kTailRegs; k < n; k++) lst[k] = d.p_list[k * NP + gp];
   // (decay, momentum, merge timer and direction already ran per cell: update_cell)
   int n_new = 0;
   if (d.p_split[gp]) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
@@ -383,6 +491,14 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
       lst[n++] = (uint8_t)slot;
       n_new++;
     }
+  }
+  if (n <= kTailRegs) {  // the common case: the rest runs on registers, one load round
+    const int nb = player_tail_regs<kTailRegs>(d, gp, lst, n, d.p_eject[gp] != 0, cpx, cpy, W);
+    for (int k = 0; k < n; k++) d.p_list[k * NP + gp] = lst[k];
+    d.p_ncells[gp] = n;
+    d.p_newc[gp] = n_new;
+    d.p_newb[gp] = nb;
+    return;
   }
   if (d.p_eject[gp])  // Player.eject (player.py:54-58)
     for (int k = 0; k < n; k++) {
@@ -1185,12 +1301,25 @@ __global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode, int fov_
 }
 // ------------------------------------------------------------ T10 merge
 __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
-  if (gp >= d.NP || !d.p_alive[gp]) return;
+  if (gp >= d.NP) return;
   const int NP = d.NP, a = gp / d.B;
-  int n = d.p_ncells[gp];
+  // liveness, count and the list's first rows in one load round (rows past
+  // the count are allocated and unused), then the first cells' timers in one
+  uint8_t l4[kTailRegs];
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) l4[k] = d.p_list[k * NP + gp];
+  const bool alive = d.p_alive[gp];
+  const int n = d.p_ncells[gp];
+  if (!alive) return;
   uint8_t cs[kMaxCells];
   int nm = 0;
-  for (int k = 0; k < n; k++) {  // getMergableCells (player.py:144-149)
+  double mt4[kTailRegs];
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) mt4[k] = k < n ? d.c_mt[(size_t)l4[k] * NP + gp] : 1.0;
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++)  // getMergableCells (player.py:144-149)
+    if (k < n && mt4[k] <= 0) cs[nm++] = l4[k];
+  for (int k = kTailRegs; k < n; k++) {
     uint8_t s = d.p_list[k * NP + gp];
     if (d.c_mt[(size_t)s * NP + gp] <= 0) cs[nm++] = s;
   }
@@ -1424,11 +1553,40 @@ __device__ void pv_player(const Dev &d, int gp) {
   // lightest virus at the grid build (k_players); viruses split during
   // virusBlobOverlap are >= (VIRUS_BASE_SIZE + 7 * 14.4) / 2, so VIRUS_BASE_SIZE bounds them
   const double vmin = fmin(d.ctl[a].vmin_mass, kVirusBase);
+  uint8_t l4[kTailRegs];  // (the list's first rows with the count: one load round)
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) l4[k] = d.p_list[k * NP + gp];
+  const bool alive = d.p_alive[gp];
   const int n = d.p_ncells[gp];
+  if (!alive) return;
   bool anyp = false;
+  // the first cells' records in one round, before any grid walk
+  double x4[kTailRegs], y4[kTailRegs], m4[kTailRegs], r4[kTailRegs];
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) {
+    x4[k] = y4[k] = m4[k] = r4[k] = 0;
+    if (k < n) {
+      const size_t ci = (size_t)l4[k] * NP + gp;
+      x4[k] = d.c_x[ci];
+      y4[k] = d.c_y[ci];
+      m4[k] = d.c_m[ci];
+      r4[k] = d.c_r[ci];
+    }
+  }
   for (int k = 0; k < n; k++) {
-    const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    const double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    size_t ci;
+    double x, y, m, r;
+    if (k < kTailRegs) {  // (select from the registers: no dynamic index)
+      uint8_t s = l4[0];
+      x = x4[0], y = y4[0], m = m4[0], r = r4[0];
+#pragma unroll
+      for (int j = 1; j < kTailRegs; j++)
+        if (k == j) s = l4[j], x = x4[j], y = y4[j], m = m4[j], r = r4[j];
+      ci = (size_t)s * NP + gp;
+    } else {
+      ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+      x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    }
     bool any = false;
     if (m > 1.25 * vmin) {
       const Rect q = footprint(x, y, r, d.size);
@@ -1451,7 +1609,7 @@ __device__ void pv_player(const Dev &d, int gp) {
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
 __global__ void __launch_bounds__(256) k_pv_active(Dev d, int64_t *scr_k, int *scr_v, int fold) {
   const int gp = GTID;
-  if (gp < d.NP && d.p_alive[gp]) pv_player(d, gp);
+  if (gp < d.NP) pv_player(d, gp);
   if (fold && last_block(d.ticket + 2, gridDim.x))
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) pv_serial_body(d, a, scr_k, scr_v);
 }

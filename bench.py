@@ -198,7 +198,7 @@ def batched(name, arenas, policy, ps, pe, seed, device, steps=20, warmup=5):
     stp = _lib.Stepper(make_cfg(name, device=device, arenas=arenas))
     stp.set_stream(torch.cuda.current_stream().cuda_stream)
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
-    stp.reset(seed + 1)
+    start = start_world(stp, name, seed + 1, arenas)
     run = lambda n: stp.run(n, policy, obs, p_split=ps, p_eject=pe, seed=seed, greedy_split=True)
     run(warmup)
     torch.cuda.synchronize()
@@ -206,10 +206,41 @@ def batched(name, arenas, policy, ps, pe, seed, device, steps=20, warmup=5):
     run(steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # k_observe over all arenas' bots in one launch: its roofline at this size
+    stp.profile(True)
+    for _ in range(10):
+        stp.observe(obs)
+    torch.cuda.synchronize()
+    obs_ms, obs_n = stp.kernel_time("observe")
+    stp.profile(False)
     stp.sync()
+    per_bot, reads_bot, alive = obs_bytes(stp, WORKLOADS[name][1], arenas)
+    obs_s = obs_ms / max(1, obs_n) / 1e3
     stp.close()
     return {"arenas": arenas, "bots": bots, "value": bots * steps / dt, "unit": "env-steps/s",
-            "ms_per_step": dt / steps * 1e3, "steps": steps}
+            "ms_per_step": dt / steps * 1e3, "steps": steps, "start": start,
+            "roofline_k_observe": {"bytes_per_launch": int(per_bot * alive), "avg_launch_ms": obs_s * 1e3,
+                                   "achieved": round(per_bot * alive / obs_s / 1e9, 2), "peak": 8000.0,
+                                   "unit": "GB/s", "frac": per_bot * alive / obs_s / 1e9 / 8000.0,
+                                   "reads": {"bytes_per_launch": int(reads_bot * alive),
+                                             "frac": reads_bot * alive / obs_s / 1e9 / 8000.0}}}
+
+
+def obs_bytes(stp, field, arenas):
+    """Algorithmic bytes of one k_observe launch from the stepper's current
+    world: (per alive bot, of which reads, alive bots)."""
+    st = stp.get_state()
+    stats = stp.player_stats()
+    alive = int(np.sum(stats[:, 0] > 0))
+    fs = np.nan_to_num(stats[:, 4])
+    area = float(np.mean((fs + 2.0) ** 2))  # FOV box incl. object radii
+    dens_p = st["n_pellets"] / float(field * field * arenas)
+    dens_c = st["n_cells"] / float(field * field * arenas)
+    dens_v = st["n_viruses"] / float(field * field * arenas)
+    ncell = st["n_cells"] / max(1, alive)
+    per_bot = obs_bytes_per_bot(stp.obs_len, dens_p * area, dens_c * area, dens_v * area, n_cells=ncell)
+    reads_bot = per_bot - stp.obs_len * 8 - 2 * 121 * 8  # minus the output row and the history writes
+    return per_bot, reads_bot, alive
 
 
 def start_world(stp, name, seed, arenas):
@@ -392,15 +423,7 @@ def main():
         stp.profile(False)
         stp.sync()
         # roofline of the dominant kernel (k_observe): algorithmic bytes per launch / avg duration
-        alive = int(np.sum(stats[:, 0] > 0))
-        fs = np.nan_to_num(stats[:, 4])
-        area = float(np.mean((fs + 2.0) ** 2))  # FOV box incl. object radii
-        dens_p = st["n_pellets"] / float(field * field * arenas)
-        dens_c = st["n_cells"] / float(field * field * arenas)
-        dens_v = st["n_viruses"] / float(field * field * arenas)
-        ncell = st["n_cells"] / max(1, alive)
-        per_bot = obs_bytes_per_bot(stp.obs_len, dens_p * area, dens_c * area, dens_v * area, n_cells=ncell)
-        reads_bot = per_bot - stp.obs_len * 8 - 2 * 121 * 8  # minus the output row and the history writes
+        per_bot, reads_bot, alive = obs_bytes(stp, field, arenas)
         obs_bytes_launch = per_bot * alive
         obs_avg_s = (obs_ms / max(1, obs_n)) / 1e3
         achieved = obs_bytes_launch / obs_avg_s / 1e9
