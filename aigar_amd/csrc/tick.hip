@@ -416,7 +416,8 @@ __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint
 
 // the rest of Player.update (split, eject, move) + performEjections +
 // handlePlayerCollisions, one thread per player (list order matters)
-__device__ __forceinline__ void update_player(const Dev &d, int gp) {
+// nn / nb_out: the new cells and blobs it made (k_players' scans take them from registers)
+__device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int &nb_out) {
   const int NP = d.NP;
   // the cell arrays never alias: let the compiler keep values in registers across stores
   double *__restrict__ cx = d.c_x, *__restrict__ cy = d.c_y, *__restrict__ cm = d.c_m, *__restrict__ cr = d.c_r;
@@ -431,8 +432,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
   for (int k = 0; k < kTailRegs; k++) lst[k] = d.p_list[k * NP + gp];
   const bool alive = d.p_alive[gp];
   int n = d.p_ncells[gp];
-  d.p_newc[gp] = 0;
-  d.p_newb[gp] = 0;
+  nn = nb_out = 0;
   if (!alive) {  // updateRespawnTime (player.py:74-75)
     d.p_respawn[gp] -= 1;
     return;
@@ -496,8 +496,8 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
     const int nb = player_tail_regs<kTailRegs>(d, gp, lst, n, d.p_eject[gp] != 0, cpx, cpy, W);
     for (int k = 0; k < n; k++) d.p_list[k * NP + gp] = lst[k];
     d.p_ncells[gp] = n;
-    d.p_newc[gp] = n_new;
-    d.p_newb[gp] = nb;
+    nn = n_new;
+    nb_out = nb;
     return;
   }
   if (d.p_eject[gp])  // Player.eject (player.py:54-58)
@@ -557,8 +557,8 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp) {
   }
   for (int k = 0; k < n; k++) d.p_list[k * NP + gp] = lst[k];
   d.p_ncells[gp] = n;
-  d.p_newc[gp] = n_new;
-  d.p_newb[gp] = nb;
+  nn = n_new;
+  nb_out = nb;
 }
 
 // updateViruses + updateBlobs + the per-cell part of updatePlayers in one
@@ -717,9 +717,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
   const int p = tile * 256 + tid, gp = a * d.B + p;
   int nn = 0, nb = 0;
   if (p < d.B) {
-    update_player(d, gp);
-    nn = d.p_newc[gp];
-    nb = d.p_newb[gp];
+    update_player(d, gp, nn, nb);  // (its counts from registers, not re-loaded)
   }
   PT_MARK(1, 1);
   const int vs = nn + nb, vb = nb;
@@ -1831,14 +1829,18 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wi = blockIdx.x * 4 + w, gp = wi / PREP_WAVES, h = wi - gp * PREP_WAVES;
   if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
-  if (gp >= d.NP || !d.p_alive[gp]) return;  // uniform per wave
+  if (gp >= d.NP) return;
+  // this wave's first list row rides the liveness / count load round (the row
+  // exists whatever the count: h < PREP_WAVES <= kMaxCells)
+  const int s_first = uni((int)d.p_list[h * d.NP + gp]);
+  if (!d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   Food F(d, a);
   const uint32_t base = d.ctl[a].food_round;
   int n = uni(d.p_ncells[gp]);  // (wave-uniform values kept in SGPRs: 4 waves per SIMD fit in 128 VGPRs)
   PT_MARK(0, 1);
   for (int k = h; k < n; k += PREP_WAVES) {
-    size_t ci = (size_t)uni((int)d.p_list[k * NP + gp]) * NP + gp;
+    size_t ci = (size_t)(k == h ? s_first : uni((int)d.p_list[k * NP + gp])) * NP + gp;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
     if (resume && d.f_done[ci] == 1) continue;  // final (here or by its owner's message)
     double x = uni(d.c_x[ci]), y = uni(d.c_y[ci]), m = uni(d.c_m[ci]), r = uni(d.c_r[ci]);
@@ -2046,23 +2048,35 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last) 
   ArenaCtl &c = d.ctl[a];
   // round r reads how many cells failed round r-1 (nothing left: skip), counts
   // its own failures, and clears the counter round r+1 will use
+  // liveness, count and the list's first row with the round counter: one load round
+  const bool alive = d.p_alive[gp];
+  const int n = d.p_ncells[gp];
+  const int s_first = d.p_list[gp];
   if (round > 1 && c.food_undone[(round - 1) % 3] == 0) return 0;
   if (p == 0) c.food_undone[(round + 1) % 3] = 0;
-  if (!d.p_alive[gp]) return 0;
+  if (!alive) return 0;
   double rgrow = 0;
   Food F(d, a);
-  int n = d.p_ncells[gp];
   for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    if (d.f_done[ci]) continue;
-    uint32_t prio = (uint32_t)p * kMaxCells + k;
+    size_t ci = (size_t)(k == 0 ? s_first : d.p_list[k * NP + gp]) * NP + gp;
+    const int *lst = d.f_list + ci * FCAP;
+    // the food list's first entries ride the done / count loads (FCAP slots
+    // exist; entries past the count are never used)
+    int l4[kTailRegs];
+#pragma unroll
+    for (int t = 0; t < kTailRegs; t++) l4[t] = lst[t];
+    const bool done = d.f_done[ci];
     int cnt = d.f_cnt[ci];
+    if (done) continue;
+    uint32_t prio = (uint32_t)p * kMaxCells + k;
     if (cnt == kOverflow) continue;  // already in the serial work list (k_food_prep)
     bool own = true;
-    const int *lst = d.f_list + ci * FCAP;
-    if (own) {
+    {  // every reservation key of the list at once (one load round for the first entries)
       uint64_t key = food_key(d.ctl[a].food_round + round, prio);
-      for (int t = 0; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
+#pragma unroll
+      for (int t = 0; t < kTailRegs; t++)
+        if (t < cnt) own &= (*F.owner(l4[t]) == key);
+      for (int t = kTailRegs; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
     }
     if (own) {
       if (food_eat_loop(d, F, a, ci, prio, lst, cnt)) rgrow = fmax(rgrow, d.c_r[ci]);
@@ -2311,7 +2325,9 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   PT_BEGIN(3);
   const int lane = threadIdx.x & 63;
   const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gp >= d.NP || !d.p_alive[gp]) return;
+  if (gp >= d.NP) return;
+  const int s_first = d.p_list[gp];  // (list row 0 rides the liveness / count load round)
+  if (!d.p_alive[gp]) return;
   const int NP = d.NP, a = gp / d.B;
   const int *st = d.cstart + (size_t)a * (d.H + 1);
   const int *it = d.citems + (size_t)a * kMaxCells * d.B;
@@ -2320,7 +2336,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   bool anyp = false;
   PT_MARK(3, 1);
   for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+    size_t ci = (size_t)(k == 0 ? s_first : d.p_list[k * NP + gp]) * NP + gp;
     double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     PT_MARK(3, 2);
     Rect q = footprint(x, y, r, d.size);
