@@ -256,6 +256,15 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // the output row is written once and read by the host / learner, never by
   // the next tick: non-temporal stores keep it from evicting the world state
   // (the next tick's working set) out of the L2s
+  // (the history grids too: read and rewritten once per observation, ~100 us
+  // apart -- AIGAR_OBS_HIST_NT, measured)
+  auto hist_st = [](double *p, double v) __attribute__((always_inline)) {
+#ifdef AIGAR_OBS_HIST_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+  };
   auto row_st = [&](int i, OutT v) __attribute__((always_inline)) {
 #ifdef AIGAR_OBS_NO_NT
     row[i] = v;
@@ -590,19 +599,19 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     }
     if (o_sslf >= 0) {
       row_st(o_sslf + t, (OutT)o_ss);
-      sslf[t] = o_sl;
+      hist_st(sslf + t, o_sl);
     }
     if (o_slf >= 0) {
       row_st(o_slf + t, (OutT)o_sl);
-      slf[t] = vs;
+      hist_st(slf + t, vs);
     }
     if (o_eslf >= 0) {
       row_st(o_eslf + t, (OutT)o_es);
-      eslf[t] = o_el;
+      hist_st(eslf + t, o_el);
     }
     if (o_elf >= 0) {
       row_st(o_elf + t, (OutT)o_el);
-      elf[t] = ve;
+      hist_st(elf + t, ve);
     }
   }
   };

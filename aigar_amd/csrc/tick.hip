@@ -2449,13 +2449,22 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
     wave_fence();
     const int gp = a * B + P;
     PA_C(0);
+    // liveness, count and the list's first row in one load round
+    const int s_first = d.p_list[gp];
+    const int n_first = d.p_ncells[gp];
     if (!d.p_alive[gp]) continue;
-    for (int i = 0; i < d.p_ncells[gp];) {  // for playerCell in player.getCells(): live list
-      const size_t pc = (size_t)d.p_list[i * NP + gp] * NP + gp;
+    for (int i = 0;;) {  // for playerCell in player.getCells(): live list
+      if (i >= (i == 0 ? n_first : d.p_ncells[gp])) break;
+      const size_t pc = (size_t)(i == 0 ? s_first : d.p_list[i * NP + gp]) * NP + gp;
       i++;
+      // the turn cell's state rides the activity load (nothing changes it before
+      // its eat loop: the candidate walk only reads)
+      const double px = d.c_x[pc], py = d.c_y[pc];
+      const int64_t pseq = d.c_seq[pc];
+      double pm = d.c_m[pc], pr = d.c_r[pc];
       if (!active_ld(d, pc)) continue;
       active_st(d, pc, 0);
-      const Rect q0 = cell_rect(d, pc);
+      const Rect q0 = footprint(px, py, pr, d.size);  // (cell_rect)
       PA_T(1);
       int nc = 0;
       wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
@@ -2494,9 +2503,6 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         s_srt[rk] = x;
       }
       wave_fence();
-      const double px = d.c_x[pc], py = d.c_y[pc];
-      const int64_t pseq = d.c_seq[pc];
-      double pm = d.c_m[pc], pr = d.c_r[pc];
       PA_T(3);
       for (int t = 0; t < nc; t++) {
         const int k = s_srt[t];
