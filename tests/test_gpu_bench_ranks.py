@@ -1,0 +1,47 @@
+"""bench.py's N > 1 path with real steppers: two ranks launched the way the
+driver launches them (torch.distributed.run, one process per rank), here
+sharing the one GPU over the gloo backend (RCCL cannot put two ranks on one
+device).  Checks the replica aggregation on rank 0's JSON line and the C4
+side line (one C3 arena tiled 2 x 1, messages all-gathered between the ranks).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_line():
+    steps = 10
+    env = dict(os.environ, AIGAR_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", str(steps), "--warmup", "3", "--no-cpu-baseline", "--no-pixels",
+           "--batched-arenas", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == steps and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "replicas2"
+    # whole-job throughput: both replicas' bots over the max-over-ranks time
+    assert d["value"] == pytest.approx(2 * 4096 * steps / (d["ms_per_step"] * steps / 1e3), rel=1e-6)
+    assert d["world"]["alive_bots"] > 4000 and d["world"]["pellets"] > 99000
+    c4 = d["c4"]
+    assert c4["scaling"] == "strong" and "tiled 2x1" in c4["workload"]
+    assert c4["eat_passes_per_tick"] >= 1.0 and c4["exchange"]["bytes_per_rank"] > 0
+    assert c4["value"] > 0 and c4["exchange"]["avg_ms"] > 0
