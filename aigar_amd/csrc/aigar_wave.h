@@ -118,7 +118,7 @@ __device__ __forceinline__ void wave_grid_for(const int *st, const int *items, i
     for (int t0 = 0; t0 < total; t0 += 64) {
       const int t = t0 + lane;
       int row = 0;
-      for (int k = 1; k < nr; k++) row = (__shfl(excl, k) <= t) ? k : row;
+      for (int k = 1; k < nr; k++) row = (__builtin_amdgcn_readlane(excl, k) <= t) ? k : row;  // (k uniform: v_readlane)
       const int idx = __shfl(lo, row) + (t - __shfl(excl, row));
       const bool valid = t < total;
       f(valid, valid ? (items ? items[idx] : idx) : -1);

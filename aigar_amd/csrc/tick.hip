@@ -1528,7 +1528,7 @@ __device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items
     for (int t0 = 0; t0 < total; t0 += 64) {
       const int t = t0 + lane;
       int row = 0;
-      for (int k = 1; k < nr; k++) row = (__shfl(excl, k) <= t) ? k : row;
+      for (int k = 1; k < nr; k++) row = (__builtin_amdgcn_readlane(excl, k) <= t) ? k : row;  // (k uniform: v_readlane)
       const int idx = __shfl(lo, row) + (t - __shfl(excl, row));
       bool hit = t < total && pred(items ? items[idx] : idx);
       if (__ballot(hit)) return true;
@@ -2369,12 +2369,17 @@ __device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool
   const int NP = d.NP;
   int gp = (int)(e % NP);
   uint8_t slot = (uint8_t)(e / NP);
+  // the count and every list row in one load round (all kMaxCells rows exist),
+  // then the compacted list is written back
+  uint8_t l[kMaxCells];
+#pragma unroll
+  for (int k = 0; k < kMaxCells; k++) l[k] = d.p_list[k * NP + gp];
+  const int n = d.p_ncells[gp];
   d.c_flags[e] = 0;
-  int n = d.p_ncells[gp], w = 0;
-  for (int k = 0; k < n; k++) {
-    uint8_t s = d.p_list[k * NP + gp];
-    if (s != slot) d.p_list[(w++) * NP + gp] = s;
-  }
+  int w = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxCells; k++)
+    if (k < n && l[k] != slot) d.p_list[(w++) * NP + gp] = l[k];
   d.p_ncells[gp] = w;
   if (w == 0) {  // deletePlayerCell: last cell -> deadPlayers, setDead (field.py:386-388)
     ArenaCtl &c = d.ctl[a];
@@ -2435,12 +2440,21 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
   PA_T(0);
   int P = -1;
   for (;;) {
-    // next pending player > P
-    int q = P + 1, found = -1;
-    for (int wd = q >> 5; wd < NW && found < 0; wd++) {
-      uint32_t bits = pend[wd];
+    // next pending player > P: 64 bitmap words per step, one per lane, and a
+    // ballot picks the first non-empty one (a turn's scan is one LDS round, not
+    // one per word)
+    const int q = P + 1;
+    int found = -1;
+    for (int wb = q >> 5; wb < NW && found < 0; wb += 64) {
+      const int wd = wb + lane;
+      uint32_t bits = wd < NW ? pend[wd] : 0u;
       if (wd == (q >> 5)) bits &= (q & 31) ? ~((1u << (q & 31)) - 1) : 0xFFFFFFFFu;
-      if (bits) found = wd * 32 + __ffs(bits) - 1;
+      const unsigned long long bal = __ballot(bits != 0);
+      if (bal) {
+        const int l = __ffsll((long long)bal) - 1;
+        const uint32_t bw = (uint32_t)__builtin_amdgcn_readlane((int)bits, l);
+        found = (wb + l) * 32 + __ffs(bw) - 1;
+      }
     }
     if (found < 0) break;
     P = found;
@@ -2544,7 +2558,8 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         wave_fence();  // (the removal above is read by the re-activation walk)
         PA_T(4);
         PA_C(2);
-        wave_grid_for(st, it, d.cols, cell_rect(d, g), expand_for(rmax), [&](bool valid, int e) {
+        // (cell_rect(d, g) from the registers: g's position and its new radius)
+        wave_grid_for(st, it, d.cols, footprint(gx, gy, gr, d.size), expand_for(rmax), [&](bool valid, int e) {
           if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
           if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;
           active_st(d, (size_t)e, 1);
@@ -2562,7 +2577,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
           if (i - 1 < d.p_ncells[gp]) {
             const size_t sk = (size_t)d.p_list[(i - 1) * NP + gp] * NP + gp;
             const double sx = d.c_x[sk], sy = d.c_y[sk], sm = d.c_m[sk], sr = d.c_r[sk];
-            wave_grid_for(st, it, d.cols, cell_rect(d, sk), expand_for(rmax), [&](bool valid, int e) {
+            wave_grid_for(st, it, d.cols, footprint(sx, sy, sr, d.size), expand_for(rmax), [&](bool valid, int e) {
               if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gp) return;
               const double me = d.c_m[e];
               if (!(overlap(sx, sy, sm, sr, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(sm, me) || can_eat(me, sm))))
