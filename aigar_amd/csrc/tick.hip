@@ -2319,6 +2319,61 @@ __device__ __forceinline__ void occ_remove(const Dev &d, int a, Rect q) {
   }
 }
 
+// The pp pass's occupancy updates, deferred: counts by non-returning atomics
+// (no round trip per eat), the touched bit words marked in an LDS bitmap and
+// rebuilt from the final counts once the pass is over (occ_rebuild_dirty).
+// Counts are sums, so the order of the updates does not matter.
+constexpr int OCC_DW = 64;  // dirty-word bitmap: up to 2048 occupancy words (C3: 900)
+__device__ __forceinline__ void occ_mark(uint32_t *dirty, int b) {
+  const int wd = b >> 6;
+  atomicOr(&dirty[wd >> 5], 1u << (wd & 31));
+}
+__device__ __forceinline__ void occ_remove_def(const Dev &d, int a, Rect q, uint32_t *dirty) {
+  int *cnt = d.occ_cnt + (size_t)a * d.H;
+  const int w = q.x1 - q.x0 + 1, n = w * (q.y1 - q.y0 + 1);
+  for (int t = threadIdx.x & 63; t < n; t += 64) {
+    const int b = (q.y0 + t / w) * d.cols + q.x0 + t % w;
+    (void)__hip_atomic_fetch_add(&cnt[b], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    occ_mark(dirty, b);
+  }
+}
+__device__ __forceinline__ void occ_grow_def(const Dev &d, int a, Rect old, Rect q, uint32_t *dirty) {
+  int *cnt = d.occ_cnt + (size_t)a * d.H;
+  const int w = q.x1 - q.x0 + 1, n = w * (q.y1 - q.y0 + 1);
+  for (int t = threadIdx.x & 63; t < n; t += 64) {
+    const int bx = q.x0 + t % w, by = q.y0 + t / w;
+    if (bx >= old.x0 && bx <= old.x1 && by >= old.y0 && by <= old.y1) continue;
+    const int b = by * d.cols + bx;
+    (void)__hip_atomic_fetch_add(&cnt[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    occ_mark(dirty, b);
+  }
+}
+// every wave of the block: the k-th dirty word goes to wave k % waves; its 64
+// counts are read at device scope (past L1) and the word is their ballot
+__device__ void occ_rebuild_dirty(const Dev &d, int a, const uint32_t *dirty) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int *cnt = d.occ_cnt + (size_t)a * d.H;
+  unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
+  static_assert(OCC_DW == 64, "one bitmap word per lane");
+  const uint32_t mine = dirty[lane];
+  unsigned long long nz = __ballot(mine != 0);  // (usually none: no pp eat this tick)
+  int k = 0;
+  while (nz) {
+    const int i = __ffsll((long long)nz) - 1;
+    nz &= nz - 1;
+    uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mine, i);
+    while (m) {
+      const int wd = i * 32 + __ffs(m) - 1;
+      m &= m - 1;
+      if (k++ % nw != w) continue;
+      const int b = wd * 64 + lane;
+      const int c = b < d.H ? __hip_atomic_load(&cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      const unsigned long long bits = __ballot(c > 0);
+      if (lane == 0) occ[wd] = bits;
+    }
+  }
+}
+
 // one wavefront per player: cells with an overlapping enemy cell at phase start
 // (+ the player's cells into the spawn occupancy)
 __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
@@ -2408,7 +2463,9 @@ __device__ __forceinline__ void active_st(const Dev &d, size_t i, uint8_t v) {
 // (candidate gathering, re-activation after growth) are spread over the lanes.
 // Cross-lane data: the LDS candidate lists, the pending bitmap and c_active.
 constexpr int PP_LCAP = 512;
-__device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend) {
+// odirty: the deferred occupancy's dirty-word bitmap (LDS, zeroed), or NULL for
+// immediate updates
+__device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend, uint32_t *odirty) {
   // pend: pending-player bitmap (B bits, LDS)
   // candidates of the current turn, with their state at turn start (only the
   // turn's own cell changes them: what it eats dies, and it stops when eaten)
@@ -2542,10 +2599,16 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         d.c_m[g] = m;
         d.c_r[g] = mr;
         // the spawn occupancy follows: the eaten cell leaves, the eater's footprint grows
-        occ_remove(d, a, pc_eats ? footprint(ox, oy, orr, d.size) : footprint(px, py, pr, d.size));
-        wave_fence();
-        if (pc_eats) occ_grow(d, a, footprint(px, py, pr, d.size), footprint(px, py, mr, d.size));
-        else occ_grow(d, a, footprint(ox, oy, orr, d.size), footprint(ox, oy, mr, d.size));
+        if (odirty) {
+          occ_remove_def(d, a, pc_eats ? footprint(ox, oy, orr, d.size) : footprint(px, py, pr, d.size), odirty);
+          if (pc_eats) occ_grow_def(d, a, footprint(px, py, pr, d.size), footprint(px, py, mr, d.size), odirty);
+          else occ_grow_def(d, a, footprint(ox, oy, orr, d.size), footprint(ox, oy, mr, d.size), odirty);
+        } else {
+          occ_remove(d, a, pc_eats ? footprint(ox, oy, orr, d.size) : footprint(px, py, pr, d.size));
+          wave_fence();
+          if (pc_eats) occ_grow(d, a, footprint(px, py, pr, d.size), footprint(px, py, mr, d.size));
+          else occ_grow(d, a, footprint(ox, oy, orr, d.size), footprint(ox, oy, mr, d.size));
+        }
         if (pc_eats) {
           pm = m;
           pr = mr;
@@ -2637,7 +2700,7 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
   oy = (double)yp;
 }
 
-__device__ void spawn_counts(const Dev &d, int a, int init);
+__device__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait);
 // ---------------------------------------------------- closing pellet update
 // Pellets never move and only a few change per tick (eaten, spawned, converted
 // from blobs), so the end-of-tick pellet layout (bucket-sorted, double buffered)
@@ -2880,7 +2943,15 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   int a = blockIdx.x;
   if (pp) {
     extern __shared__ uint32_t pend[];
-    if (threadIdx.x < 64) pp_serial_body(d, a, scr_k, scr_v, pend);
+    __shared__ uint32_t s_odirty[OCC_DW];
+    const bool defer = d.occ_words <= OCC_DW * 32;
+    for (int i = threadIdx.x; i < OCC_DW; i += blockDim.x) s_odirty[i] = 0;
+    __syncthreads();
+    // (the barrier's workgroup release waits for wave 0's count atomics; the
+    // rebuild reads the counts at device scope, from L2)
+    if (threadIdx.x < 64) pp_serial_body(d, a, scr_k, scr_v, pend, defer ? s_odirty : nullptr);
+    __syncthreads();
+    if (defer) occ_rebuild_dirty(d, a, s_odirty);
     __syncthreads();
   }
   PT_MARK(5, 1);
@@ -2949,7 +3020,31 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   if (d.virus_enabled && (dirty & DIRTY_VIRUS)) grid_small_build<2>(d, a, gcnt, sflag);
   PT_MARK(5, 3);
   // (the spawn occupancy is built by k_pp_active and kept by the pp pass above)
-  if (tid == 0) spawn_counts(d, a, init);
+  // spawnPlayers' dead list (deadPlayers in order; respawnTime == 0 respawns):
+  // partitioned by the whole block, a chunk of T players per round (a serial
+  // loop was one load chain per dead player: ~8 us per greedy tick)
+  int n_resp = 0, n_wait = 0;
+  if (!init) {
+    const int nd = c.n_dead;
+    int *dl = d.dead + (size_t)a * d.B, *rl = d.respawn_list + (size_t)a * d.B;
+    for (int base = 0; base < nd; base += T) {
+      const int i = base + tid;
+      int p = -1;
+      bool rsp = false;
+      if (i < nd) {
+        p = dl[i];
+        rsp = d.p_respawn[(size_t)a * d.B + p] == 0;
+      }
+      int tr, tw;
+      const int rr = block_rank(i < nd && rsp, sflag, &tr);
+      const int rw = block_rank(i < nd && !rsp, sflag, &tw);  // (every read of this chunk is done)
+      if (i < nd && rsp) rl[n_resp + rr] = p;
+      if (i < nd && !rsp) dl[n_wait + rw] = p;  // (n_wait + rw <= i: never ahead of an unread entry)
+      n_resp += tr;
+      n_wait += tw;
+    }
+  }
+  if (tid == 0) spawn_counts(d, a, init, n_resp, n_wait);
   __syncthreads();
   PT_MARK(5, 4);
   if (close) {
@@ -2960,7 +3055,8 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
 }
 
 // spawnStuff's counts (field.py:227-280): pellets and viruses to add, players to respawn
-__device__ void spawn_counts(const Dev &d, int a, int init) {
+// (n_resp / n_wait: the dead list's partition, done by the caller's block when !init)
+__device__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait) {
   ArenaCtl &c = d.ctl[a];
   c.dirty = 0;
   // spawnPellets: while len(pellets) < maxCollectibleCount
@@ -2996,18 +3092,13 @@ __device__ void spawn_counts(const Dev &d, int a, int init) {
   c.n_spawn_v = kv;
   c.n_vir += kv;
   // spawnPlayers: deadPlayers in order, respawnTime == 0
-  int np = 0, w = 0;
-  int *dl = d.dead + (size_t)a * d.B;
+  int np = 0;
   int *rl = d.respawn_list + (size_t)a * d.B;
   if (init) {
     for (int p = 0; p < d.B; p++) rl[np++] = p;
   } else {
-    for (int i = 0; i < c.n_dead; i++) {
-      int p = dl[i];
-      if (d.p_respawn[(size_t)a * d.B + p] == 0) rl[np++] = p;
-      else dl[w++] = p;
-    }
-    c.n_dead = w;
+    np = n_resp;
+    c.n_dead = n_wait;
   }
   c.n_spawn_pl = np;
   if (!init) c.seq_next += np;  // at initialize() players already own seqs 0..B-1
