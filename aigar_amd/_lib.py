@@ -92,6 +92,7 @@ def load(build_if_missing=False):
         "aigar_tile_resume": [vp],
         "aigar_tile_end": [vp, vp, i32],
         "aigar_tile_exchange_local": [C.POINTER(vp), i32],
+        "aigar_tile_observers": [vp, C.POINTER(C.c_int32)],
     }
     for name, args in sig.items():
         f = getattr(L, name, None)
@@ -347,12 +348,13 @@ class Stepper:
 
     # ---- C4 tiles (include/aigar.h: aigar_tile_*)
     def tile_info(self):
-        info = (C.c_int32 * 12)()
+        info = (C.c_int32 * 14)()
         ob, ib, nb = C.c_void_p(), C.c_void_p(), C.c_int64(0)
         self._chk(self.L.aigar_tile_info(self.h, info, C.byref(ob), C.byref(ib), C.byref(nb)))
         v = list(info)
         return {"ntiles": v[0], "tile_id": v[1], "own": tuple(v[2:6]), "held": tuple(v[6:10]), "tcap": v[10],
-                "bm_words": v[11], "outbox": ob.value, "inbox": ib.value, "msg_bytes": nb.value}
+                "bm_words": v[11], "hcap": v[12], "hrec": v[13], "handoff_bytes": v[12] * v[13] * 32,
+                "outbox": ob.value, "inbox": ib.value, "msg_bytes": nb.value}
 
     def tile_msg_bytes(self):
         """Bytes of the current pass's message (the first pass sends no bitmap)."""
@@ -368,10 +370,21 @@ class Stepper:
         prm = _abi.RunParams(pol, 0, float(p_split), float(p_eject), int(seed))
         self._chk(self.L.aigar_tile_begin(self.h, C.byref(prm)))
 
-    def tile_apply(self):
+    def tile_apply(self, wait=True):
+        """Apply the gathered messages; wait: return the owned cells still undone on
+        all tiles (a host round trip), else None (the next pass gates itself)."""
+        if not wait:
+            self._chk(self.L.aigar_tile_apply(self.h, None))
+            return None
         u = C.c_int(0)
         self._chk(self.L.aigar_tile_apply(self.h, C.byref(u)))
         return u.value
+
+    def tile_observers(self):
+        """Per player: the tile that computed its row at the last observation (-1: dead)."""
+        out = np.zeros(self.NP, np.int32)
+        self._chk(self.L.aigar_tile_observers(self.h, out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out
 
     def tile_resume(self):
         self._chk(self.L.aigar_tile_resume(self.h))

@@ -63,6 +63,7 @@ struct ArenaCtl {
   // tile ate this tick, this pass's outbox fill / pellet kills / undone owned
   // cells, and the undone owned cells of all tiles after the last exchange
   int n_pel_glob, n_eaten_glob, n_out, n_out_pel, n_undone, n_undone_glob;
+  int n_ho;  // observation history hand-off slots in this tile's first-pass message
   // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
   // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
   int64_t stat[8];
@@ -70,7 +71,9 @@ struct ArenaCtl {
 
 enum : uint32_t {
   ERR_PELLET_CAP = 1, ERR_BLOB_CAP = 2, ERR_VIRUS_CAP = 4, ERR_EVENT_CAP = 8, ERR_WORK_CAP = 16,
-  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256, ERR_TILE_CAP = 512, ERR_TILE_LOOKUP = 1024
+  ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256, ERR_TILE_CAP = 512, ERR_TILE_LOOKUP = 1024,
+  ERR_TILE_OBS = 2048,    // a tile observed a bot whose view reaches beyond its held pellets
+  ERR_TILE_PASSES = 4096  // a device-bounded tiled tick ended with owned cells undone
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
@@ -86,18 +89,31 @@ enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4
 // the pellets whose centre bucket lies in its tile plus a halo.  The eat phase
 // is resolved per tile; the outcomes of the cells a tile owns (centre bucket in
 // the tile) travel in one all-gathered message per pass:
-//   outbox = [TR_HDR][tcap records][final-cell bitmap, 16 * NP bits]
+//   first pass of a tick: [TR_HDR][tcap records][hcap hand-off slots of hrec records]
+//   later passes:         [TR_HDR][tcap records][final-cell bitmap, 16 * NP bits]
+// Observation ownership: a bot is observed by ONE tile; its last-frame history
+// grids (bot.py:480-495) live there.  t_holder[gp] names the tile whose copy is
+// current (-1: every tile's copy is); a bot whose view centre left its holder's
+// tile, or that died, has its history handed off in the next tick's first
+// message (slot = [TR_HIST rec: idx = player, x = lastFovSize][nh grids]) and
+// every tile applies it, so any tile can take the bot over.
 struct TileRec {
-  int32_t kind, idx;  // TR_*; idx: blob slot / cell pool index / (header) record count
+  int32_t kind, idx;  // TR_*; idx: blob slot / cell pool index / player / (header) record count
   int64_t seq;        // pellet creation sequence / (header) undone owned cells
-  double x, y;        // pellet position / cell mass, radius / (header) pellet kills, -
+  double x, y;        // pellet position / cell mass, radius / lastFovSize / (header) pellet kills, hand-off slots
 };
-enum : int32_t { TR_HDR = 0, TR_PELLET = 1, TR_BLOB = 2, TR_CELL = 3 };
+enum : int32_t { TR_HDR = 0, TR_PELLET = 1, TR_BLOB = 2, TR_CELL = 3, TR_HIST = 4 };
+constexpr int kHcapMax = 256;  // hand-off slots per message (LDS list of the plan kernel)
 
 struct Dev {
   int A, B, NP, size, cols, H;
   int tiled, tile_id, ntiles, tcap, bm_words;  // tcap: records per outbox; bm_words: u64 words of the bitmap
   int tile_flags;                              // AIGAR_TILE_*
+  int tile_nx, tile_ny;                        // tile grid (tile_id = iy * tile_nx + ix)
+  int tile_gate;  // a later eat pass issued without a host decision: its kernels do nothing once no owned cell is undone
+  int hcap, hrec, nh;  // hand-off slots per message, records per slot, history grids per bot (0..4)
+  int *t_holder;  // [NP] tile holding the bot's current observation history, -1: every tile
+  int *t_obsby;   // [NP] tile that observed the bot since the last plan, -1: none
   int own_bx0, own_bx1, own_by0, own_by1;      // owned centre buckets [x0, x1) x [y0, y1)
   int loc_bx0, loc_bx1, loc_by0, loc_by1;      // held pellets: owned range + halo
   TileRec *outbox;       // [1 + tcap] records + bitmap

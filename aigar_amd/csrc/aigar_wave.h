@@ -66,6 +66,28 @@ __device__ __forceinline__ bool tile_near_rect(const Dev &d, Rect r, int e) {
   return !d.tiled || (r.x0 <= r.x1 && r.y0 <= r.y1 && r.x1 >= d.loc_bx0 - e && r.x0 < d.loc_bx1 + e &&
                       r.y1 >= d.loc_by0 - e && r.y0 < d.loc_by1 + e);
 }
+// the tile owning the centre bucket of (x, y) (tile k owns buckets
+// [k * cols / n, (k + 1) * cols / n) along each axis, as aigar_create cuts them)
+__device__ __forceinline__ int tile_of(const Dev &d, double x, double y) {
+  const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
+  int ix = 0, iy = 0;
+  for (int i = 1; i < d.tile_nx; i++) ix = bx >= i * d.cols / d.tile_nx ? i : ix;
+  for (int i = 1; i < d.tile_ny; i++) iy = by >= i * d.cols / d.tile_ny ? i : iy;
+  return iy * d.tile_nx + ix;
+}
+// the j-th observation-history grid a bot keeps (the ones the channels need, in
+// the order self LF, self SLF, enemy LF, enemy SLF): the hand-off slot layout
+__device__ __forceinline__ double *hist_grid(const Dev &d, int j) {
+  const uint32_t ch = d.obs_ch;
+  const int s = (ch & (AIGAR_OBS_SELF_LF | AIGAR_OBS_SELF_SLF)) ? 1 : 0, ss = (ch & AIGAR_OBS_SELF_SLF) ? 1 : 0;
+  const int e = (ch & (AIGAR_OBS_ENEMY_LF | AIGAR_OBS_ENEMY_SLF)) ? 1 : 0;
+  if (s && j == 0) return d.o_self_lf;
+  j -= s;
+  if (ss && j == 0) return d.o_self_slf;
+  j -= ss;
+  if (e && j == 0) return d.o_en_lf;
+  return d.o_en_slf;
+}
 
 // Wave-parallel walk over the grid rows around q (expanded by E): the rows'
 // item ranges are loaded by one lane each and flattened with a prefix sum, so

@@ -20,7 +20,7 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp);
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v);
 void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first);
-void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs);
+void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch,
                     const uint8_t *mask = nullptr);
@@ -78,6 +78,8 @@ struct aigar_handle {
   std::vector<void *> allocs;
   int box_recs = 0;   // C4: TileRec slots of a full exchange message (header + records + bitmap)
   int pass_recs = 0;  // ... of the current pass's message (the first pass sends no bitmap)
+  int first_pass = 0;  // the current pass is the tick's first (its message carries the history hand-off)
+  hipEvent_t ev_x = nullptr;  // in-process transport: this handle's outbox is written / its inbox is filled
   bool profile = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // timer name -> recorded (start, stop) event pairs, resolved lazily
@@ -141,6 +143,7 @@ static void free_all(aigar_handle *h) {
   h->pix_bytes = 0;
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->ev_x) (void)hipEventDestroy(h->ev_x);
   for (auto &m : h->marks) {
     (void)hipEventDestroy(m.second.first);
     (void)hipEventDestroy(m.second.second);
@@ -242,6 +245,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
     // reach <= 6 buckets from its centre bucket at the mass cap: with 7 its owner
     // holds every food it can touch, so every cell is decidable somewhere
     const int hb = std::max(7, (halo + kBucket - 1) / kBucket);
+    if (d.ntiles > 64) return bad("at most 64 tiles");
     d.tile_id = cfg->tile_id;
     d.tile_flags = cfg->tile_flags;
     d.own_bx0 = ix * d.cols / tx;
@@ -253,9 +257,21 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
     d.loc_by0 = std::max(0, d.own_by0 - hb);
     d.loc_by1 = std::min(d.cols, d.own_by1 + hb);
   }
+  d.tile_nx = tx;
+  d.tile_ny = ty;
+  d.tile_gate = 0;
   d.tcap = cfg->tile_cap > 0 ? cfg->tile_cap : 2048;
   d.bm_words = (int)(((size_t)kMaxCells * d.NP + 255) / 256 * 4);  // 16 * NP bits, whole TileRecs
-  h->box_recs = 1 + d.tcap + d.bm_words / 4;
+  // observation-history hand-off: the grids the observation keeps per bot
+  // (self / enemy, last / second-last frame), 4 doubles per 32-byte record
+  {
+    const uint32_t ch = cfg->obs_channels;
+    d.nh = ((ch & (AIGAR_OBS_SELF_LF | AIGAR_OBS_SELF_SLF)) ? 1 : 0) + ((ch & AIGAR_OBS_SELF_SLF) ? 1 : 0) +
+           ((ch & (AIGAR_OBS_ENEMY_LF | AIGAR_OBS_ENEMY_SLF)) ? 1 : 0) + ((ch & AIGAR_OBS_ENEMY_SLF) ? 1 : 0);
+    d.hrec = 1 + (d.nh * G * G + 3) / 4;
+    d.hcap = std::min(kHcapMax, std::max(16, d.tcap / 64));
+  }
+  h->box_recs = 1 + d.tcap + std::max(d.bm_words / 4, d.hcap * d.hrec);
   for (int k = 0; k <= kMaxCells; k++) d.pow_n032[k] = aigar_math::pow_glibc((double)k, 0.32);
   d.cshift = 3;  // coarse blob/virus grids: 160 x 160 field units per cell, <= 4096 cells (grid_small_build)
   while ((((d.cols + (1 << d.cshift) - 1) >> d.cshift) * ((d.cols + (1 << d.cshift) - 1) >> d.cshift)) > 4096)
@@ -321,6 +337,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(p_time, int, NP);
   AL(o_last_mass, double, NP);
   if (d.tiled) {
+    AL(t_holder, int, NP);
+    AL(t_obsby, int, NP);
     AL(outbox, TileRec, h->box_recs);
     TileRec *ib = nullptr;
     ib = dalloc<TileRec>(h, (size_t)h->box_recs * d.ntiles);
@@ -371,7 +389,9 @@ static int check_device_errors(aigar_handle *h) {
   for (int a = 0; a < h->d.A; a++)
     if (ctl[a].err)
       return fail("device error bits 0x%x in arena %d (1 pellet cap, 2 blob cap, 4 virus cap, 8 event cap, "
-                  "16 worklist cap, 32 observation cap, 64 candidate cap, 128 slot, 256 pixel-frame object cap)",
+                  "16 worklist cap, 32 observation cap, 64 candidate cap, 128 slot, 256 pixel-frame object cap, "
+                  "512 tile message cap, 1024 tile record lookup, 2048 tile view beyond the held pellets, "
+                  "4096 tiled tick ended with undone cells)",
                   ctl[a].err, a);
   return 0;
 }
@@ -399,6 +419,10 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   HIPCHK(hipMemsetAsync(d.o_act_cur, 0, sizeof(double) * NP * 4, h->stream));
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
     HIPCHK(hipMemsetAsync(p, 0, sizeof(double) * NP * GG, h->stream));
+  if (d.tiled) {  // every tile's history copy is current (all zero)
+    HIPCHK(hipMemsetAsync(d.t_holder, 0xFF, sizeof(int) * NP, h->stream));
+    HIPCHK(hipMemsetAsync(d.t_obsby, 0xFF, sizeof(int) * NP, h->stream));
+  }
   launch_reset(d, h->stream, seed);
   HIPCHK(hipGetLastError());
   return check_device_errors(h);
@@ -531,8 +555,8 @@ extern "C" int aigar_tile_info(aigar_handle *h, int32_t *info, void **outbox, vo
   if (need_tiled(h)) return -1;
   const Dev &d = h->d;
   if (info) {
-    const int32_t v[12] = {d.ntiles, d.tile_id, d.own_bx0, d.own_bx1, d.own_by0, d.own_by1,
-                           d.loc_bx0, d.loc_bx1, d.loc_by0, d.loc_by1, d.tcap, d.bm_words};
+    const int32_t v[14] = {d.ntiles, d.tile_id, d.own_bx0, d.own_bx1, d.own_by0, d.own_by1,
+                           d.loc_bx0, d.loc_bx1, d.loc_by0, d.loc_by1, d.tcap, d.bm_words, d.hcap, d.hrec};
     memcpy(info, v, sizeof v);
   }
   if (outbox) *outbox = d.outbox;
@@ -565,18 +589,21 @@ extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
   Mark m(h, "tile_begin");
   launch_tick_pre(h->d, h->stream, h->scr_k, h->scr_v, &rp);
   launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 1);
-  h->pass_recs = 1 + h->d.tcap;
+  h->pass_recs = 1 + h->d.tcap + h->d.hcap * h->d.hrec;  // (+ the observation-history hand-off slots)
+  h->first_pass = 1;
   HIPCHK(hipGetLastError());
   return 0;
 }
 extern "C" int aigar_tile_apply(aigar_handle *h, int *undone) {
-  if (need_tiled(h) || !undone) return undone ? -1 : fail("null argument");
+  if (need_tiled(h)) return -1;
+  if (!h->pass_recs) return fail("tile_apply: no pass begun");
   HIPCHK(hipSetDevice(h->cfg.device));
   {
     Mark m(h, "tile_apply");
-    launch_tile_apply(h->d, h->stream, h->pass_recs);
+    launch_tile_apply(h->d, h->stream, h->pass_recs, h->first_pass);
   }
   HIPCHK(hipGetLastError());
+  if (!undone) return 0;  // device-decided passes: no host round trip (aigar_tile_resume gates itself)
   ArenaCtl c;
   HIPCHK(hipMemcpyAsync(&c, h->d.ctl, sizeof c, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -589,7 +616,8 @@ extern "C" int aigar_tile_resume(aigar_handle *h) {
   HIPCHK(hipSetDevice(h->cfg.device));
   Mark m(h, "tile_resume");
   launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 0);
-  h->pass_recs = h->box_recs;
+  h->pass_recs = 1 + h->d.tcap + h->d.bm_words / 4;
+  h->first_pass = 0;
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -609,23 +637,58 @@ extern "C" int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype) {
   return 0;
 }
 // in-process transport: every handle's outbox into every handle's inbox slot
+// No host synchronisation: each source's outbox is complete when its stream
+// reaches the recorded event (every destination waits for it before copying),
+// and every source's later work (the next pass rewrites its outbox) waits for
+// all destinations' copies.
 extern "C" int aigar_tile_exchange_local(aigar_handle **hs, int n) {
   if (!hs || n < 1) return fail("null argument");
+  uint64_t seen = 0;
   for (int i = 0; i < n; i++) {
     if (need_tiled(hs[i])) return -1;
     if (hs[i]->d.ntiles != n || hs[i]->pass_recs != hs[0]->pass_recs || hs[i]->pass_recs == 0)
       return fail("tile_exchange_local: tiles are not at the same pass");
+    const uint64_t bit = 1ull << hs[i]->d.tile_id;
+    if (seen & bit) return fail("tile_exchange_local: tile %d appears twice", hs[i]->d.tile_id);
+    seen |= bit;
     HIPCHK(hipSetDevice(hs[i]->cfg.device));
-    HIPCHK(hipStreamSynchronize(hs[i]->stream));
+    if (!hs[i]->ev_x) HIPCHK(hipEventCreateWithFlags(&hs[i]->ev_x, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(hs[i]->ev_x, hs[i]->stream));  // outbox written
   }
   const size_t bytes = (size_t)hs[0]->pass_recs * sizeof(TileRec);
-  for (int i = 0; i < n; i++)
+  for (int i = 0; i < n; i++) {
+    HIPCHK(hipSetDevice(hs[i]->cfg.device));
+    for (int k = 0; k < n; k++)
+      if (k != i) HIPCHK(hipStreamWaitEvent(hs[i]->stream, hs[k]->ev_x, 0));
+  }
+  for (int i = 0; i < n; i++) {
+    HIPCHK(hipSetDevice(hs[i]->cfg.device));
     for (int k = 0; k < n; k++) {
       const aigar_handle *src = hs[k];
       HIPCHK(hipMemcpyAsync((char *)hs[i]->d.inbox + (size_t)src->d.tile_id * bytes, src->d.outbox, bytes,
                             hipMemcpyDeviceToDevice, hs[i]->stream));
     }
+  }
+  for (int i = 0; i < n; i++) {  // inbox i filled (re-recorded: the outbox events are waited on already)
+    HIPCHK(hipSetDevice(hs[i]->cfg.device));
+    HIPCHK(hipEventRecord(hs[i]->ev_x, hs[i]->stream));
+  }
+  for (int k = 0; k < n; k++) {
+    HIPCHK(hipSetDevice(hs[k]->cfg.device));
+    for (int i = 0; i < n; i++)
+      if (i != k) HIPCHK(hipStreamWaitEvent(hs[k]->stream, hs[i]->ev_x, 0));
+  }
   return 0;
+}
+
+// the tile that computed each bot's row at the last observation (-1: dead /
+// not observed); every tile computes the same assignment
+extern "C" int aigar_tile_observers(aigar_handle *h, int32_t *out) {
+  if (need_tiled(h) || !out) return out ? -1 : fail("null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipMemcpyAsync(out, h->d.t_obsby, sizeof(int32_t) * h->d.NP, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return check_device_errors(h);
 }
 
 // One learner decision for every player (bot.py:166-233 batched, the loop of
@@ -1211,6 +1274,10 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
                      __builtin_nan(""));
   for (double *p : {d.o_self_lf, d.o_self_slf, d.o_en_lf, d.o_en_slf})
     HIPCHK(hipMemsetAsync(p + p0 * GG, 0, 8 * B * GG, h->stream));
+  if (d.tiled) {
+    HIPCHK(hipMemsetAsync(d.t_holder, 0xFF, sizeof(int) * d.NP, h->stream));
+    HIPCHK(hipMemsetAsync(d.t_obsby, 0xFF, sizeof(int) * d.NP, h->stream));
+  }
   launch_player_fov(d, h->stream);  // FOV cache of the loaded players
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;

@@ -285,6 +285,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
     return;
   }
+  if (d.tiled) {  // C4: one tile observes the bot -- its history holder, else its view centre's tile (k_tile_plan)
+    const int hold = d.t_holder[gp];
+    const int by = hold >= 0 ? hold : tile_of(d, fx, fy);
+    if (lane == 0) d.t_obsby[gp] = by;  // (every tile records the same observer)
+    if (by != d.tile_id) return;
+  }
   // own cells (getPortionOfCellsInFov(player.getCells())), loaded up front
   double ox = 0, oy = 0, orad = 0, omass = 0;
   if (lane < ncell) {
@@ -298,12 +304,11 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const int cols = (int)ceil(fs / gs);
   const double lim = fs - 1;
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
-  // C4 tiles: a bot whose view reaches beyond the held pellets gets its pellet
-  // channel from the tiles that hold them all (NaN here); everything else --
-  // cells, viruses, walls and the last-frame history, all replicated -- every
-  // tile computes, so the history stays the same on every tile
+  // C4 tiles: the observing tile must hold every pellet the view can see; one
+  // that does not (a halo below the view's reach) is an error, and the pellet
+  // channel is NaN
   const bool held = tile_holds_rect(d, rect_grow(Q, 1, d.cols));
-  if (!held && lane == 0 && alive && tile_owns(d, fx, fy)) atomicOr(&d.ctl[a].warn, WARN_TILE_OBS);  // halo < view / 2
+  if (!held && lane == 0) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
   // owner of cell pool index g = slot * NP + player, without a 64-bit modulo
   const double inv_np = 1.0 / NP;
   auto pool_owner = [&](size_t g) {

@@ -37,6 +37,13 @@
 namespace aigar {
 
 #define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
+// C4: a later eat pass issued without a host decision (aigar_tile_apply with no
+// readback) does nothing once the last exchange left no owned cell undone on any
+// tile -- the count is in every tile's ArenaCtl, written by k_tile_apply
+#define TILE_GATE(d)                                          \
+  do {                                                        \
+    if ((d).tile_gate && (d).ctl[0].n_undone_glob == 0) return; \
+  } while (0)
 
 // Diagnostics build only (-DAIGAR_PHASE_TIMING, tools/phase_timing.py): per
 // wave, its start time (slot 0, low 32 bits of the 100 MHz wall clock) and the
@@ -1821,6 +1828,7 @@ constexpr int PREP_WAVES = 1;  // wavefronts per player (wave h takes cells h, h
 // are skipped.  resume: only cells not yet final (f_done != 1) are prepared.
 __device__ __forceinline__ double tile_rall() { return sqrt(kMaxMass / kPi) * (1 + 1e-9); }  // any cell's radius bound
 __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int resume) {
+  TILE_GATE(d);
   __shared__ int64_t s_seq[4][PREP_CAND];
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
   __shared__ int s_idx[4][PREP_CAND];
@@ -2107,6 +2115,7 @@ __device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v
 // (wave 0, arena after arena; the grid's extra blocks do not take part)
 __global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last, int64_t *scr_k, int *scr_v,
                                                      int rounds, int fold) {
+  TILE_GATE(d);
   const int ncommit = (d.NP + 255) / 256;
   if ((int)blockIdx.x >= ncommit) {  // extra blocks: player-cell grid counts (round 1), scatter (round 2)
     const int e = blockIdx.x - ncommit, nb = cgrid_blocks(d);
@@ -2276,6 +2285,7 @@ __device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v
   }
 }
 __global__ void __launch_bounds__(64) k_food_serial(Dev d, int64_t *scr_k, int *scr_v, int rounds) {
+  TILE_GATE(d);
   food_serial_body(d, blockIdx.x, scr_k, scr_v, rounds);
 }
 
@@ -2380,6 +2390,8 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   PT_BEGIN(3);
   const int lane = threadIdx.x & 63;
   const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // C4, device-bounded eat passes: the tick may go on only if no owned cell is undone
+  if (d.tiled && gp == 0 && lane == 0 && d.ctl[0].n_undone_glob != 0) atomicOr(&d.ctl[0].err, ERR_TILE_PASSES);
   if (gp >= d.NP) return;
   const int s_first = d.p_list[gp];  // (list row 0 rides the liveness / count load round)
   if (!d.p_alive[gp]) return;
@@ -3662,12 +3674,97 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
 // appended by the eat loops; the bitmap marks the owned cells now final; the
 // header carries the record count, the owned cells left undone and the pellet
 // kills.
-__global__ void k_tile_pass_begin(Dev d, int first) {
+__global__ void k_tile_pass_begin(Dev d) {  // a later pass
   ArenaCtl &c = d.ctl[0];
   c.n_out = c.n_out_pel = c.n_undone = 0;
-  if (first) c.n_eaten_glob = 0;
+  c.n_ho = 0;
+}
+// The tick's first pass opens with the observation hand-off plan (one block;
+// every tile computes the same plan from replicated state).  A bot's history is
+// current on t_holder (-1: on every tile), or on the tile that observed it since
+// the last plan (t_obsby).  It is handed off -- sent by its holder, applied by
+// every tile, t_holder := -1 -- when the bot is dead (it respawns anywhere) or
+// its view centre (the FOV cache, end of the last tick) lies in another tile;
+// otherwise the holder observes it again and, the centre having moved at most one
+// tick's distance from its tile, the held halo covers the view.  At most hcap
+// bots per holder per tick (in player order); the rest wait a tick.
+__global__ void __launch_bounds__(1024) k_tile_plan(Dev d) {
+  __shared__ int wcnt[16][64];
+  __shared__ int run[64];
+  __shared__ int sl_gp[kHcapMax];
+  ArenaCtl &c = d.ctl[0];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, T = d.ntiles;
+  if (tid == 0) {
+    c.n_out = c.n_out_pel = c.n_undone = 0;
+    c.n_eaten_glob = 0;
+  }
+  if (tid < T) run[tid] = 0;
+  __syncthreads();
+  for (int base = 0; base < d.NP; base += 1024) {
+    const int gp = base + tid;
+    int h = -1;
+    bool tr = false;
+    if (gp < d.NP) {
+      h = d.t_holder[gp];
+      const int ob = d.t_obsby[gp];
+      if (ob >= 0) {
+        h = ob;
+        d.t_obsby[gp] = -1;
+      }
+      if (h >= 0) tr = !d.p_alive[gp] || tile_of(d, d.p_fx[gp], d.p_fy[gp]) != h;
+    }
+    int lrank = 0;
+    for (int k = 0; k < T; k++) {  // rank among this chunk's hand-offs of the same holder
+      const unsigned long long m = __ballot(tr && h == k);
+      if (tr && h == k) lrank = __popcll(m & ((1ull << lane) - 1));
+      if (lane == 0) wcnt[w][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (tid < T) {  // exclusive prefix over the waves, carried over the chunks
+      int r = run[tid];
+      for (int v = 0; v < 16; v++) {
+        const int t = wcnt[v][tid];
+        wcnt[v][tid] = r;
+        r += t;
+      }
+      run[tid] = r;
+    }
+    __syncthreads();
+    if (gp < d.NP) {
+      int hn = h;
+      if (tr) {
+        const int rank = lrank + wcnt[w][h];
+        if (rank < d.hcap) {
+          hn = -1;
+          if (h == d.tile_id) sl_gp[rank] = gp;
+        }
+      }
+      d.t_holder[gp] = hn;
+    }
+    __syncthreads();
+  }
+  const int nho = min(run[d.tile_id], d.hcap);
+  if (tid == 0) c.n_ho = nho;
+  // this tile's slots: [TR_HIST: player, lastFovSize][nh history grids]
+  const int GG = d.G * d.G, per = d.nh * GG;
+  TileRec *ho = d.outbox + 1 + d.tcap;
+  for (int e = tid; e < nho * (1 + per); e += 1024) {
+    const int sl = e / (1 + per), j = e - sl * (1 + per), gp = sl_gp[sl];
+    TileRec *slot = ho + (size_t)sl * d.hrec;
+    if (j == 0) {
+      slot->kind = TR_HIST;
+      slot->idx = gp;
+      slot->seq = 0;
+      slot->x = d.o_lastfov[gp];
+      slot->y = 0;
+    } else {
+      const int q = j - 1, g = q / GG, t = q - g * GG;
+      ((double *)(slot + 1))[q] = hist_grid(d, g)[(size_t)gp * GG + t];
+    }
+  }
 }
 __global__ void __launch_bounds__(256) k_tile_collect(Dev d, int with_bitmap) {
+  TILE_GATE(d);
   const int gp = GTID;
   if (gp >= d.NP || !d.p_alive[gp]) return;
   unsigned long long *bm = (unsigned long long *)(d.outbox + 1 + d.tcap);
@@ -3688,13 +3785,18 @@ __global__ void k_tile_header(Dev d) {
   h.idx = min(c.n_out, d.tcap);
   h.seq = c.n_undone;
   h.x = (double)c.n_out_pel;
-  h.y = 0;
+  h.y = (double)c.n_ho;
 }
 // The first pass's message has no bitmap: a tick that needs a second pass
 // learns the other tiles' non-eating final cells from the second pass's
 // bitmaps (it may take one pass longer; ticks rarely need a second at all).
-void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first) {
-  hipLaunchKernelGGL(k_tile_pass_begin, dim3(1), dim3(1), 0, s, d, first);
+// A later pass is gated (Dev::tile_gate): issued without asking the host whether
+// it is needed, its kernels return at once when no owned cell is undone.
+void launch_tile_pass(const Dev &d0, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first) {
+  Dev d = d0;
+  d.tile_gate = first ? 0 : 1;
+  if (first) hipLaunchKernelGGL(k_tile_plan, dim3(1), dim3(1024), 0, s, d);
+  else hipLaunchKernelGGL(k_tile_pass_begin, dim3(1), dim3(1), 0, s, d);
   launch_food(d, s, rounds, Scratch{scr_k, scr_v}, first ? 0 : 1);
   if (!first) (void)hipMemsetAsync(d.outbox + 1 + d.tcap, 0, 8 * (size_t)d.bm_words, s);
   hipLaunchKernelGGL(k_tile_collect, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, first ? 0 : 1);
@@ -3704,8 +3806,9 @@ void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, i
 // new masses), their final cells, and the totals (thread 0)
 // box_recs: records per inbox slot (the pass's message size); bitmaps only when
 // the messages carry them (box_recs covers them)
-__global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
-  const int T = d.ntiles, nrec = T * d.tcap, nbm = box_recs > 1 + d.tcap ? T * d.bm_words : 0;
+// (first: the messages carry the observation-history hand-off slots instead of bitmaps)
+__global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int first) {
+  const int T = d.ntiles, nrec = T * d.tcap, nbm = first ? 0 : T * d.bm_words;
   int gi = GTID;
   ArenaCtl &c = d.ctl[0];
   if (gi == 0) {
@@ -3756,6 +3859,23 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
     return;
   }
   gi -= nrec;
+  if (first) {  // hand-off slots: every tile takes the sender's history copy (k_tile_plan)
+    const int GG = d.G * d.G, per = d.nh * GG, slot_e = 1 + per, nho = T * d.hcap * slot_e;
+    if (gi >= nho) return;
+    const int k = gi / (d.hcap * slot_e), r = gi - k * d.hcap * slot_e, sl = r / slot_e, j = r - sl * slot_e;
+    const TileRec *box = d.inbox + (size_t)k * box_recs;
+    if (k == d.tile_id || sl >= (int)box[0].y) return;
+    const TileRec *slot = box + 1 + d.tcap + (size_t)sl * d.hrec;
+    const int gp = slot->idx;
+    if (slot->kind != TR_HIST || gp < 0 || gp >= d.NP) return set_err(d, 0, ERR_TILE_LOOKUP);
+    if (j == 0) {
+      d.o_lastfov[gp] = slot->x;
+    } else {
+      const int q = j - 1, g = q / GG, t = q - g * GG;
+      hist_grid(d, g)[(size_t)gp * GG + t] = ((const double *)(slot + 1))[q];
+    }
+    return;
+  }
   if (gi < nbm) {
     const int k = gi / d.bm_words, w = gi - k * d.bm_words;
     if (k == d.tile_id) return;
@@ -3767,9 +3887,10 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs) {
     }
   }
 }
-void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs) {
-  const long n = (long)d.ntiles * (d.tcap + (box_recs > 1 + d.tcap ? d.bm_words : 0));
-  hipLaunchKernelGGL(k_tile_apply, dim3(nblk(n, 256)), dim3(256), 0, s, d, box_recs);
+void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first) {
+  const long extra = first ? (long)d.hcap * (1 + d.nh * d.G * d.G) : d.bm_words;
+  const long n = (long)d.ntiles * (d.tcap + extra);
+  hipLaunchKernelGGL(k_tile_apply, dim3(nblk(n, 256)), dim3(256), 0, s, d, box_recs, first);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty

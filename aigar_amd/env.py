@@ -19,11 +19,15 @@ each tick against the lastMass of the previous decision); the observation is
 Bot.getStateRepresentation of every NN player (NaN rows for dead players, where
 the reference returns None).
 
-Episodes (aigar.py:833-837, 876-887): an arena whose world has run RESET_LIMIT
-ticks is reset (Model.resetModel + the bots' reset) and reported in `done`.
-With several arenas the reset timers start staggered by RESET_LIMIT / n_arenas,
-as the reference desynchronises its collectors, so arenas do not all restart
-in the same decision.
+Episodes (aigar.py:833-837, 876-887): an arena's episode ends after the
+decision in which its tick count passes RESET_LIMIT - FRAME_SKIP_RATE + 2 (the
+reference's collector test); the arena is then reset (Model.resetModel + the
+bots' reset) and reported in `done`.  With several arenas the game stages are
+desynchronised the way the reference desynchronises its collectors: before the
+first decision arena k has played k * int(RESET_LIMIT / n_arenas) ticks of its
+own world with its own population (the NN players on random actions during
+that warm-up, the reference's untrained networks), then every bot is reset
+(Model.resetBots).
 """
 import numpy as np
 
@@ -76,18 +80,57 @@ class AgarVecEnv:
         self._nn_u8 = self.nn.to(torch.uint8)
         self._mixed = bool((self.roles != _abi.ROLE_NN).any())
         self.reset_limit = int(g("RESET_LIMIT", 20000) if reset_limit is None else reset_limit)
+        self.desync = bool(desync) and self.reset_limit > 0 and n_arenas > 1
         self.age = np.zeros(n_arenas, np.int64)
-        if desync and self.reset_limit > 0:  # aigar.py:833-837: collector k starts (k-1) R / N ticks in
-            self.age = (np.arange(n_arenas) * self.reset_limit) // n_arenas
         self._resets = 0
         self.obs = torch.empty((self.NP, self.stepper.obs_len), dtype=torch.float64, device=self.dev)
+        self._mask = torch.zeros(self.NP, dtype=torch.uint8, device=self.dev)  # (persistent: read on the stepper's stream)
         self._r = torch.empty(self.NP, dtype=torch.float64, device=self.dev)
         self._act = {}  # n_act -> persistent action buffer (the decision graph is keyed by its address)
 
     def reset(self, seed=None):
-        """Field.reset + every bot's reset (lastMass = None, history grids cleared)."""
-        self.stepper.reset(self.seed if seed is None else seed)
+        """Field.reset + every bot's reset (lastMass = None, history grids cleared);
+        with several arenas, the desynchronising warm-up (aigar.py:833-837)."""
+        seed = self.seed if seed is None else int(seed)
+        self.stepper.reset(seed)
+        self.age[:] = 0
+        self._resets = 0
+        if self.desync:
+            self._desynchronise(seed)
         return self.observe()
+
+    def _desynchronise(self, seed):
+        """Arena k plays k * int(R / N) ticks from a fresh world before the first
+        decision (collector k + 1 of aigar.py:833-837): all arenas are stepped
+        together for (N - 1) * int(R / N) ticks and arena k gets its fresh world when
+        k * int(R / N) of them are left; then Model.resetBots for every arena."""
+        per = self.reset_limit // self.A
+        total = (self.A - 1) * per
+        has_g, has_r = bool((self.roles == _abi.ROLE_GREEDY).any()), bool((self.roles == _abi.ROLE_RANDOM).any())
+        greedy = self.torch.as_tensor(self.roles == _abi.ROLE_GREEDY, device=self.dev).to(self.torch.uint8)
+        gsplit = bool(getattr(self.parameters, "ENABLE_GREEDY_SPLIT", False)) if self.parameters is not None else False
+        for t in range(total + 1):
+            for a in range(self.A):
+                if t > 0 and total - a * per == t:
+                    self.stepper.reset_arena(a, seed + 104729 * (a + 1))
+            if t == total:
+                break
+            # NN players: random points in their view (an untrained network's moves);
+            # Greedy / Random bots: their own device policies
+            self.stepper.policy_random(0.0, 0.0, seed ^ 0x5DEECE66D)
+            if has_g:
+                self.stepper.policy_greedy(gsplit, greedy)
+            if has_r:
+                self.stepper.policy_random_bots()
+            self.stepper.step(1)
+        for a in range(self.A):  # Model.resetBots: every bot of every arena (the world goes on)
+            self.stepper.load_state(self.stepper.get_state(a), a)
+        self.age[:] = np.arange(self.A) * per
+
+    def episode_over(self):
+        """Arenas whose episode is over: the collector's test step > RESET_LIMIT -
+        FRAME_SKIP_RATE + 2 (aigar.py:876)."""
+        return self.age > self.reset_limit - self.skip + 2
 
     def observe(self):
         """A fresh tensor: the device buffer is rewritten by the next decision, so
@@ -102,7 +145,7 @@ class AgarVecEnv:
         if self.reset_limit <= 0:
             return done
         self.age += self.skip + 1
-        ended = np.nonzero(self.age >= self.reset_limit)[0]
+        ended = np.nonzero(self.episode_over())[0]
         if not len(ended):
             return done
         mask = np.zeros(self.NP, np.uint8)
@@ -114,7 +157,8 @@ class AgarVecEnv:
         done[torch.as_tensor(mask.astype(bool), device=self.dev)] = True
         # the new episodes' first states (NN players of the reset arenas)
         nn_reset = (mask & (self.roles == _abi.ROLE_NN)).astype(np.uint8)
-        self.stepper.observe(self.obs, mask=torch.as_tensor(nn_reset, device=self.dev))
+        self._mask.copy_(torch.as_tensor(nn_reset))
+        self.stepper.observe(self.obs, mask=self._mask)
         return done
 
     def step(self, actions):

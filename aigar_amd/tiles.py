@@ -14,6 +14,12 @@ masses, which cells are final -- in one message per pass that every tile
 all-gathers (`include/aigar.h`, aigar_tile_*).  The spawn deficit is global:
 the messages carry each tile's pellet kills.
 
+The observation (bot.py:272-497) is divided: every bot is observed by ONE tile
+-- the one holding its last-frame history grids, else the tile of its view
+centre -- and a bot whose view centre changed tile (or that died) has its
+history handed off in the next tick's first message.  Every tile computes the
+same assignment (`aigar_tile_observers`).
+
 Transports:
   - `LocalTransport`: all tiles in this process (one GPU): device copies.
   - `TorchTransport`: one tile per rank; `torch.distributed.all_gather_into_tensor`
@@ -68,15 +74,33 @@ def merge_states(states):
     return d
 
 
-def tiled_tick(tiles, transport, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None):
+def tiled_tick(tiles, transport, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None, extra_passes=None):
     """One tick of the tiles in `tiles` (all of them, or this rank's one): begin,
     then exchange / apply passes until no owned cell is undone on any tile (the
     count comes with the messages, so every tile takes the same decision), then
-    the rest of the tick.  Returns the number of eat passes."""
+    the rest of the tick.  Returns the number of eat passes issued.
+
+    extra_passes=K (an int): no host round trip -- K further passes are issued
+    whatever happens and do nothing on the device once every cell is final; the
+    tick raises (device error bit) if cells are still undone after them.  With
+    the default halo every cell is decided by the first pass (K = 0)."""
     for t in tiles:
         t.tile_begin(policy, p_split, p_eject, seed)
     passes = 1
     transport.exchange(tiles)
+    if extra_passes is not None:
+        for t in tiles:
+            t.tile_apply(wait=False)
+        for _ in range(int(extra_passes)):
+            for t in tiles:
+                t.tile_resume()
+            transport.exchange(tiles)
+            for t in tiles:
+                t.tile_apply(wait=False)
+            passes += 1
+        for k, t in enumerate(tiles):
+            t.tile_end(None if obs is None else obs[k])
+        return passes
     undone = [t.tile_apply() for t in tiles]
     while undone[0] > 0:
         if len(set(undone)) != 1:
@@ -130,10 +154,10 @@ class TiledArena:
         for t in self.tiles:
             t.set_commands(cmd)
 
-    def tick(self, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None):
+    def tick(self, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None, extra_passes=None):
         """One Field.update() of the tiled arena; obs: per-tile device tensors
-        (observations of the bots each tile holds)."""
-        self.passes.append(tiled_tick(self.tiles, self.transport, policy, p_split, p_eject, seed, obs))
+        (each tile writes the rows of the bots it observes)."""
+        self.passes.append(tiled_tick(self.tiles, self.transport, policy, p_split, p_eject, seed, obs, extra_passes))
 
     def step(self, n=1, **kw):
         for _ in range(n):
@@ -150,26 +174,33 @@ class TiledArena:
             self._geo = [t.tile_info() for t in self.tiles]
         return self._geo
 
-    def _owner(self, x, y, cols):
-        bx = np.clip((np.asarray(x) / 20).astype(np.int64), 0, cols - 1)
-        by = np.clip((np.asarray(y) / 20).astype(np.int64), 0, cols - 1)
+    def owner(self, x, y):
+        """Tile owning the centre bucket of each (x, y); -1 where x or y is NaN
+        (a dead player's FOV)."""
+        x, y = np.asarray(x, np.float64), np.asarray(y, np.float64)
+        ok = np.isfinite(x) & np.isfinite(y)
+        cols = max(g["own"][1] for g in self._geometry())
+        bx = np.clip(np.where(ok, x, 0.0) // 20, 0, cols - 1).astype(np.int64)
+        by = np.clip(np.where(ok, y, 0.0) // 20, 0, cols - 1).astype(np.int64)
         own = np.full(bx.shape, -1, np.int64)
         for k, g in enumerate(self._geometry()):
             x0, x1, y0, y1 = g["own"]
-            own[(bx >= x0) & (bx < x1) & (by >= y0) & (by < y1)] = k
+            own[ok & (bx >= x0) & (bx < x1) & (by >= y0) & (by < y1)] = k
         return own
 
     def observe(self):
-        """Every bot's observation, each from the tile that owns its view's centre
-        (the FOV cache is replicated; tiles that also hold a bot compute the same row)."""
+        """Every bot's observation: each tile computes the rows of the bots it
+        observes (aigar_tile_observers: the same assignment on every tile); dead
+        bots get NaN rows."""
         rows = [t.observe() for t in self.tiles]
-        st = self.tiles[0].player_stats()
-        cols = max(g["own"][1] for g in self._geometry())
-        own = self._owner(st[:, 2], st[:, 3], cols)
+        by = self.tiles[0].tile_observers()
+        for t in self.tiles[1:]:
+            if not np.array_equal(t.tile_observers(), by):
+                raise RuntimeError("tiles disagree on the observation owners")
+        self.last_observers = by
         out = np.full((self.NP, self.obs_len), np.nan)
-        alive = st[:, 0] > 0
         for k in range(len(self.tiles)):
-            sel = alive & (own == k)
+            sel = by == k
             out[sel] = rows[k][sel]
         return out
 

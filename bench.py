@@ -7,12 +7,14 @@ env-steps = bots x steps.  Default workload = BASELINE.json configs[2] (C3):
 4096 bots, 100k pellets, 1152 viruses, split + eject on, field 4800, on one
 MI355X, started from the matured tick-50 world of data/c3_t50.npz (the
 survey's warm distribution: mean cell mass 17.4, max ~54; tools/mature.py).
-For N > 1 (launched by torch.distributed.run, one rank per GPU) `value` is
-every rank stepping its own C3 arena (independent replicas, weak scaling, no
-collective in the data path); the timed region is bracketed by barrier +
-synchronize and the max over ranks is taken.  Beside it, the "c4" object
-times ONE C3 arena tiled over the N ranks (BASELINE configs[3]: RCCL
-all-gather of the tiles' eat-phase messages over xGMI, strong scaling).
+For N > 1 (launched by torch.distributed.run, one rank per GPU) `value` is the
+metric's own world: ONE C3 arena (4096 bots x 100k pellets) tiled 2-D over the
+N ranks (BASELINE configs[3], C4: each rank one tile, the tiles' eat-phase
+messages and observation-history hand-offs all-gathered over RCCL / xGMI, each
+bot observed by one tile; strong scaling, no host round trip per tick).  The
+timed region is bracketed by barrier + synchronize and the max over ranks is
+taken.  Beside it, "replicas" times every rank stepping its own C3 arena
+(independent replicas, weak scaling, no collective in the data path).
 
 The timed steps are issued with aigar_run: each step (policy + tick +
 observation) is one hipGraph replay.  The per-phase breakdown and the roofline
@@ -278,40 +280,77 @@ def tick_bytes(st, alive, field, n_eaten):
 
 def c4_leg(args, name, rank, world, local, seed, dist, backend):
     """BASELINE configs[3]: ONE C3 arena tiled over the N ranks (aigar_amd/tiles.py),
-    each rank one tile; the eat-phase messages all-gathered over RCCL (xGMI).
-    Strong scaling: the same 4096 bots whatever N.  Returns the side object."""
+    each rank one tile; the eat-phase messages (and the observation-history
+    hand-offs) all-gathered over RCCL (xGMI).  Strong scaling: the same 4096 bots
+    whatever N.  One step = the random policy + Field.update + the observation of
+    every bot (each by one tile).  The passes are device-decided (no host round
+    trip): first with no extra pass; if a tick needed one (device error bit), the
+    world is reloaded and timed again with one extra pass per tick."""
     import torch
     from aigar_amd import _lib, tiles
     tx, ty = tiles.tile_grid(world)
     cfg = tiles.tile_config(make_cfg(name, device=local, arenas=1), tx, ty, rank)
     stp = _lib.Stepper(cfg)
     tr = tiles.TorchTransport.for_stepper(stp, staged=(backend != "nccl"))
-    start = start_world(stp, name, seed, 1)
     bots, field, pellets, virus, ps, pe, ch, ex, _ = WORKLOADS[name]
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
-    steps, warm = max(10, min(args.steps, 100)), 5
-    tick = lambda: tiles.tiled_tick([stp], tr, "random", ps, pe, args.seed, [obs])
-    for _ in range(warm):
+    steps, warm = args.steps, args.warmup
+    dev = "cuda" if backend == "nccl" else None
+    for extra in (0, 1):
+        start = start_world(stp, name, seed, 1)  # every tile loads the same world and keeps its held pellets
+        tick = lambda: tiles.tiled_tick([stp], tr, "random", ps, pe, args.seed, [obs], extra_passes=extra)
+        try:
+            for _ in range(warm):
+                tick()
+            torch.cuda.synchronize()
+            stp.sync()
+            replicas.barrier(dist)
+            torch.cuda.synchronize()
+            tr.reset_timing()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                tick()
+            torch.cuda.synchronize()
+            replicas.barrier(dist)
+            el = time.perf_counter() - t0
+            stp.sync()  # raises on a device error (every tile raises alike: the undone count is global)
+            break
+        except RuntimeError as e:
+            if extra == 1 or "device error bits" not in str(e):
+                raise
+    el = replicas.max_over_ranks(dist, el, device=dev)
+    ex_ms = tr.avg_exchange_ms()
+    # per-tile breakdown: the next steps as separate calls, HIP events on the tile's stream
+    nb = min(steps, 30)
+    stp.profile(True)
+    tr.reset_timing()
+    for _ in range(nb):
         tick()
     torch.cuda.synchronize()
-    replicas.barrier(dist)
-    tr.reset_timing()
-    passes = 0
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        passes += tick()
-    torch.cuda.synchronize()
-    replicas.barrier(dist)
-    el = replicas.max_over_ranks(dist, time.perf_counter() - t0, device="cuda" if backend == "nccl" else None)
-    ex_ms = tr.avg_exchange_ms()
+    br = {k: stp.kernel_time(k) for k in ("tile_begin", "tile_apply", "tile_resume", "tile_end", "observe")}
+    stp.profile(False)
+    ex_ms_b = tr.avg_exchange_ms()
     stp.sync()
+    observed = int(np.sum(stp.tile_observers() == rank))
     info = stp.tile_info()
     stp.close()
-    return {"workload": "C4: one C3 arena (%d bots) tiled %dx%d over %d GPUs, start %s" % (bots, tx, ty, world, start),
+    per_tile = {"tile": rank, "bots_observed": observed,
+                "ms_per_step": {k: v[0] / nb for k, v in br.items() if v[1]},
+                "exchange_ms_per_pass": ex_ms_b,
+                "note": "tile_begin = policy + updateViruses .. playerVirusOverlap + the first eat pass and the "
+                        "hand-off plan; tile_end = playerPlayerOverlap .. spawnStuff; observe = this tile's bots"}
+    tiles_all = [per_tile]
+    if dist is not None:
+        tiles_all = [None] * world
+        dist.all_gather_object(tiles_all, per_tile)
+    return {"workload": "C4: one C3 arena (%d bots, %d pellets) tiled %dx%d over %d GPUs, start %s" % (
+                bots, int(pellets), tx, ty, world, start),
             "value": bots * steps / el, "unit": "env-steps/s", "scaling": "strong", "steps": steps,
-            "ms_per_step": el / steps * 1e3, "eat_passes_per_tick": passes / steps,
-            "exchange": {"collective": "all_gather_into_tensor (%s)" % backend, "bytes_per_rank": info["msg_bytes"],
-                         "avg_ms": ex_ms}}
+            "ms_per_step": el / steps * 1e3, "eat_passes_per_tick": 1 + extra, "extra_passes": extra,
+            "exchange": {"collective": "all_gather_into_tensor (%s)" % backend,
+                         "bytes_per_rank_first_pass": (1 + info["tcap"]) * 32 + info.get("handoff_bytes", 0),
+                         "avg_ms": ex_ms},
+            "per_tile": tiles_all}
 
 
 def main():
@@ -327,7 +366,8 @@ def main():
                          "the GPU (reported under 'batched', never as 'value'); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pixels", action="store_true", help="skip the pixel-observation side measurement")
-    ap.add_argument("--no-c4", action="store_true", help="skip the tiled single-arena (C4) side measurement")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N > 1: report the replicas as value instead of the tiled single arena (C4)")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the warm-up and the timed graph replays (for rocprofv3: one call per step)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -468,8 +508,16 @@ def main():
             out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
         if args.policy == "random" and name == "c3":  # the same start with the reference's Greedy bots
             out["greedy"] = greedy_side(name, args.seed, local)
-    if not args.profile_run and not args.no_c4 and world > 1 and name == "c3":
-        out["c4"] = c4_leg(args, name, rank, world, local, args.seed, dist, backend)
+    if not args.no_c4 and world > 1 and name == "c3":
+        # the metric's world at N GPUs: one 4096-bot arena tiled over them (value);
+        # the replicas measured above become the side line
+        c4 = c4_leg(args, name, rank, world, local, args.seed, dist, backend)
+        out["replicas"] = {"value": out["value"], "ms_per_step": out["ms_per_step"], "scaling": "weak",
+                           "workload": "%d independent C3 arenas, one per GPU" % world}
+        out["value"], out["ms_per_step"], out["scaling"] = c4["value"], c4["ms_per_step"], "strong"
+        out["config"]["workload"] = c4["workload"]
+        out["config"]["parallelism"] = "tiles%dx%d" % replicas_tiles(world)
+        out["c4"] = c4
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_run:  # (N = 1 only)
         out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget, policy=args.policy)
         if name == "c3":
@@ -480,6 +528,11 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def replicas_tiles(world):
+    from aigar_amd import tiles
+    return tiles.tile_grid(world)
 
 
 def greedy_side(name, seed, device, steps=30, warmup=5):

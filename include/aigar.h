@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AIGAR_ABI_VERSION 3
+#define AIGAR_ABI_VERSION 4
 
 /* random number stream of the world (spawns, explosion angles) */
 #define AIGAR_RNG_PHILOX 0   /* Philox4x64-10 keyed by (seed, site, index): device + oracle */
@@ -307,18 +307,32 @@ int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int cap, int *n);
  *                           undone on all tiles (same value on every tile)
  *   while (u > 0) { aigar_tile_resume(h); <all-gather>; aigar_tile_apply(h, &u); }
  *   aigar_tile_end(h, obs, dtype)  playerPlayerOverlap .. spawnStuff; then, if obs
- *                           (DEVICE) is given, every bot's observation: exact for
- *                           the bots whose view lies in the held pellets; the
- *                           others have NaN in the pellet channel (their tile --
- *                           the one owning the view's centre -- has it)
+ *                           (DEVICE) is given, the observations of the bots THIS
+ *                           tile observes (bot.py:272-497; the other rows are left
+ *                           as they are, dead bots get NaN on every tile)
+ * Without host round trips: aigar_tile_apply(h, NULL) returns at once, and a
+ * fixed number K of further (aigar_tile_resume, all-gather, aigar_tile_apply)
+ * rounds follow; a resume pass does nothing on the device once no owned cell is
+ * undone, and aigar_tile_end raises error bit 4096 if cells are still undone
+ * after the K passes (K = 0 with the default halo in practice: one pass).
+ * Observation: each bot is observed by ONE tile -- the one holding its
+ * last-frame history grids (bot.py:480-495), else the tile of its view centre.
+ * A bot whose view centre moved to another tile, or that died, has its history
+ * handed off in the next tick's first message and every tile takes it, so the
+ * next observation is made by the view centre's tile; a view the observing
+ * tile does not hold sets error bit 2048.  aigar_tile_observers: per player,
+ * the observing tile of the last observation (-1: dead), identical on every tile.
  * The spawn deficit is global: each tile's message carries its pellet kills.
- * aigar_tile_info: info[12] = ntiles, tile_id, owned bucket range x0, x1, y0, y1
- * (half-open), held range x0, x1, y0, y1, records per message, bitmap words;
+ * aigar_tile_info: info[14] = ntiles, tile_id, owned bucket range x0, x1, y0, y1
+ * (half-open), held range x0, x1, y0, y1, records per message, bitmap words,
+ * hand-off slots per message, records per hand-off slot;
  * the device outbox / inbox and the bytes of one message (the inbox holds
  * ntiles messages, tile k at k * bytes).  A message is 32-byte records:
- * [header: kind 0, record count, undone owned cells, pellet kills as double]
- * [records: kind 1 pellet kill (seq, x, y) | 2 blob kill (slot, seq) | 3 cell
- * outcome (pool index, seq, mass, radius)] [bitmap: owned cells now final].
+ * [header: kind 0, record count, undone owned cells, pellet kills as double,
+ * hand-off slots as double] [records: kind 1 pellet kill (seq, x, y) | 2 blob
+ * kill (slot, seq) | 3 cell outcome (pool index, seq, mass, radius)] and, in
+ * the tick's first pass, [hand-off slots: kind 4 (player, lastFovSize) + the
+ * bot's history grids as doubles], in later passes [bitmap: owned cells now final].
  * aigar_tile_set_buffers: use caller-owned device buffers instead (e.g. torch
  * tensors that RCCL fills); aigar_tile_exchange_local: the in-process transport
  * -- copies every handle's outbox into every handle's inbox (same process).
@@ -335,6 +349,7 @@ int aigar_tile_apply(aigar_handle *h, int *undone);
 int aigar_tile_resume(aigar_handle *h);
 int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype);
 int aigar_tile_exchange_local(aigar_handle **hs, int n);
+int aigar_tile_observers(aigar_handle *h, int32_t *out);
 
 /* The event log as raw rows (key_hi = tick << 8 | phase, key_lo = order within the
  * phase, code, a, b), unsorted: tiled arenas merge their tiles' logs by key. */

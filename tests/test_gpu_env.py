@@ -212,16 +212,21 @@ def test_mixed_population_matches_oracle():
 
 
 def test_reset_limit_and_desynchronised_arenas():
-    """RESET_LIMIT episodes (aigar.py:876-887): with 4 arenas and staggered timers
-    (aigar.py:833-837) the arenas restart in different decisions, each once per
-    RESET_LIMIT ticks, with a fresh world and fresh bots."""
+    """RESET_LIMIT episodes (aigar.py:876-887) with desynchronised arenas
+    (aigar.py:833-837): before the first decision arena a has played a *
+    int(R / N) ticks of its own world; an episode ends after the decision in which
+    the arena's tick count passes R - FRAME_SKIP_RATE + 2, with a fresh world and
+    fresh bots."""
     import torch
     from aigar_amd.env import AgarVecEnv
     p = _params(FRAME_SKIP_RATE=1, RESET_LIMIT=16)
     env = AgarVecEnv(32, p, n_arenas=4, field_size=250, max_viruses=6, seed=1)
     env.reset(2)
+    assert [env.stepper.get_state(a)["tick"] for a in range(4)] == [0, 4, 8, 12]
+    w = [env.stepper.get_state(a) for a in range(4)]
+    assert len({int(x["n_pellets"]) for x in w} | {int(x["seq_next"]) for x in w}) > 1  # different game stages
     ends = []
-    for t in range(16):
+    for t in range(20):
         act = torch.rand((128, 4), dtype=torch.float64, device="cuda")
         obs, rew, alive, done = env.step(act)
         arenas = sorted(set((done.nonzero().flatten() // 32).tolist()))
@@ -230,9 +235,12 @@ def test_reset_limit_and_desynchronised_arenas():
             st = env.stepper.get_state(a)
             assert st["tick"] == 0 and st["n_cells"] == 32  # a fresh world, every player respawned
             assert not torch.isnan(obs[a * 32:(a + 1) * 32, 0]).any()  # the new episode's first states
-    # 2 ticks per decision, 16 ticks per episode: each arena ends every 8 decisions, arena a first
-    # at decision 8 - 2a (timers start at a * 16 / 4 ticks)
+    # 2 ticks per decision; arena a starts at 4a ticks and ends when its count passes 16 - 1 + 2 = 17
     for a in range(4):
         hits = [t for t, e in enumerate(ends) if a in e]
-        assert hits == [7 - 2 * a, 15 - 2 * a], (a, hits)
+        first = (17 - 4 * a) // 2  # the decision index t with 4a + 2 (t + 1) > 17 first
+        assert hits == [h for h in (first, first + 9, first + 18) if h < 20], (a, hits)
+    # an explicit reset restarts the timers and the desynchronisation
+    env.reset(3)
+    assert list(env.age) == [0, 4, 8, 12]
     env.close()

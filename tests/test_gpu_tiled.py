@@ -28,7 +28,7 @@ C3_CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi
 
 
 def run(cfg, tx, ty, ticks, seed, cmd_fn, halo=0, obs_every=0, check_every=10, ftol=parity.FTOL, flags=0,
-        start=None):
+        start=None, extra_passes=None):
     ta, o = TiledArena(cfg, tx, ty, halo=halo, flags=flags), Oracle(cfg)
     if start is None:
         ta.reset(seed)
@@ -39,11 +39,12 @@ def run(cfg, tx, ty, ticks, seed, cmd_fn, halo=0, obs_every=0, check_every=10, f
     dif = parity.diff_states(ta.get_state(), o.get_state())
     assert not dif, dif
     kinds, nev = set(), 0
+    prev_by, moved, per_tile = None, 0, np.zeros(tx * ty, np.int64)
     for t in range(ticks):
         cmd = cmd_fn(t, o)
         ta.set_commands(cmd)
         o.set_commands(cmd)
-        ta.tick()
+        ta.tick(extra_passes=extra_passes)
         o.step(1)
         eg, eo = ta.events(), o.events()
         if not np.array_equal(eg, eo):
@@ -59,7 +60,14 @@ def run(cfg, tx, ty, ticks, seed, cmd_fn, halo=0, obs_every=0, check_every=10, f
         if obs_every and (t + 1) % obs_every == 0:
             og, oo = ta.observe(), o.observe()
             assert parity.obs_close(og, oo), "tick %d: observations differ" % t
-    stats = {"kinds": kinds, "events": nev, "passes": list(ta.passes)}
+            by = ta.last_observers
+            alive = o.player_stats()[:, 0] > 0
+            assert np.array_equal(by >= 0, alive), "tick %d: observed set != alive set" % t
+            per_tile += np.bincount(by[by >= 0], minlength=tx * ty)
+            if prev_by is not None:  # a bot observed by another tile than last time: its history was handed off
+                moved += int(np.sum((by >= 0) & (prev_by >= 0) & (by != prev_by)))
+            prev_by = by
+    stats = {"kinds": kinds, "events": nev, "passes": list(ta.passes), "moved": moved, "per_tile": per_tile}
     ta.close()
     o.close()
     return stats
@@ -82,17 +90,67 @@ def c3_config(**kw):
                        **kw)
 
 
-@pytest.mark.parametrize("tx,ty", [(2, 1), (2, 2)])
+@pytest.mark.parametrize("tx,ty", [(2, 1), (2, 2), (4, 2)])
 def test_c3_tiled_matches_untiled_oracle(tx, ty):
     """C3 (4096 bots, 100k pellets, 1152 viruses, split p 2.5e-3 / eject p 1e-2)
     from the matured tick-600 world (cells past 125, multi-cell players), 200 ticks:
     splits, ejections, blob eating, explosions, merges, cell-eats-cell across the
-    tile borders."""
+    tile borders.  (4, 2) is C4's own layout (tiles 1200 x 2400).
+    Every 25 ticks every bot's observation, each from the one tile that observes
+    it (its history holder or its view centre's tile): bots that crossed a border
+    in between arrive with their history handed off."""
     st = run(c3_config(), tx, ty, 200, 31, synthetic(4096, 4800, 2.5e-3, 1e-2, 31), obs_every=25, check_every=25,
              start=parity.load_snapshot("c3_t600"))
     assert st["events"] > 10000
     assert {_abi.EV_CELL_EAT_PELLET, _abi.EV_CELL_EAT_BLOB, _abi.EV_RESPAWN, _abi.EV_MERGE, _abi.EV_EXPLODE,
             _abi.EV_CELL_EAT_CELL, _abi.EV_CELL_EAT_VIRUS} <= st["kinds"], st["kinds"]
+    assert st["moved"] > 0, "no bot changed its observing tile"
+    # the observation is divided: every tile observes its share (~1/N of the bots)
+    share = st["per_tile"] / st["per_tile"].sum()
+    assert share.max() < 2.0 / (tx * ty), share
+
+
+def test_c3_4x2_history_handoff_every_tick():
+    """C4 layout, observation EVERY tick for 60 ticks (the last-frame channels
+    compare each bot's history): a bot whose view centre crosses into another
+    tile, or that dies and respawns anywhere, is observed next by a tile that got
+    its history in that tick's first message; no host round trip per pass
+    (extra_passes=0: the device-bounded path the benchmark runs)."""
+    st = run(c3_config(), 4, 2, 60, 33, synthetic(4096, 4800, 2.5e-3, 1e-2, 33), obs_every=1, check_every=20,
+             start=parity.load_snapshot("c3_t600"), extra_passes=0)
+    assert st["moved"] >= 10, st["moved"]
+    assert set(st["passes"]) == {1}
+
+
+def test_device_bounded_passes_raise_when_cells_stay_undone():
+    """extra_passes=0 with a small halo deciding only owned cells: a tick that needs
+    a second exchange pass must fail loudly (device error bit), not go on."""
+    with pytest.raises(RuntimeError, match="device error bits"):
+        run(c3_config(), 2, 2, 60, 32, synthetic(4096, 4800, 2.5e-3, 1e-2, 32), halo=140, check_every=10,
+            flags=_abi.TILE_OWNED_ONLY, start=parity.load_snapshot("c3_t600"), extra_passes=0)
+
+
+def test_view_beyond_the_held_pellets_is_refused():
+    """A view the observing tile does not hold (here: a cell at the mass cap on a
+    tile border, view ~287 wide, with the smallest halo, 7 buckets) must raise
+    instead of returning a row with pellets missing."""
+    cfg = make_config(bots=256, channels=C3_CH, extras=0x1F)
+    o = Oracle(cfg)
+    o.reset(3)
+    snap = o.get_state()
+    o.close()
+    owner = np.asarray(snap["cells_i"])[:, 0]
+    k = int(np.nonzero(owner == 0)[0][0])
+    cf = np.array(snap["cells_f"], copy=True)
+    cf[k, 0] = cf[k, 1] = 600.5
+    cf[k, 2] = 22500.0
+    cf[k, 3] = np.sqrt(22500.0 / np.pi)
+    snap["cells_f"] = cf
+    ta = TiledArena(cfg, 2, 2, halo=140)
+    ta.load_state(snap)
+    with pytest.raises(RuntimeError, match="device error bits"):
+        ta.observe()
+    ta.close()
 
 
 def test_c3_small_halo_forces_cross_tile_passes():
