@@ -14,6 +14,7 @@ RNG_MT19937 = 1
 
 OBS_PELLET, OBS_SELF, OBS_WALL, OBS_ENEMY, OBS_ALL, OBS_VIRUS = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
 OBS_SELF_SLF, OBS_SELF_LF, OBS_ENEMY_SLF, OBS_ENEMY_LF = 0x40, 0x80, 0x100, 0x200
+OBS_SIMPLE = 0x400  # GRID_VIEW_ENABLED = False: getSimpleStateRepresentation, 12 values
 EX_LAST_FOV, EX_FOV, EX_MASS, EX_LAST_ACT, EX_2LAST_ACT = 0x1, 0x2, 0x4, 0x8, 0x10
 
 EV_MERGE, EV_VIRUS_EAT_BLOB, EV_VIRUS_SPLIT, EV_CELL_EAT_VIRUS, EV_EXPLODE = 1, 2, 3, 4, 5
@@ -153,6 +154,8 @@ def struct_to_dict(st, arrays):
 
 
 def obs_len(grid_squares, channels, extras):
+    if channels & OBS_SIMPLE:
+        return 12
     g = grid_squares or 11
     n = bin(channels & 0x3FF).count("1")
     e = (1 if extras & EX_LAST_FOV else 0) + (1 if extras & EX_FOV else 0) + (1 if extras & EX_MASS else 0) \

@@ -218,6 +218,7 @@ struct Dev {
   uint32_t *ob_mask;
   uint8_t *ob_own;
   int *ob_perm;
+  uint64_t *ob_wmask;  // [OBcap][4] x / y index masks of the wide grid (grid_squares > 16)
 };
 
 constexpr int FCAP = 32;  // stored candidate foods per cell (overflow -> serial)

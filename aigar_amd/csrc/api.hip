@@ -122,6 +122,7 @@ static T *dalloc(aigar_handle *h, size_t n) {
 
 static int obs_len_of(const aigar_config &c) {
   int G = c.grid_squares ? c.grid_squares : 11, n = 0, e = 0;
+  if (c.obs_channels & AIGAR_OBS_SIMPLE) return 12;  // getSimpleStateRepresentation (bot.py:511-547)
   for (int b = 0; b < 10; b++) n += (c.obs_channels >> b) & 1;
   e += (c.obs_extras & AIGAR_EX_LAST_FOV) ? 1 : 0;
   e += (c.obs_extras & AIGAR_EX_FOV) ? 1 : 0;
@@ -187,7 +188,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   if (cfg->rng_mode != AIGAR_RNG_PHILOX)
     return fail("aigar_create: the device stepper runs AIGAR_RNG_PHILOX only (MT19937 lives in the CPU oracle)");
   int G = cfg->grid_squares ? cfg->grid_squares : 11;
-  if (G < 1 || G > 16) return fail("aigar_create: grid_squares must be in [1, 16]");
+  if (G < 1 || G > 127) return fail("aigar_create: grid_squares must be in [1, 127]");
   if (cfg->obs_channels & AIGAR_OBS_ALL &&
       cfg->obs_channels & (AIGAR_OBS_SELF_LF | AIGAR_OBS_SELF_SLF | AIGAR_OBS_ENEMY_LF | AIGAR_OBS_ENEMY_SLF))
     return fail("aigar_create: ALL_PLAYER_GRID with last-frame grids is undefined in the reference");
@@ -347,6 +348,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   }
   AL(p_fx, double, NP); AL(p_fy, double, NP); AL(p_fs, double, NP); AL(p_mass, double, NP); AL(ob_seq, int64_t, d.OBcap); AL(ob_m, double, d.OBcap); AL(ob_r, double, d.OBcap);
   AL(ob_mask, uint32_t, d.OBcap); AL(ob_own, uint8_t, d.OBcap); AL(ob_perm, int, d.OBcap);
+  d.ob_wmask = nullptr;
+  if (G > 16) AL(ob_wmask, uint64_t, 4 * (size_t)d.OBcap);
 #undef AL
   h->scr_k = dalloc<int64_t>(h, A * d.Wcap);
   h->scr_v = dalloc<int>(h, A * d.Wcap);

@@ -152,8 +152,9 @@ __device__ __forceinline__ int span_rows(const Span &s) { return (s.bx1 >= s.bx0
 template <class P, class F>
 // rmax_c / rmax_v: the arena's largest cell / virus radius (ArenaCtl), read by
 // the caller together with its first loads
-__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, double fx, double fy, double fs,
-                                              double rmax_c, double rmax_v, bool want_p, bool want_v, P pre, F f) {
+__device__ __forceinline__ void wave_fov_walk_k(const Dev &d, int a, Rect Q, double fx, double fy, double fs,
+                                                double rmax_c, double rmax_v, bool want_p, bool want_c, bool want_v,
+                                                P pre, F f) {
   const int lane = threadIdx.x & 63;
   const bool qok = Q.x1 >= Q.x0 && Q.y1 >= Q.y0;
   const double rc = fmax(rmax_c, radius_of(kStartMass)), rv = fmax(rmax_v, radius_of(kVirusBase));
@@ -169,7 +170,7 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
   const Span sc = grid_span(Q, Ec, d.cols, d.cshift_c), sv = grid_span(Q, Ev, d.cols, d.cshift);
 #endif
   const int np_rows = (qok && want_p) ? span_rows(sp) : 0;
-  const int nc_rows = qok ? span_rows(sc) : 0;
+  const int nc_rows = (qok && want_c) ? span_rows(sc) : 0;
   const int nv_rows = (qok && want_v) ? span_rows(sv) : 0;
   const int nrows = np_rows + nc_rows + nv_rows;
   const size_t H1 = (size_t)a * (d.H + 1);
@@ -213,6 +214,13 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
       f(valid, kd, g);
     }
   }
+}
+
+// (every kind's rows: pellets and viruses as asked, player cells always)
+template <class P, class F>
+__device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, double fx, double fy, double fs,
+                                              double rmax_c, double rmax_v, bool want_p, bool want_v, P pre, F f) {
+  wave_fov_walk_k(d, a, Q, fx, fy, fs, rmax_c, rmax_v, want_p, true, want_v, pre, f);
 }
 
 #ifdef AIGAR_OBS_WPE
@@ -980,9 +988,23 @@ void launch_player_fov(const Dev &d, hipStream_t s) {
 // blends are order-dependent).
 #include "pixels.inc"
 
+#include "obs_wide.inc"
+
+// the state representation the configuration asks for (bot.py:272-299): the
+// default grid (<= 16 squares per side), the wide grid (CNN grid view), or the
+// simple representation (GRID_VIEW_ENABLED = False)
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch, const uint8_t *mask) {
-  if (dtype == 0) hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
-  else hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+  if (d.obs_ch & AIGAR_OBS_SIMPLE) {
+    if (dtype == 0) hipLaunchKernelGGL(k_observe_simple<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, mask);
+    else hipLaunchKernelGGL(k_observe_simple<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, mask);
+  } else if (d.G > 16) {
+    if (dtype == 0) hipLaunchKernelGGL(k_observe_wide<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
+    else hipLaunchKernelGGL(k_observe_wide<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+  } else if (dtype == 0) {
+    hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
+  } else {
+    hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+  }
 }
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt) {
   hipLaunchKernelGGL(k_policy_random, dim3((d.NP + 255) / 256), dim3(256), 0, s, d, ps, pe, salt);

@@ -62,13 +62,11 @@ def obs_masks(parameters):
     """(channels, extras, grid squares) of a reference networkParameters-like object."""
     if parameters is None:  # networkParameters.py defaults for one NN bot
         return _abi.OBS_PELLET, _abi.EX_FOV | _abi.EX_MASS, 11
+    if not getattr(parameters, "GRID_VIEW_ENABLED", True):  # bot.py:296-297: getSimpleStateRepresentation
+        return _abi.OBS_SIMPLE, 0, 11
     if getattr(parameters, "SIZE_GRID", False):
         raise NotImplementedError("SIZE_GRID observations are not implemented")
-    if getattr(parameters, "CNN_REPR", False) and not getattr(parameters, "CNN_P_REPR", False):
-        # bot.py:284: a CNN over getGridStateRepresentation() with CNN_INPUT_DIM_* (42 / 84) squares per side
-        raise NotImplementedError("CNN over the grid view (CNN_REPR without CNN_P_REPR) needs more than 16 grid "
-                                  "squares per side, beyond the device observation; the pixel CNN path "
-                                  "(CNN_P_REPR) is supported")
+    cnn_grid = getattr(parameters, "CNN_REPR", False) and not getattr(parameters, "CNN_P_REPR", False)
     ch = 0
     for name, bit in _CHANNEL_FLAGS:
         if getattr(parameters, name, False):
@@ -76,10 +74,18 @@ def obs_masks(parameters):
     if ch & _abi.OBS_ALL:  # networkParameters.py: ALL_PLAYER_GRID disables SELF/ENEMY
         ch &= ~(_abi.OBS_SELF | _abi.OBS_ENEMY)
     ex = 0
-    if getattr(parameters, "EXTRA_INPUT", True):
+    if getattr(parameters, "EXTRA_INPUT", True) and not cnn_grid:
         for name, bit in _EXTRA_FLAGS:
             if getattr(parameters, name, False):
                 ex |= bit
+    if cnn_grid:  # bot.py:103-111, 284: the grid view alone, CNN_INPUT_DIM_* squares per side (42 / 84)
+        if getattr(parameters, "CNN_USE_L1", False):
+            g = parameters.CNN_INPUT_DIM_1
+        elif getattr(parameters, "CNN_USE_L2", False):
+            g = parameters.CNN_INPUT_DIM_2
+        else:
+            g = parameters.CNN_INPUT_DIM_3
+        return ch, 0, int(g)
     return ch, ex, int(getattr(parameters, "GRID_SQUARES_PER_FOV", 11))
 
 
@@ -328,6 +334,7 @@ class Field:
         c.virus_enabled = int(self.virusEnabled)
         c.max_pellets, c.max_viruses = float(self.max_pellets), float(self.max_viruses)
         c.grid_squares, c.obs_channels, c.obs_extras = g, ch, ex
+        self.grid_squares = g
         c.rng_mode, c.device = _abi.RNG_PHILOX, self.device
         c.flags = _abi.FLAG_EVENTS if self.record_events else 0
         return c
@@ -710,11 +717,13 @@ class Bot:
     def getStateRepresentation(self):  # bot.py:272-299
         if not self.player.getIsAlive():
             return None
-        if not self._param("GRID_VIEW_ENABLED", True):
-            raise NotImplementedError("getSimpleStateRepresentation (GRID_VIEW_ENABLED = False) is not implemented")
+        if not self._param("GRID_VIEW_ENABLED", True):  # getSimpleStateRepresentation (bot.py:511-547): a list
+            return [float(v) for v in self.field._state_row(self.player.index)]
         if self._param("CNN_REPR", False):
-            if not self._param("CNN_P_REPR", False):
-                raise NotImplementedError("CNN over the grid view is not implemented (see obs_masks)")
+            if not self._param("CNN_P_REPR", False):  # bot.py:284: the grid view [NUM_OF_GRIDS, G, G]
+                row = self.field._state_row(self.player.index)
+                g = self.field.grid_squares
+                return row.reshape(-1, g, g).copy()
             rgb_values = self.rgbGenerator.get_cnn_inputRGB(self.player)
             stateRepr = (rgb_values - 255) / 100  # bot.py:279
             if self._param("CNN_LAST_GRID", False):

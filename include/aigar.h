@@ -47,6 +47,10 @@ extern "C" {
 #define AIGAR_OBS_SELF_LF    0x080u  /* SELF_GRID_LF   (last frame)       */
 #define AIGAR_OBS_ENEMY_SLF  0x100u  /* ENEMY_GRID_SLF                    */
 #define AIGAR_OBS_ENEMY_LF   0x200u  /* ENEMY_GRID_LF                     */
+/* GRID_VIEW_ENABLED = False (networkParameters.py:119): getSimpleStateRepresentation
+ * (bot.py:511-547) instead of the grids -- 12 values per bot (first own cell,
+ * closest enemy cell, closest pellet, visible field edges); no grids, no extras */
+#define AIGAR_OBS_SIMPLE     0x400u
 /* extra inputs, in getAdditionalFeatures order (bot.py:302-323) */
 #define AIGAR_EX_LAST_FOV    0x01u
 #define AIGAR_EX_FOV         0x02u
@@ -80,7 +84,9 @@ typedef struct aigar_config {
   int32_t virus_enabled;   /* Field(virusEnabled) (field.py:30, VIRUS_SPAWN)          */
   double max_pellets;      /* < 0 -> size*size*0.015 (field.py:65, parameters.py:16)  */
   double max_viruses;      /* < 0 -> size*size*5e-5 (field.py:66, parameters.py:17)   */
-  int32_t grid_squares;    /* GRID_SQUARES_PER_FOV (networkParameters.py:97); 0 -> 11 */
+  int32_t grid_squares;    /* GRID_SQUARES_PER_FOV (networkParameters.py:97), or the CNN
+                            * grid view's CNN_INPUT_DIM_* (bot.py:103-111: 42 / 84);
+                            * 0 -> 11; at most 127                                     */
   uint32_t obs_channels;   /* AIGAR_OBS_* mask (networkParameters.py:76-96)           */
   uint32_t obs_extras;     /* AIGAR_EX_* mask (networkParameters.py:91-95)            */
   int32_t rng_mode;        /* AIGAR_RNG_*                                             */

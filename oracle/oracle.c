@@ -1045,22 +1045,83 @@ static void fh_insert_all(FHash *fh, double size, double gs, double left, double
     double cl = py_max(0, px - r), ct = py_max(0, py - r);
     double bl = cl - py_mod(cl, gs), bt = ct - py_mod(ct, gs);
     double lx = py_min(size - 1, px + r), ly = py_min(size - 1, py + r);
-    int seen[256], ns = 0;
+    /* the ids form a set (spatialHashTable.py:89): an object enters a bucket once
+     * (at 42 / 84 squares per side a cell covers thousands of them) */
+    int nb = fh->cols * fh->rows;
+    unsigned char *seen = (unsigned char *)calloc((size_t)nb, 1);
     for (double x = bl; x <= lx; x += gs)
       for (double y = bt; y <= ly; y += gs) {
         int id = (int)(long)(x / gs) + (int)(long)(y / gs) * fh->cols;
-        int dup = 0;
-        for (int q = 0; q < ns; q++)
-          if (seen[q] == id) dup = 1;
-        if (dup) continue;
-        if (ns < 256) seen[ns++] = id;
+        if (seen[id]) continue;
+        seen[id] = 1;
         cv_push(&fh->b[id], o);
       }
+    free(seen);
   }
+}
+
+/* Bot.getSimpleStateRepresentation (bot.py:511-547; GRID_VIEW_ENABLED = False):
+ * the first own cell, the closest enemy cell and the closest pellet relative to
+ * the integer view box, then the distances to the visible field edges -- 12
+ * values.  The enemy query uses the real fovSize, the pellet query the
+ * truncated one (bot.py:531 passes size = int(size)); "closest" is min() over
+ * the query's list (creation order), first one on ties. */
+static void rel_cell(const Cell *c, int64_t left, int64_t top, int64_t size, double *o, int with_r) {
+  if (!c) { /* getRelativeCellPos -> [0, 0] (+ [0]) */
+    o[0] = o[1] = 0;
+    if (with_r) o[2] = 0;
+    return;
+  }
+  o[0] = oracle_py_round5((c->x - (double)left) / (double)size);
+  o[1] = oracle_py_round5((c->y - (double)top) / (double)size);
+  if (with_r) o[2] = oracle_py_round5(c->radius <= (double)size ? c->radius / (double)size : 1.0);
+}
+static void simple_one(Arena *A, int p, double *out) {
+  Player *P = &A->pl[p];
+  if (!P->alive) {
+    for (int i = 0; i < 12; i++) out[i] = NAN;
+    return;
+  }
+  double fs = player_fov_size(P), fx, fy;
+  player_fov_pos(P, &fx, &fy);
+  const int64_t x = (int64_t)fx, y = (int64_t)fy;
+  const int64_t left = x - (int64_t)(fs / 2), top = y - (int64_t)(fs / 2), size = (int64_t)fs;
+  const Cell *first = P->cells.a[0];
+  rel_cell(first, left, top, size, out, 1);
+  CVec q = {0};
+  const Cell *best = NULL;
+  double bd = 0;
+  hash_query(&A->plh, fx, fy, fs / 2, &q); /* getEnemyPlayerCellsInFov (field.py:434-436) */
+  for (int i = 0; i < q.n; i++) {
+    const Cell *c = q.a[i];
+    if (c->player == p || !in_fov(c, fx, fy, fs)) continue;
+    const double dd = sqdist(c, first);
+    if (!best || dd < bd) { best = c; bd = dd; }
+  }
+  rel_cell(best, left, top, size, out + 3, 1);
+  best = NULL;
+  hash_query(&A->ph, fx, fy, (double)size / 2, &q); /* getPelletsInFov(midPoint, int size) */
+  for (int i = 0; i < q.n; i++) {
+    const Cell *c = q.a[i];
+    if (!in_fov(c, fx, fy, (double)size)) continue;
+    const double dd = sqdist(c, first);
+    if (!best || dd < bd) { best = c; bd = dd; }
+  }
+  rel_cell(best, left, top, size, out + 6, 0);
+  const double w = (double)A->size, sz = (double)size;
+  out[8] = left <= 0 ? (double)x / sz : 1.0;
+  out[9] = left + size >= A->size ? (w - (double)x) / sz : 1.0;
+  out[10] = top <= 0 ? (double)y / sz : 1.0;
+  out[11] = top + size >= A->size ? (w - (double)y) / sz : 1.0;
+  cv_free(&q);
 }
 
 static void observe_one(Oracle *O, Arena *A, int p, double *out) {
   const uint32_t ch = O->cfg.obs_channels, ex = O->cfg.obs_extras;
+  if (ch & AIGAR_OBS_SIMPLE) {
+    simple_one(A, p, out);
+    return;
+  }
   const int G = A->G, GG = G * G;
   Player *P = &A->pl[p];
   if (!P->alive) {
@@ -1416,6 +1477,7 @@ int oracle_pixels(void *h, int L, uint64_t seed, uint8_t *out) {
 
 static int obs_len(const aigar_config *c) {
   int G = c->grid_squares ? c->grid_squares : 11, n = 0, e = 0;
+  if (c->obs_channels & AIGAR_OBS_SIMPLE) return 12;
   for (int b = 0; b < 10; b++) n += (c->obs_channels >> b) & 1;
   e += (c->obs_extras & AIGAR_EX_LAST_FOV) ? 1 : 0;
   e += (c->obs_extras & AIGAR_EX_FOV) ? 1 : 0;

@@ -28,7 +28,8 @@ def golden_config(z, arenas=1):
     return make_config(n_arenas=arenas, bots=int(z["n_players"]), field_size=int(z["size"]),
                        virus=bool(z["virus_enabled"]), max_pellets=float(z["max_pellets"]),
                        max_viruses=float(z["max_viruses"]), channels=int(z["obs_channels"]),
-                       extras=int(z["obs_extras"]), rng_mode=_abi.RNG_PHILOX)
+                       extras=int(z["obs_extras"]), rng_mode=_abi.RNG_PHILOX,
+                       grid_squares=int(z["grid_squares"]) if "grid_squares" in z.files else 11)
 
 
 def load_golden(name):

@@ -56,7 +56,7 @@ def test_create_fails_loudly_without_device_or_with_bad_config():
     h = C.c_void_p()
     assert L.aigar_create(C.byref(cfg), C.byref(h)) < 0
     assert b"PHILOX" in L.aigar_last_error()
-    cfg.rng_mode, cfg.grid_squares = _abi.RNG_PHILOX, 40
+    cfg.rng_mode, cfg.grid_squares = _abi.RNG_PHILOX, 128  # (42 / 84: the CNN grid view; at most 127)
     assert L.aigar_create(C.byref(cfg), C.byref(h)) < 0
     assert b"grid_squares" in L.aigar_last_error()
 
@@ -67,3 +67,5 @@ def test_obs_len_formula():
           | _abi.OBS_ENEMY_LF)
     ex = _abi.EX_LAST_FOV | _abi.EX_FOV | _abi.EX_MASS | _abi.EX_LAST_ACT
     assert _abi.obs_len(11, ch, ex) == 854  # C3 (virus + split), SURVEY.md §8a25
+    assert _abi.obs_len(84, ch, 0) == 7 * 84 * 84  # CNN grid view (bot.py:284): the grids alone
+    assert _abi.obs_len(11, _abi.OBS_SIMPLE, ex) == 12  # getSimpleStateRepresentation (bot.py:511-547)

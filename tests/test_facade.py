@@ -94,6 +94,20 @@ def test_obs_masks_reproduce_state_repr_len(virus, split, eject, n):
     assert _abi.obs_len(g, ch, ex) == p.STATE_REPR_LEN
 
 
+def test_obs_masks_state_variants():
+    """GRID_VIEW_ENABLED = False -> getSimpleStateRepresentation (12 values);
+    CNN_REPR without CNN_P_REPR -> the grid view alone at CNN_INPUT_DIM_* squares."""
+    p = reference_like_parameters(True, True, False, 16)
+    p.GRID_VIEW_ENABLED = False
+    ch, ex, g = M.obs_masks(p)
+    assert ch == _abi.OBS_SIMPLE and _abi.obs_len(g, ch, ex) == 12
+    p.GRID_VIEW_ENABLED = True
+    p.CNN_REPR, p.CNN_P_REPR = True, False
+    p.CNN_USE_L1, p.CNN_USE_L2, p.CNN_INPUT_DIM_1, p.CNN_INPUT_DIM_2 = False, True, 42, 84
+    ch, ex, g = M.obs_masks(p)
+    assert g == 84 and ex == 0 and _abi.obs_len(g, ch, ex) == p.NUM_OF_GRIDS * 84 * 84
+
+
 def test_unsupported_paths_fail_loudly():
     p = reference_like_parameters(False, False, False, 2)
     p.SIZE_GRID = True

@@ -136,3 +136,46 @@ def test_cnn_pixel_state_representation():
     b = model.Bot(bots[1].player, m.field, "NN", StubLearner(), p, m.rgbGenerator)
     with pytest.raises(ValueError):
         b.getStateRepresentation()
+
+
+@pytest.mark.parametrize("variant", ["simple", "cnn_grid"])
+def test_state_variants_through_the_facade(variant):
+    """Bot.getStateRepresentation for GRID_VIEW_ENABLED = False (a 12-value list,
+    bot.py:296-297, 511-547) and for the CNN over the grid view (CNN_REPR without
+    CNN_P_REPR: [NUM_OF_GRIDS, 84, 84], bot.py:284), equal to the oracle's states
+    of the same bots in the same world."""
+    p = params()
+    if variant == "simple":
+        p.GRID_VIEW_ENABLED = False
+    else:
+        p.CNN_REPR, p.CNN_P_REPR = True, False
+        p.CNN_USE_L1, p.CNN_USE_L2, p.CNN_INPUT_DIM_1, p.CNN_INPUT_DIM_2 = False, True, 42, 84
+    m = model.Model(False, False, p, seed=6, field_size=300, max_viruses=10)
+    bots = [m.createBot("Greedy") for _ in range(10)]
+    m.initialize()
+    o = Oracle(m.field.stepper.cfg)
+    o.load_state(m.field.stepper.get_state())
+    for t in range(12):
+        m.update()
+        o.set_commands(_commands(m.field.stepper.get_state()))  # the commands the tick ran with
+        o.step(1)
+    want = o.observe()
+    for b in bots:
+        s = b.getStateRepresentation()
+        i = b.player.index
+        if not b.player.getIsAlive():
+            assert s is None
+            continue
+        if variant == "simple":
+            assert isinstance(s, list) and len(s) == 12
+            got = np.array(s)
+        else:
+            assert s.shape == (7, 84, 84)
+            got = s.reshape(-1)
+        assert parity.obs_close(got[None], want[i][None]), (variant, i)
+    o.close()
+
+
+def _commands(st):
+    pf, pi = np.asarray(st["players_f"]), np.asarray(st["players_i"])
+    return np.c_[pf[:, 0], pf[:, 1], pi[:, 2], pi[:, 3]].astype(np.float64)

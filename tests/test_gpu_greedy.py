@@ -91,3 +91,35 @@ def test_greedy_matches_reference_commands_at_checkpoints(name, seed, gsplit, go
         assert checked > 0
     for x in (g, om, op):
         x.close()
+
+
+def test_c2_greedy_population_matches_oracle():
+    """BASELINE configs[1] / SURVEY.md §8d C2 at its stated population: 256 Greedy
+    bots, field 1200 (75 * sqrt(256)), 10,000 pellets, no viruses / split / eject,
+    250 ticks (the survey's 100-tick warm-up and 150 more): every command, every
+    event and the world against the oracle, and every bot's observation
+    (pellet, wall and enemy grids + fov extras) every 25 ticks."""
+    cfg = make_config(bots=256, virus=False, field_size=0, max_pellets=10000.0,
+                      channels=_abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY, extras=0x3)
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    g.reset(21)
+    o.reset(21)
+    assert g.get_state()["field_size"] == 1200
+    eaten = 0
+    for t in range(250):
+        g.policy_greedy(False)
+        o.policy_greedy(False)
+        cg, co = commands(g.get_state()), commands(o.get_state())
+        assert np.array_equal(cg, co), "tick %d: greedy commands differ" % t
+        g.step(1)
+        o.step(1)
+        ev = g.events()
+        assert np.array_equal(ev, o.events()), "events differ at tick %d" % t
+        eaten += int(np.sum(ev[:, 1] == _abi.EV_CELL_EAT_PELLET))
+        if (t + 1) % 25 == 0:
+            assert parity.obs_close(g.observe(), o.observe()), "observations differ at tick %d" % t
+            dif = parity.diff_states(g.get_state(), o.get_state())
+            assert not dif, "tick %d: %s" % (t, dif[:3])
+    assert eaten > 1000  # greedy bots converge on the pellets
+    g.close()
+    o.close()

@@ -1,0 +1,95 @@
+"""GPU: the state-representation variants of Bot.getStateRepresentation
+(bot.py:272-299) beside the default grid (a25 of SURVEY.md §8):
+
+  * getSimpleStateRepresentation (GRID_VIEW_ENABLED = False, bot.py:511-547):
+    k_observe_simple, 12 values per bot;
+  * the CNN over the grid view (CNN_REPR without CNN_P_REPR, bot.py:103-111, 284)
+    at CNN_INPUT_DIM 42 and 84 squares per side: k_observe_wide.
+
+The oracle's restatements reproduce the reference's own states bit-exactly
+(tests/test_oracle_golden.py: simple16, cnn42, cnn84, MT mode).  Here the device
+runs the same scenarios re-keyed to Philox and matches the oracle: events
+exact, every bot's state every tick within 1e-5 (fov sizes and view boxes
+exactly equal)."""
+import numpy as np
+import pytest
+
+from aigar_amd import _abi
+from oracle_lib import Oracle, make_config
+import parity
+
+pytestmark = pytest.mark.gpu
+_lib = pytest.importorskip("aigar_amd._lib")
+
+
+def _run(cfg, ticks, seed, ps, pe, obs_every=1):
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    g.reset(seed)
+    o.reset(seed)
+    assert g.obs_len == o.obs_len
+    rng = np.random.default_rng(seed)
+    size = g.get_state()["field_size"]
+    n = cfg.bots_per_arena
+    for t in range(ticks):
+        cmd = parity.synthetic_commands(rng, None, n, size, ps, pe)
+        g.set_commands(cmd)
+        o.set_commands(cmd)
+        g.step(1)
+        o.step(1)
+        assert np.array_equal(g.events(), o.events()), "events differ at tick %d" % t
+        if (t + 1) % obs_every == 0:
+            og, oo = g.observe(), o.observe()
+            assert parity.obs_close(og, oo), "tick %d: states differ (max %g)" % (
+                t, np.nanmax(np.abs(np.nan_to_num(og, nan=0) - np.nan_to_num(oo, nan=0))))
+    dif = parity.diff_states(g.get_state(), o.get_state())
+    assert not dif, dif
+    out = g.observe(), o.observe()
+    g.close()
+    o.close()
+    return out
+
+
+@pytest.mark.parametrize("bots,field,virus,seed", [(16, 0, True, 8), (64, 600, True, 3), (128, 0, False, 4)])
+def test_simple_state_matches_oracle(bots, field, virus, seed):
+    cfg = make_config(bots=bots, field_size=field, virus=virus, max_viruses=20 if virus else -1.0,
+                      channels=_abi.OBS_SIMPLE, extras=0)
+    og, oo = _run(cfg, 80, seed, 0.03, 0.03)
+    assert og.shape == (bots, 12)
+    alive = ~np.isnan(oo[:, 0])
+    # some bots see an enemy cell and a pellet, some see a field edge
+    assert (og[alive, 3:6] != 0).any() and (og[alive, 6:8] != 0).any() and (og[alive, 8:12] != 1).any()
+
+
+@pytest.mark.parametrize("G,bots,seed", [(42, 24, 9), (84, 12, 10), (17, 32, 11)])
+def test_wide_grid_matches_oracle(G, bots, seed):
+    ch = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
+          | _abi.OBS_ENEMY_LF | _abi.OBS_SELF_SLF | _abi.OBS_ENEMY_SLF)
+    cfg = make_config(bots=bots, virus=True, max_viruses=12, channels=ch, extras=0, grid_squares=G)
+    og, oo = _run(cfg, 40, seed, 0.04, 0.04, obs_every=5)
+    assert og.shape == (bots, 9 * G * G)
+
+
+def test_wide_grid_overflow_pool_and_big_views():
+    """Big cells (wide views, thousands of visible pellets: the lists leave LDS for
+    the global pool) at 42 squares per side."""
+    ch = _abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_ENEMY | _abi.OBS_WALL
+    cfg = make_config(bots=8, field_size=500, channels=ch, extras=_abi.EX_FOV | _abi.EX_MASS, grid_squares=42)
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    o.reset(12)
+    st = o.get_state()
+    cf = np.array(st["cells_f"], copy=True)
+    cf[:3, 2] = [9000.0, 3000.0, 800.0]
+    cf[:3, 3] = np.sqrt(cf[:3, 2] / np.pi)
+    st["cells_f"] = cf
+    o.load_state(st)
+    g.load_state(st)
+    rng = np.random.default_rng(12)
+    for t in range(10):
+        cmd = parity.synthetic_commands(rng, None, 8, 500, 0.0, 0.0)
+        g.set_commands(cmd)
+        o.set_commands(cmd)
+        g.step(1)
+        o.step(1)
+        assert parity.obs_close(g.observe(), o.observe()), "tick %d" % t
+    g.close()
+    o.close()

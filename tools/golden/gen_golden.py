@@ -300,7 +300,24 @@ SCENARIOS = {
     # 64 reference Random bots (split + eject enabled via their own policy)
     "random64": dict(n=64, driver="random", size_per_player=75, density=0.0083, virus=False, split=True,
                      eject=True, ticks=120, ck_every=30, obs=False, seed=7),
+    # GRID_VIEW_ENABLED = False: getSimpleStateRepresentation (bot.py:511-547), 12 values per bot;
+    # big players see the field edges, small ones not
+    "simple16": dict(n=16, driver="scripted", virus=True, virus_density=4e-4, split=True, eject=True,
+                     p_split=0.03, p_eject=0.03, ticks=120, ck_every=20, obs=True, seed=8,
+                     boost=[(0, 900.0), (1, 300.0), (2, 120.0)], obs_over=dict(GRID_VIEW_ENABLED=False),
+                     obs_kind="simple"),
+    # CNN over the grid view (bot.py:103-111, 284: CNN_REPR without CNN_P_REPR): 42 squares per side,
+    # every channel incl. viruses and the last-frame grids, no extra inputs
+    "cnn42": dict(n=12, driver="scripted", virus=True, virus_density=4e-4, split=True, eject=True,
+                  p_split=0.03, p_eject=0.03, ticks=80, ck_every=40, obs=True, seed=9, boost=[(0, 400.0)],
+                  obs_over=dict(CNN_REPR=True, CNN_P_REPR=False, CNN_USE_L1=True), obs_kind="cnn"),
+    # ... and 84 squares per side (CNN_USE_L2) with Greedy bots that split
+    "cnn84": dict(n=6, driver="greedy", virus=False, split=True, eject=False, greedy_split=True, ticks=60,
+                  ck_every=30, obs=True, seed=10,
+                  obs_over=dict(CNN_REPR=True, CNN_P_REPR=False, CNN_USE_L1=False, CNN_USE_L2=True),
+                  obs_kind="cnn"),
 }
+OBS_SIMPLE = 0x400  # include/aigar.h AIGAR_OBS_SIMPLE
 
 
 def scripted_commands(field, rng, sc):
@@ -383,13 +400,20 @@ def run_scenario(ref, rec, name, sc):
         for p in field.players:
             obs_bots.append(ref.bot.Bot(p, field, "NN", None, params))
     ch_mask, ex_mask = obs_masks(params)
+    kind = sc.get("obs_kind", "grid")
+    G, L = params.GRID_SQUARES_PER_FOV, params.STATE_REPR_LEN
+    if kind == "simple":  # no grids, no extra inputs
+        ch_mask, ex_mask, L = OBS_SIMPLE, 0, 12
+    elif kind == "cnn":  # the grid view alone, [NUM_OF_GRIDS, G, G] with the bot's CNN side
+        G = obs_bots[0].gridSquaresPerFov if obs_bots else G
+        ex_mask, L = 0, params.NUM_OF_GRIDS * G * G
 
     out = {
         "n_players": np.int64(n), "size": np.int64(field.size),
         "max_pellets": np.float64(field.maxCollectibleCount), "max_viruses": np.float64(field.maxVirusCount),
         "virus_enabled": np.int64(int(field.virusEnabled)),
         "obs_channels": np.int64(ch_mask), "obs_extras": np.int64(ex_mask),
-        "obs_len": np.int64(params.STATE_REPR_LEN), "obs_grids": np.int64(params.NUM_OF_GRIDS),
+        "obs_len": np.int64(L), "obs_grids": np.int64(params.NUM_OF_GRIDS), "grid_squares": np.int64(G),
         "ticks": np.int64(sc["ticks"]),
     }
     for k, v in snapshot(field).items():
@@ -407,7 +431,6 @@ def run_scenario(ref, rec, name, sc):
     ck_ticks = []
 
     def record_obs(tag):
-        L = params.STATE_REPR_LEN
         arr = np.full((n, L), np.nan)
         for i, b in enumerate(obs_bots):
             s = b.getStateRepresentation()
