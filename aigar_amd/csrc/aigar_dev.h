@@ -105,6 +105,13 @@ struct TileRec {
 enum : int32_t { TR_HDR = 0, TR_PELLET = 1, TR_BLOB = 2, TR_CELL = 3, TR_HIST = 4 };
 constexpr int kHcapMax = 256;  // hand-off slots per message (LDS list of the plan kernel)
 
+// a pellet (field.py:303-313, 107-110): position, mass and creation sequence
+struct alignas(32) PelRec {
+  double x, y, m;
+  int64_t seq;
+};
+constexpr int kPelStride = 4;  // PelRec in 8-byte words (per-lane strided loads of one field)
+
 struct Dev {
   int A, B, NP, size, cols, H;
   int tiled, tile_id, ntiles, tcap, bm_words;  // tcap: records per outbox; bm_words: u64 words of the bitmap
@@ -156,11 +163,9 @@ struct Dev {
   double *sb_x, *sb_y, *sb_svx, *sb_svy;
   uint8_t *sb_slot;
   // pellets: two record buffers + staging
-  double *pel_x[2], *pel_y[2], *pel_m[2];
-  int64_t *pel_seq[2];
+  PelRec *pel[2];  // one 32-byte record per pellet: a bucket row's gather touches whole lines
   int *pel_col[2];  // colour owner: the player whose colour a blob-made pellet carries, -1: its own
-  double *pn_x, *pn_y, *pn_m;
-  int64_t *pn_seq;
+  PelRec *pn;
   int *pn_col;
   uint8_t *pel_dead;  // [A*Pcap] for the eat-phase buffer
   int *pel_rank;      // scratch [A*(Pcap)]

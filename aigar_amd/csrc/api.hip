@@ -301,10 +301,10 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(sb_x, double, C); AL(sb_y, double, C); AL(sb_svx, double, C); AL(sb_svy, double, C); AL(sb_slot, uint8_t, C);
   const size_t P = A * d.Pcap;
   for (int b = 0; b < 2; b++) {
-    AL(pel_x[b], double, P); AL(pel_y[b], double, P); AL(pel_m[b], double, P); AL(pel_seq[b], int64_t, P);
+    AL(pel[b], PelRec, P);
     AL(pel_col[b], int, P);
   }
-  AL(pn_x, double, P); AL(pn_y, double, P); AL(pn_m, double, P); AL(pn_seq, int64_t, P); AL(pn_col, int, P);
+  AL(pn, PelRec, P); AL(pn_col, int, P);
   AL(pel_dead, uint8_t, P); AL(pel_rank, int, 2 * P); AL(pcnt, int, A * H1); AL(pncnt, int, A * H1); AL(pstart, int, A * H1);
   AL(pel_owner, uint64_t, P);
   const size_t E = A * d.Ecap, V = A * d.Vcap;
@@ -988,10 +988,15 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
   std::vector<int> bsvc, vsvc, pcol, bcol;
   std::vector<uint32_t> bfl, vfl;
   const int pb = c.pcur;
-  if (d2h(h, px, d.pel_x[pb] + po, c.n_pel) || d2h(h, py, d.pel_y[pb] + po, c.n_pel) ||
-      d2h(h, pm, d.pel_m[pb] + po, c.n_pel) || d2h(h, ps, d.pel_seq[pb] + po, c.n_pel) ||
-      d2h(h, pcol, d.pel_col[pb] + po, c.n_pel))
-    return -1;
+  {
+    std::vector<PelRec> pr;
+    if (d2h(h, pr, d.pel[pb] + po, c.n_pel) || d2h(h, pcol, d.pel_col[pb] + po, c.n_pel)) return -1;
+    HIPCHK(hipStreamSynchronize(h->stream));  // (unpacked below)
+    px.resize(pr.size()); py.resize(pr.size()); pm.resize(pr.size()); ps.resize(pr.size());
+    for (size_t i = 0; i < pr.size(); i++) {
+      px[i] = pr[i].x; py[i] = pr[i].y; pm[i] = pr[i].m; ps[i] = pr[i].seq;
+    }
+  }
   double *bfs[8] = {d.b_x, d.b_y, d.b_m, d.b_r, d.b_vx, d.b_vy, d.b_svx, d.b_svy};
   double *vfs[8] = {d.v_x, d.v_y, d.v_m, d.v_r, d.v_vx, d.v_vy, d.v_svx, d.v_svy};
   for (int f = 0; f < 8; f++)
@@ -1193,16 +1198,15 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   }
   host_grid(d.cols, px, py, start, order);
   {
-    std::vector<double> sx(order.size()), sy(order.size()), sm(order.size());
-    std::vector<int64_t> ss(order.size());
+    std::vector<PelRec> sr(order.size());
     std::vector<int> sc(order.size());
     for (size_t i = 0; i < order.size(); i++) {
-      sx[i] = px[order[i]]; sy[i] = py[order[i]]; sm[i] = pm[order[i]]; ss[i] = ps[order[i]]; sc[i] = pc[order[i]];
+      sr[i] = PelRec{px[order[i]], py[order[i]], pm[order[i]], ps[order[i]]};
+      sc[i] = pc[order[i]];
     }
     const size_t po = (size_t)arena * d.Pcap;
-    if (h2d(h, d.pel_x[0] + po, sx) || h2d(h, d.pel_y[0] + po, sy) || h2d(h, d.pel_m[0] + po, sm) ||
-        h2d(h, d.pel_seq[0] + po, ss) || h2d(h, d.pel_col[0] + po, sc))
-      return -1;
+    if (h2d(h, d.pel[0] + po, sr) || h2d(h, d.pel_col[0] + po, sc)) return -1;
+    HIPCHK(hipStreamSynchronize(h->stream));  // (the host records go out of scope)
     HIPCHK(hipMemcpyAsync(d.pstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
     std::vector<int> cnt(d.H);  // per-bucket counts (the closing update keeps them with pstart)
     for (int b = 0; b < d.H; b++) cnt[b] = start[b + 1] - start[b];

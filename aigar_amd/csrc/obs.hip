@@ -366,21 +366,25 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     };
     wave_fov_walk(d, a, Q, fx, fy, fs, rmax_c, rmax_v, held && (d.obs_ch & AIGAR_OBS_PELLET), d.virus_enabled, own_cells,
                   [&](bool valid, int kd, size_t g) {
-      const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
-      const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
-      const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
+      // per-lane base and stride: a pellet is one 32-byte record (x, y, m, seq), the
+      // other kinds structure-of-arrays -- one load instruction per field either way
+      const PelRec *PR = d.pel[pcur];
+      const double *X = kd == 0 ? &PR->x : (kd == 1 ? d.c_x : d.v_x);
+      const double *Y = kd == 0 ? &PR->y : (kd == 1 ? d.c_y : d.v_y);
+      const double *M = kd == 0 ? &PR->m : (kd == 1 ? d.c_m : d.v_m);
       const double *RR = kd == 1 ? d.c_r : d.v_r;
-      const int64_t *S = kd == 0 ? d.pel_seq[pcur] : d.v_seq;
+      const int64_t *S = kd == 0 ? &PR->seq : d.v_seq;
       const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
+      const size_t gr = kd == 0 ? g * kPelStride : g;
       bool ok = false;
       double x = 0, y = 0, m = 0, r = 0;
       int64_t sq = 0;
       if (valid) {
-        x = X[g];
-        y = Y[g];
-        m = M[g];
+        x = X[gr];
+        y = Y[gr];
+        m = M[gr];
         r = kd == 0 ? 0.0 : RR[g];
-        sq = kd == 1 ? 0 : S[g];
+        sq = kd == 1 ? 0 : S[gr];
         uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
         if (kd == 0) r = pellet_radius(m);
         ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && pool_owner(g) == gp) &&
@@ -762,13 +766,15 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   wave_fov_walk(d, a, Q, fx, fy, fs, ctl.rmax_cell, ctl.rmax_virus, true, d.virus_enabled, [] {},
                 [&](bool valid, int kd, size_t g) {
     if (!valid) return;
-    const double *X = kd == 0 ? d.pel_x[pcur] : (kd == 1 ? d.c_x : d.v_x);
-    const double *Y = kd == 0 ? d.pel_y[pcur] : (kd == 1 ? d.c_y : d.v_y);
-    const double *M = kd == 0 ? d.pel_m[pcur] : (kd == 1 ? d.c_m : d.v_m);
+    const PelRec *PR = d.pel[pcur];
+    const double *X = kd == 0 ? &PR->x : (kd == 1 ? d.c_x : d.v_x);
+    const double *Y = kd == 0 ? &PR->y : (kd == 1 ? d.c_y : d.v_y);
+    const double *M = kd == 0 ? &PR->m : (kd == 1 ? d.c_m : d.v_m);
     const double *RR = kd == 1 ? d.c_r : d.v_r;
-    const int64_t *S = kd == 0 ? d.pel_seq[pcur] : (kd == 1 ? d.c_seq : d.v_seq);
+    const int64_t *S = kd == 0 ? &PR->seq : (kd == 1 ? d.c_seq : d.v_seq);
     const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
-    const double x = X[g], y = Y[g], m = M[g];
+    const size_t gr = kd == 0 ? g * kPelStride : g;
+    const double x = X[gr], y = Y[gr], m = M[gr];
     const double r = kd == 0 ? pellet_radius(m) : RR[g];
     const uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
     if ((fl & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
@@ -777,7 +783,7 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
     if (kd != 0 && !(bm > 1.25 * m)) return;  // the biggest own cell must be able to eat it
     const double sd = (x - bx) * (x - bx) + (y - by) * (y - by);
     const double k = m / (sd != 0 ? sd : 1);
-    const uint64_t ord = ((uint64_t)kd << 56) | (uint64_t)S[g];
+    const uint64_t ord = ((uint64_t)kd << 56) | (uint64_t)S[gr];
     if (k > best || (k == best && ord < bord)) {
       best = k;
       bord = ord;

@@ -242,10 +242,7 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
       return;
     }
     size_t pj = (size_t)a * d.Pcap + j;
-    d.pn_x[pj] = d.b_x[gi];
-    d.pn_y[pj] = d.b_y[gi];
-    d.pn_m[pj] = d.b_m[gi];
-    d.pn_seq[pj] = d.b_seq[gi];
+    d.pn[pj] = PelRec{d.b_x[gi], d.b_y[gi], d.b_m[gi], d.b_seq[gi]};
     d.pn_col[pj] = d.b_col[gi];  // (addPellet(blob): the same object, its colour kept)
     d.b_flags[gi] = 0;
     atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
@@ -1215,7 +1212,7 @@ __device__ __forceinline__ void pgrid_count_bucket(const Dev &d, int a, int i, i
 // (tiles: a record outside the held range is dropped, rank -1)
 __device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
   const size_t g = (size_t)a * d.Pcap + j, H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
-  const int bx = center_bucket_coord(d.pn_x[g], d.cols), by = center_bucket_coord(d.pn_y[g], d.cols);
+  const int bx = center_bucket_coord(d.pn[g].x, d.cols), by = center_bucket_coord(d.pn[g].y, d.cols);
   if (!tile_holds_bucket(d, bx, by)) {
     d.pel_rank[R0 + d.Pcap + j] = -1;
     return;
@@ -1256,10 +1253,13 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
       d.pel_dead[g] = 0;
       return;
     }
-    x = d.pel_x[src][g];
-    y = d.pel_y[src][g];
-    m = d.pel_m[src][g];
-    s = d.pel_seq[src][g];
+    {
+      const PelRec r_ = d.pel[src][g];
+      x = r_.x;
+      y = r_.y;
+      m = r_.m;
+      s = r_.seq;
+    }
     col = d.pel_col[src][g];
     int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
     pos = d.pstart[H1 + b] + d.pel_rank[R0 + i];
@@ -1276,10 +1276,13 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
     }
     const int rk = d.pel_rank[R0 + d.Pcap + j];
     if (rk < 0) return;  // (tiles: not held here)
-    x = d.pn_x[g];
-    y = d.pn_y[g];
-    m = d.pn_m[g];
-    s = d.pn_seq[g];
+    {
+      const PelRec r_ = d.pn[g];
+      x = r_.x;
+      y = r_.y;
+      m = r_.m;
+      s = r_.seq;
+    }
     col = d.pn_col[g];
     int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
     pos = d.pstart[H1 + b + 1] - 1 - rk;
@@ -1289,10 +1292,7 @@ __device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode
     return;
   }
   size_t o = (size_t)a * d.Pcap + pos;
-  d.pel_x[dst][o] = x;
-  d.pel_y[dst][o] = y;
-  d.pel_m[dst][o] = m;
-  d.pel_seq[dst][o] = s;
+  d.pel[dst][o] = PelRec{x, y, m, s};
   d.pel_col[dst][o] = col;
   if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
 }
@@ -1758,13 +1758,30 @@ struct Food {
   __device__ size_t g(int j) const { return (size_t)a * d.Pcap + j; }               // pellet j
   __device__ size_t gs(int j) const { return (size_t)a * d.Pcap + (j - n0); }       // staged pellet j
   __device__ size_t gb(int j) const { return (size_t)a * d.Ecap + (j & ~kBlobBit); }  // blob
-  __device__ double x(int j) const { return blob(j) ? d.b_x[gb(j)] : (j < n0 ? d.pel_x[pb][g(j)] : d.pn_x[gs(j)]); }
-  __device__ double y(int j) const { return blob(j) ? d.b_y[gb(j)] : (j < n0 ? d.pel_y[pb][g(j)] : d.pn_y[gs(j)]); }
-  __device__ double m(int j) const { return blob(j) ? d.b_m[gb(j)] : (j < n0 ? d.pel_m[pb][g(j)] : d.pn_m[gs(j)]); }
+  __device__ double x(int j) const { return blob(j) ? d.b_x[gb(j)] : (j < n0 ? d.pel[pb][g(j)].x : d.pn[gs(j)].x); }
+  __device__ double y(int j) const { return blob(j) ? d.b_y[gb(j)] : (j < n0 ? d.pel[pb][g(j)].y : d.pn[gs(j)].y); }
+  __device__ double m(int j) const { return blob(j) ? d.b_m[gb(j)] : (j < n0 ? d.pel[pb][g(j)].m : d.pn[gs(j)].m); }
   __device__ double r(int j) const { return blob(j) ? d.b_r[gb(j)] : radius_of(m(j)); }
   __device__ int64_t seq(int j) const {
-    return blob(j) ? d.b_seq[gb(j)] : (j < n0 ? d.pel_seq[pb][g(j)] : d.pn_seq[gs(j)]);
+    return blob(j) ? d.b_seq[gb(j)] : (j < n0 ? d.pel[pb][g(j)].seq : d.pn[gs(j)].seq);
   }
+  // the whole food record in one round of loads (a pellet: its 32-byte record)
+  __device__ void load(int j, double &x, double &y, double &m, int64_t &sq) const {
+    if (blob(j)) {
+      const size_t b = gb(j);
+      x = d.b_x[b];
+      y = d.b_y[b];
+      m = d.b_m[b];
+      sq = d.b_seq[b];
+    } else {
+      const PelRec r = j < n0 ? d.pel[pb][g(j)] : d.pn[gs(j)];
+      x = r.x;
+      y = r.y;
+      m = r.m;
+      sq = r.seq;
+    }
+  }
+  __device__ double rad(int j, double m) const { return blob(j) ? d.b_r[gb(j)] : radius_of(m); }
   __device__ bool alive(int j) const { return blob(j) ? (d.b_flags[gb(j)] & F_ALIVE) != 0 : !d.pel_dead[g(j)]; }
   __device__ int64_t ej(int j) const { return blob(j) ? d.b_ej[gb(j)] : -2; }
   __device__ void kill(int j) const {
@@ -1867,18 +1884,18 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
     auto visit = [&](bool valid, int j) {
       bool keep = false;
       double fx = 0, fy = 0, fm = 0;
-      if (valid && F.alive(j) && F.ej(j) != cseq) {  // a blob's own ejecter cell skips it (field.py:219)
-        fx = F.x(j);
-        fy = F.y(j);
-        fm = F.m(j);
-        keep = rect_hit(footprint(fx, fy, F.r(j), d.size), q);
+      int64_t fsq = 0;
+      if (valid) {  // the record and the liveness in one round of loads
+        F.load(j, fx, fy, fm, fsq);
+        // a blob's own ejecter cell skips it (field.py:219)
+        keep = F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(fx, fy, F.rad(j, fm), d.size), q);
       }
       unsigned long long bal = __ballot(keep);
       int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
       if (keep) {
         lsum += fm;
         if (slot < PREP_CAND) {
-          s_seq[w][slot] = Food::order_key(j, F.seq(j));
+          s_seq[w][slot] = Food::order_key(j, fsq);
           s_x[w][slot] = fx;
           s_y[w][slot] = fy;
           s_m[w][slot] = fm;
@@ -1897,18 +1914,18 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
     auto visit_b = [&](bool valid, int j) {  // as visit, against the blob-turn box bound
       bool keep = false;
       double fx = 0, fy = 0, fm = 0;
-      if (valid && F.alive(j) && F.ej(j) != cseq) {  // a blob's own ejecter cell skips it (field.py:219)
-        fx = F.x(j);
-        fy = F.y(j);
-        fm = F.m(j);
-        keep = rect_hit(footprint(fx, fy, F.r(j), d.size), qb);
+      int64_t fsq = 0;
+      if (valid) {  // the record and the liveness in one round of loads
+        F.load(j, fx, fy, fm, fsq);
+        // a blob's own ejecter cell skips it (field.py:219)
+        keep = F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(fx, fy, F.rad(j, fm), d.size), qb);
       }
       unsigned long long bal = __ballot(keep);
       int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
       if (keep) {
         lsum += fm;
         if (slot < PREP_CAND) {
-          s_seq[w][slot] = Food::order_key(j, F.seq(j));
+          s_seq[w][slot] = Food::order_key(j, fsq);
           s_x[w][slot] = fx;
           s_y[w][slot] = fy;
           s_m[w][slot] = fm;
@@ -2806,8 +2823,8 @@ __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
         double x, y;
         if (j < nconv) {
           const size_t g = (size_t)a * d.Pcap + j;
-          x = d.pn_x[g];
-          y = d.pn_y[g];
+          x = d.pn[g].x;
+          y = d.pn[g].y;
           live = !d.pel_dead[(size_t)a * d.Pcap + n0 + j];
         } else {
           spawn_pellet_at(d, a, j - nconv, &x, &y);
@@ -2850,8 +2867,8 @@ __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
       double x, y;
       if (tid < nconv) {
         const size_t g = (size_t)a * d.Pcap + tid;
-        x = d.pn_x[g];
-        y = d.pn_y[g];
+        x = d.pn[g].x;
+        y = d.pn[g].y;
         live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
       } else {
         spawn_pellet_at(d, a, tid - nconv, &x, &y);
@@ -2888,7 +2905,7 @@ __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
       int64_t k = 0;
       if (j < nst) {
         const size_t g = (size_t)a * d.Pcap + j;
-        const int bx = center_bucket_coord(d.pn_x[g], d.cols), by = center_bucket_coord(d.pn_y[g], d.cols);
+        const int bx = center_bucket_coord(d.pn[g].x, d.cols), by = center_bucket_coord(d.pn[g].y, d.cols);
         live = !(j < nconv && d.pel_dead[(size_t)a * d.Pcap + n0 + j]) && tile_holds_bucket(d, bx, by);
         k = ((int64_t)(by * d.cols + bx) << 32) | j;
       }
@@ -3140,10 +3157,7 @@ __device__ void spawn_pellet_at(const Dev &d, int a, int j, double *px, double *
   int64_t seq;
   spawn_pellet_rec(d, c, j, x, y, m, seq);
   size_t o = (size_t)a * d.Pcap + c.n_pnew + j;
-  d.pn_x[o] = x;
-  d.pn_y[o] = y;
-  d.pn_m[o] = m;
-  d.pn_seq[o] = seq;
+  d.pn[o] = PelRec{x, y, m, seq};
   d.pn_col[o] = -1;  // Cell(..., None): a colour of its own
   if (px) {
     *px = x;
@@ -3161,10 +3175,7 @@ __device__ __forceinline__ void spawn_pellet(const Dev &d, int gi, bool rank_sta
   int64_t sr = (int64_t)mulhi(u[2], 50);
   double m = (sr > 50 - 4) ? (double)(50 - sr) : 1.0;  // randomSize (field.py:20-26)
   size_t o = (size_t)a * d.Pcap + c.n_pnew + j;
-  d.pn_x[o] = (double)x;
-  d.pn_y[o] = (double)y;
-  d.pn_m[o] = m;
-  d.pn_seq[o] = c.seq_base_spawn + j;
+  d.pn[o] = PelRec{(double)x, (double)y, m, c.seq_base_spawn + j};
   d.pn_col[o] = -1;  // Cell(..., None): a colour of its own
   if (rank_staged) pgrid_rank_staged(d, a, c.n_pnew + j);  // rebuild ranks taken at spawn time
 }
@@ -3262,8 +3273,8 @@ __device__ __forceinline__ void pellet_lists_wave(const Dev &d, const ArenaCtl &
     double x, y;
     if (tid < nconv) {
       const size_t g = (size_t)a * d.Pcap + tid;
-      x = d.pn_x[g];
-      y = d.pn_y[g];
+      x = d.pn[g].x;
+      y = d.pn[g].y;
       live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
     } else {  // (nsp <= kSpawnAhead)
       const size_t o = (size_t)a * kSpawnAhead + tid - nconv;
@@ -3379,10 +3390,7 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
         const int pos = i - kb + sb;
         if (pos < d.Pcap) {
           const size_t o = P0 + pos;
-          d.pel_x[dst][o] = x;
-          d.pel_y[dst][o] = y;
-          d.pel_m[dst][o] = m;
-          d.pel_seq[dst][o] = sq;
+          d.pel[dst][o] = PelRec{x, y, m, sq};
           d.pel_col[dst][o] = col;
         }
       }
@@ -3409,10 +3417,7 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
     const int pos = start + surv + r;
     if (pos >= d.Pcap) continue;
     const size_t o = P0 + pos, gs = P0 + (int)(ls[t] & 0xFFFFFFFFll);
-    d.pel_x[dst][o] = d.pn_x[gs];
-    d.pel_y[dst][o] = d.pn_y[gs];
-    d.pel_m[dst][o] = d.pn_m[gs];
-    d.pel_seq[dst][o] = d.pn_seq[gs];
+    d.pel[dst][o] = d.pn[gs];
     d.pel_col[dst][o] = d.pn_col[gs];
   }
   d.pstart[(size_t)a * (d.H + 1) + i] = start;
@@ -3441,10 +3446,13 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
   int col = -1, s0 = 0, c0 = 0;
   if (pel && i < n0) {
     dead = d.pel_dead[g];
-    x = d.pel_x[src][g];
-    y = d.pel_y[src][g];
-    m = d.pel_m[src][g];
-    sq = d.pel_seq[src][g];
+    {
+      const PelRec r_ = d.pel[src][g];
+      x = r_.x;
+      y = r_.y;
+      m = r_.m;
+      sq = r_.seq;
+    }
     col = d.pel_col[src][g];
   } else if (!pel && i < d.H) {
     s0 = d.pstart[(size_t)a * (d.H + 1) + i];
@@ -3488,10 +3496,7 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
         const int pos = i - count_below_i32(K, nk, i) + count_below_i64(S, ns, (int64_t)b << 32);
         if (pos < d.Pcap) {
           const size_t o = P0 + pos;
-          d.pel_x[dst][o] = x;
-          d.pel_y[dst][o] = y;
-          d.pel_m[dst][o] = m;
-          d.pel_seq[dst][o] = sq;
+          d.pel[dst][o] = PelRec{x, y, m, sq};
           d.pel_col[dst][o] = col;
         }
       }
@@ -3508,18 +3513,12 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
       const size_t o = P0 + pos;
       if (small && js >= nconv) {  // a spawn, drawn by k_tick_begin (k_spawn_plan did not stage it)
         const size_t so = (size_t)a * kSpawnAhead + js - nconv;
-        d.pel_x[dst][o] = d.spec_x[so];
-        d.pel_y[dst][o] = d.spec_y[so];
-        d.pel_m[dst][o] = d.spec_m[so];
-        d.pel_seq[dst][o] = c.seq_base_spawn + (js - nconv);
+        d.pel[dst][o] = PelRec{d.spec_x[so], d.spec_y[so], d.spec_m[so], c.seq_base_spawn + (js - nconv)};
         d.pel_col[dst][o] = -1;
         continue;
       }
       const size_t gs = P0 + js;
-      d.pel_x[dst][o] = d.pn_x[gs];
-      d.pel_y[dst][o] = d.pn_y[gs];
-      d.pel_m[dst][o] = d.pn_m[gs];
-      d.pel_seq[dst][o] = d.pn_seq[gs];
+      d.pel[dst][o] = d.pn[gs];
       d.pel_col[dst][o] = d.pn_col[gs];
     }
     d.pstart[(size_t)a * (d.H + 1) + i] = start;
@@ -3832,7 +3831,7 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int fir
       const Food F(d, 0);
       const int b = by * d.cols + bx, lo = min(d.pstart[b], F.n0), hi = min(d.pstart[b + 1], F.n0);
       for (int t = lo; t < hi; t++)
-        if (d.pel_seq[F.pb][F.g(t)] == r.seq) {
+        if (d.pel[F.pb][F.g(t)].seq == r.seq) {
           uint8_t *pd = d.pel_dead + F.g(t);  // (flag set through its 32-bit word: the first setter notes the kill)
           unsigned *w = (unsigned *)((uintptr_t)pd & ~(uintptr_t)3);
           const unsigned sh = (unsigned)((uintptr_t)pd & 3) * 8;
@@ -3840,7 +3839,7 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int fir
           return;
         }
       for (int j = F.n0; j < F.n0 + F.nst; j++)  // this tick's blob conversions (staged)
-        if (d.pn_seq[F.gs(j)] == r.seq) {
+        if (d.pn[F.gs(j)].seq == r.seq) {
           d.pel_dead[F.g(j)] = 1;
           return;
         }

@@ -82,8 +82,9 @@ def obs_bytes_per_bot(L, p_fov, c_fov, v_fov, n_cells=1.2):
 
 
 def pmc_traffic(kernel_prefix, workload):
-    """HBM-side bytes per launch of the kernel from the newest committed PMC
-    summary (profiles/r*_pmc_<workload>.json, written by tools/pmc.sh +
+    """HBM-side bytes per launch of the kernel (kernel_prefix "_step": per env
+    step, all the step's kernels) from the newest committed PMC summary
+    (profiles/r*_pmc_<workload>.json, written by tools/pmc.sh +
     tools/pmc_summary.py on the same bench command).  None if absent."""
     import glob
     import re
@@ -96,7 +97,7 @@ def pmc_traffic(kernel_prefix, workload):
         return None, None
     data = json.load(open(files[-1]))
     for k, v in data.items():
-        if kernel_prefix in k:
+        if kernel_prefix in k and "traffic_bytes" in v:
             return float(v["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
     return None, None
 
@@ -469,6 +470,7 @@ def main():
         achieved = obs_bytes_launch / obs_avg_s / 1e9
         peak = 8000.0
         traffic, traffic_src = pmc_traffic("k_observe", name)
+        step_traffic, step_src = pmc_traffic("_step", name)
         eaten = work["pellets_eaten"] - w0["pellets_eaten"] if "pellets_eaten" in work else 0
         step_bytes = tick_bytes(st, alive, field, eaten / ticks_timed) * arenas + obs_bytes_launch
         out["roofline"] = {
@@ -478,7 +480,9 @@ def main():
             "reads": {"bytes_per_launch": int(reads_bot * alive),
                       "frac": reads_bot * alive / obs_avg_s / 1e9 / peak},
             "step": {"bytes_per_step": int(step_bytes), "frac": step_bytes / (elapsed / args.steps) / 1e9 / peak,
-                     "note": "algorithmic bytes of the whole env step (tick + observation) / ms_per_step"}}
+                     "traffic": None if step_traffic is None else int(step_traffic), "traffic_source": step_src,
+                     "note": "algorithmic bytes of the whole env step (tick + observation) / ms_per_step; "
+                             "traffic: PMC bytes of all the step's kernels per step"}}
         out["breakdown_ms_per_step"] = {"policy": pol_ms / max(1, pol_n), "tick": tick_ms / max(1, tick_n),
                                         "observe": obs_ms / max(1, obs_n)}
     out["world"] = {"pellets": st["n_pellets"], "cells": st["n_cells"], "viruses": st["n_viruses"],

@@ -30,6 +30,7 @@ def _run(cfg, ticks, seed, ps, pe, obs_every=1):
     rng = np.random.default_rng(seed)
     size = g.get_state()["field_size"]
     n = cfg.bots_per_arena
+    seen = []
     for t in range(ticks):
         cmd = parity.synthetic_commands(rng, None, n, size, ps, pe)
         g.set_commands(cmd)
@@ -41,23 +42,23 @@ def _run(cfg, ticks, seed, ps, pe, obs_every=1):
             og, oo = g.observe(), o.observe()
             assert parity.obs_close(og, oo), "tick %d: states differ (max %g)" % (
                 t, np.nanmax(np.abs(np.nan_to_num(og, nan=0) - np.nan_to_num(oo, nan=0))))
+            seen.append(oo)
     dif = parity.diff_states(g.get_state(), o.get_state())
     assert not dif, dif
-    out = g.observe(), o.observe()
     g.close()
     o.close()
-    return out
+    return np.concatenate(seen)
 
 
 @pytest.mark.parametrize("bots,field,virus,seed", [(16, 0, True, 8), (64, 600, True, 3), (128, 0, False, 4)])
 def test_simple_state_matches_oracle(bots, field, virus, seed):
     cfg = make_config(bots=bots, field_size=field, virus=virus, max_viruses=20 if virus else -1.0,
                       channels=_abi.OBS_SIMPLE, extras=0)
-    og, oo = _run(cfg, 80, seed, 0.03, 0.03)
-    assert og.shape == (bots, 12)
-    alive = ~np.isnan(oo[:, 0])
-    # some bots see an enemy cell and a pellet, some see a field edge
-    assert (og[alive, 3:6] != 0).any() and (og[alive, 6:8] != 0).any() and (og[alive, 8:12] != 1).any()
+    states = _run(cfg, 80, seed, 0.03, 0.03)
+    assert states.shape == (80 * bots, 12)
+    live = states[~np.isnan(states[:, 0])]
+    # over the run, bots saw enemy cells, pellets and field edges
+    assert (live[:, 3:6] != 0).any() and (live[:, 6:8] != 0).any() and (live[:, 8:12] != 1).any()
 
 
 @pytest.mark.parametrize("G,bots,seed", [(42, 24, 9), (84, 12, 10), (17, 32, 11)])
@@ -65,8 +66,8 @@ def test_wide_grid_matches_oracle(G, bots, seed):
     ch = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
           | _abi.OBS_ENEMY_LF | _abi.OBS_SELF_SLF | _abi.OBS_ENEMY_SLF)
     cfg = make_config(bots=bots, virus=True, max_viruses=12, channels=ch, extras=0, grid_squares=G)
-    og, oo = _run(cfg, 40, seed, 0.04, 0.04, obs_every=5)
-    assert og.shape == (bots, 9 * G * G)
+    states = _run(cfg, 40, seed, 0.04, 0.04, obs_every=5)
+    assert states.shape == (8 * bots, 9 * G * G)
 
 
 def test_wide_grid_overflow_pool_and_big_views():
