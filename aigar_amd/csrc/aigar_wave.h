@@ -9,6 +9,17 @@
 
 namespace aigar {
 
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, workgroup dispatch), so block b and b + 1 sit on
+// different L2s.  Kernels with one wave per player remap b so that the players
+// of consecutive logical blocks -- whose per-player words share 128-B lines
+// (p_fx, c_x[slot * NP + gp], ...) -- are served by one XCD's L2.  Placement
+// is only observed, never guaranteed: a bijection, correct for any placement.
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int per = nb >> 3, rem = nb & 7, x = b & 7, i = b >> 3;
+  return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+}
+
 // a wave-uniform value moved to SGPRs (the compiler keeps a uniform value that
 // came from a vector load in VGPRs; in a register-bound kernel that costs waves)
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }

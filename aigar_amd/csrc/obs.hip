@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   __shared__ int64_t v_seqs[OBS_VCAP];
   __shared__ uint32_t v_mask[OBS_VCAP];
 
-  const int gp = blockIdx.x, lane = threadIdx.x;
+  const int gp = xcd_block(blockIdx.x, gridDim.x), lane = threadIdx.x;
   const int NP = d.NP, a = gp / d.B, G = d.G, GG = G * G, L = d.L;
   // a masked-out bot does not compute its state this tick: no row, no history update
   // (the reference's getStateRepresentation runs only for NN bots that are not skipping)
@@ -731,7 +731,7 @@ __device__ __forceinline__ double py_round5(double v) {
 // each by creation sequence).  mask (optional): which players are Greedy bots.
 // mask: NULL = every player; want < 0: players with mask != 0; else mask == want
 __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, const uint8_t *mask, int want) {
-  const int gp = blockIdx.x, lane = threadIdx.x, NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  const int gp = xcd_block(blockIdx.x, gridDim.x), lane = threadIdx.x, NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   if (!d.p_alive[gp] || (mask && (want < 0 ? !mask[gp] : mask[gp] != want))) return;  // (dead players keep their command)
   const ArenaCtl &ctl = d.ctl[a];
   const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];

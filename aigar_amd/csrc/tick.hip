@@ -1852,7 +1852,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   __shared__ uint8_t s_sel[4][PREP_CAND];
   PT_BEGIN(0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wi = blockIdx.x * 4 + w, gp = wi / PREP_WAVES, h = wi - gp * PREP_WAVES;
+  const int wi = xcd_block(blockIdx.x, gridDim.x) * 4 + w, gp = wi / PREP_WAVES, h = wi - gp * PREP_WAVES;
   if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP) return;
   // this wave's first list row rides the liveness / count load round (the row
@@ -2406,7 +2406,7 @@ __device__ void occ_rebuild_dirty(const Dev &d, int a, const uint32_t *dirty) {
 __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   PT_BEGIN(3);
   const int lane = threadIdx.x & 63;
-  const int gp = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int gp = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
   // C4, device-bounded eat passes: the tick may go on only if no owned cell is undone
   if (d.tiled && gp == 0 && lane == 0 && d.ctl[0].n_undone_glob != 0) atomicOr(&d.ctl[0].err, ERR_TILE_PASSES);
   if (gp >= d.NP) return;
