@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
     return;
   }
-  if (d.tiled) {  // C4: one tile observes the bot -- its history holder, else its view centre's tile (k_tile_plan)
+  if (d.tiled) {  // C4: one tile observes the bot -- its history holder, else its view centre's tile (tile_plan_thread)
     const int hold = d.t_holder[gp];
     const int by = hold >= 0 ? hold : tile_of(d, fx, fy);
     if (lane == 0) d.t_obsby[gp] = by;  // (every tile records the same observer)

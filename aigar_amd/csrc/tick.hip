@@ -597,6 +597,49 @@ __device__ void tick_zero(const Dev &d, int gi) {
     if (j < c.pu_nconv && c.pu_n0 + j < d.Pcap) d.pel_dead[(size_t)a * d.Pcap + c.pu_n0 + j] = 0;
   }
 }
+// C4: the tick's first pass opens with the observation hand-off plan: extra
+// threads of k_tick_begin, one per player.  A bot's history is current on
+// t_holder (-1: on every tile), or on the tile that observed it since the last
+// plan (t_obsby) -- that update is replicated, every tile makes it.  The holder
+// hands the history off when the bot is dead (it respawns anywhere) or its
+// view centre (the FOV cache, end of the last tick) lies in another tile: it
+// takes a slot of its first-pass message (at most hcap per tick, in any order;
+// the rest wait a tick) and drops the bot (t_holder := -1); every other tile
+// does the same for the slots it receives (k_tile_apply), so the holders stay
+// identical on every tile.  Otherwise the holder observes the bot again: its
+// centre moved at most one tick's distance from the tile, which the halo covers.
+__device__ void tile_plan_thread(const Dev &d, int gp) {
+  ArenaCtl &c = d.ctl[0];
+  if (gp == 0) {  // the first pass's counters
+    c.n_out = c.n_out_pel = c.n_undone = 0;
+    c.n_eaten_glob = 0;
+  }
+  if (gp >= d.NP) return;
+  int h = d.t_holder[gp];
+  const int ob = d.t_obsby[gp];
+  if (ob >= 0) {
+    h = ob;
+    d.t_obsby[gp] = -1;
+    d.t_holder[gp] = h;
+  }
+  if (h != d.tile_id) return;
+  if (d.p_alive[gp] && tile_of(d, d.p_fx[gp], d.p_fy[gp]) == h) return;
+  const int sl = atomicAdd(&c.n_ho, 1);
+  if (sl >= d.hcap) return;  // (the header clamps the slot count)
+  d.t_holder[gp] = -1;
+  const int GG = d.G * d.G;
+  TileRec *slot = d.outbox + 1 + d.tcap + (size_t)sl * d.hrec;
+  slot->kind = TR_HIST;
+  slot->idx = gp;
+  slot->seq = 0;
+  slot->x = d.o_lastfov[gp];
+  slot->y = 0;
+  double *dst = (double *)(slot + 1);
+  for (int g = 0; g < d.nh; g++) {
+    const double *src = hist_grid(d, g) + (size_t)gp * GG;
+    for (int t = 0; t < GG; t++) dst[g * GG + t] = src[t];
+  }
+}
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   PT_BEGIN(2);
   int gi = GTID;
@@ -617,7 +660,9 @@ __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   gi -= d.A * d.Ecap;
   if (gi < d.A * kSpawnAhead) return spawn_ahead(d, gi / kSpawnAhead, gi % kSpawnAhead);
   gi -= d.A * kSpawnAhead;
-  if (gi < kTickZero) tick_zero(d, gi);
+  if (gi < kTickZero) return tick_zero(d, gi);
+  gi -= kTickZero;
+  if (d.tiled) tile_plan_thread(d, gi);  // C4: the observation hand-off plan
 }
 
 // rank of this thread among the flagged threads of the block (thread order);
@@ -3635,7 +3680,9 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap +
                        (long)d.A * kSpawnAhead + kTickZero;
-  hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin, 256)), dim3(256), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
+  // (C4 tiles: + one block, the observation hand-off plan of the tick's first eat pass)
+  hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin + (d.tiled ? d.NP : 0), 256)), dim3(256), 0, s, d,
+                     rp ? *rp : RandomPolicy{0, 0, 0, 0});
   // + the virus grid (extra block) and the blob grid (last block) of updateHashTables
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + (d.virus_enabled ? 1 : 0), d.A), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
@@ -3678,218 +3725,146 @@ __global__ void k_tile_pass_begin(Dev d) {  // a later pass
   c.n_out = c.n_out_pel = c.n_undone = 0;
   c.n_ho = 0;
 }
-// The tick's first pass opens with the observation hand-off plan (one block;
-// every tile computes the same plan from replicated state).  A bot's history is
-// current on t_holder (-1: on every tile), or on the tile that observed it since
-// the last plan (t_obsby).  It is handed off -- sent by its holder, applied by
-// every tile, t_holder := -1 -- when the bot is dead (it respawns anywhere) or
-// its view centre (the FOV cache, end of the last tick) lies in another tile;
-// otherwise the holder observes it again and, the centre having moved at most one
-// tick's distance from its tile, the held halo covers the view.  At most hcap
-// bots per holder per tick (in player order); the rest wait a tick.
-__global__ void __launch_bounds__(1024) k_tile_plan(Dev d) {
-  __shared__ int wcnt[16][64];
-  __shared__ int run[64];
-  __shared__ int sl_gp[kHcapMax];
-  ArenaCtl &c = d.ctl[0];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, T = d.ntiles;
-  if (tid == 0) {
-    c.n_out = c.n_out_pel = c.n_undone = 0;
-    c.n_eaten_glob = 0;
-  }
-  if (tid < T) run[tid] = 0;
-  __syncthreads();
-  for (int base = 0; base < d.NP; base += 1024) {
-    const int gp = base + tid;
-    int h = -1;
-    bool tr = false;
-    if (gp < d.NP) {
-      h = d.t_holder[gp];
-      const int ob = d.t_obsby[gp];
-      if (ob >= 0) {
-        h = ob;
-        d.t_obsby[gp] = -1;
-      }
-      if (h >= 0) tr = !d.p_alive[gp] || tile_of(d, d.p_fx[gp], d.p_fy[gp]) != h;
-    }
-    int lrank = 0;
-    for (int k = 0; k < T; k++) {  // rank among this chunk's hand-offs of the same holder
-      const unsigned long long m = __ballot(tr && h == k);
-      if (tr && h == k) lrank = __popcll(m & ((1ull << lane) - 1));
-      if (lane == 0) wcnt[w][k] = __popcll(m);
-    }
-    __syncthreads();
-    if (tid < T) {  // exclusive prefix over the waves, carried over the chunks
-      int r = run[tid];
-      for (int v = 0; v < 16; v++) {
-        const int t = wcnt[v][tid];
-        wcnt[v][tid] = r;
-        r += t;
-      }
-      run[tid] = r;
-    }
-    __syncthreads();
-    if (gp < d.NP) {
-      int hn = h;
-      if (tr) {
-        const int rank = lrank + wcnt[w][h];
-        if (rank < d.hcap) {
-          hn = -1;
-          if (h == d.tile_id) sl_gp[rank] = gp;
-        }
-      }
-      d.t_holder[gp] = hn;
-    }
-    __syncthreads();
-  }
-  const int nho = min(run[d.tile_id], d.hcap);
-  if (tid == 0) c.n_ho = nho;
-  // this tile's slots: [TR_HIST: player, lastFovSize][nh history grids]
-  const int GG = d.G * d.G, per = d.nh * GG;
-  TileRec *ho = d.outbox + 1 + d.tcap;
-  for (int e = tid; e < nho * (1 + per); e += 1024) {
-    const int sl = e / (1 + per), j = e - sl * (1 + per), gp = sl_gp[sl];
-    TileRec *slot = ho + (size_t)sl * d.hrec;
-    if (j == 0) {
-      slot->kind = TR_HIST;
-      slot->idx = gp;
-      slot->seq = 0;
-      slot->x = d.o_lastfov[gp];
-      slot->y = 0;
-    } else {
-      const int q = j - 1, g = q / GG, t = q - g * GG;
-      ((double *)(slot + 1))[q] = hist_grid(d, g)[(size_t)gp * GG + t];
-    }
-  }
-}
+__device__ void tile_header(const Dev &d);
 __global__ void __launch_bounds__(256) k_tile_collect(Dev d, int with_bitmap) {
   TILE_GATE(d);
   const int gp = GTID;
-  if (gp >= d.NP || !d.p_alive[gp]) return;
-  unsigned long long *bm = (unsigned long long *)(d.outbox + 1 + d.tcap);
-  const int NP = d.NP, n = d.p_ncells[gp];
-  int und = 0;
-  for (int k = 0; k < n; k++) {
-    const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-    if (!tile_owns(d, d.c_x[ci], d.c_y[ci])) continue;
-    if (d.f_done[ci] != 1) und++;
-    else if (with_bitmap) atomicOr(&bm[ci >> 6], 1ull << (ci & 63));
+  if (gp < d.NP && d.p_alive[gp]) {
+    unsigned long long *bm = (unsigned long long *)(d.outbox + 1 + d.tcap);
+    const int NP = d.NP, n = d.p_ncells[gp];
+    int und = 0;
+    for (int k = 0; k < n; k++) {
+      const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+      if (!tile_owns(d, d.c_x[ci], d.c_y[ci])) continue;
+      if (d.f_done[ci] != 1) und++;
+      else if (with_bitmap) atomicOr(&bm[ci >> 6], 1ull << (ci & 63));
+    }
+    if (und) atomicAdd(&d.ctl[0].n_undone, und);
   }
-  if (und) atomicAdd(&d.ctl[0].n_undone, und);
+  // the message header, once every owned cell is counted (the last block)
+  if (last_block(d.ticket + 3, gridDim.x) && threadIdx.x == 0) tile_header(d);
 }
-__global__ void k_tile_header(Dev d) {
+__device__ void tile_header(const Dev &d) {
   const ArenaCtl &c = d.ctl[0];
   TileRec &h = d.outbox[0];
   h.kind = TR_HDR;
   h.idx = min(c.n_out, d.tcap);
   h.seq = c.n_undone;
   h.x = (double)c.n_out_pel;
-  h.y = (double)c.n_ho;
+  h.y = (double)min(c.n_ho, d.hcap);
 }
 // The first pass's message has no bitmap: a tick that needs a second pass
 // learns the other tiles' non-eating final cells from the second pass's
 // bitmaps (it may take one pass longer; ticks rarely need a second at all).
 // A later pass is gated (Dev::tile_gate): issued without asking the host whether
 // it is needed, its kernels return at once when no owned cell is undone.
+// The first pass's bookkeeping (counters, the hand-off plan) ran in k_tick_begin.
 void launch_tile_pass(const Dev &d0, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first) {
   Dev d = d0;
   d.tile_gate = first ? 0 : 1;
-  if (first) hipLaunchKernelGGL(k_tile_plan, dim3(1), dim3(1024), 0, s, d);
-  else hipLaunchKernelGGL(k_tile_pass_begin, dim3(1), dim3(1), 0, s, d);
-  launch_food(d, s, rounds, Scratch{scr_k, scr_v}, first ? 0 : 1);
+  if (!first) hipLaunchKernelGGL(k_tile_pass_begin, dim3(1), dim3(1), 0, s, d);
+  launch_food(d, s, rounds, Scratch{scr_k, scr_v}, first ? 0 : 1, 1);  // (serial rest in the last commit block)
   if (!first) (void)hipMemsetAsync(d.outbox + 1 + d.tcap, 0, 8 * (size_t)d.bm_words, s);
   hipLaunchKernelGGL(k_tile_collect, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, first ? 0 : 1);
-  hipLaunchKernelGGL(k_tile_header, dim3(1), dim3(1), 0, s, d);
 }
 // the other tiles' messages: their owned cells' outcomes (pellet and blob kills,
 // new masses), their final cells, and the totals (thread 0)
 // box_recs: records per inbox slot (the pass's message size); bitmaps only when
 // the messages carry them (box_recs covers them)
-// (first: the messages carry the observation-history hand-off slots instead of bitmaps)
+// One block per source tile k (first: the messages carry the observation-
+// history hand-off slots instead of bitmaps); the block of this tile's own
+// message sums the headers.
 __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int first) {
-  const int T = d.ntiles, nrec = T * d.tcap, nbm = first ? 0 : T * d.bm_words;
-  int gi = GTID;
+  const int T = d.ntiles, k = blockIdx.x, tid = threadIdx.x;
   ArenaCtl &c = d.ctl[0];
-  if (gi == 0) {
-    int kills = 0, und = 0;
-    for (int k = 0; k < T; k++) {
-      const TileRec &h = d.inbox[(size_t)k * box_recs];
-      kills += (int)h.x;
-      und += (int)h.seq;
+  const TileRec *box = d.inbox + (size_t)k * box_recs;
+  if (k == d.tile_id) {
+    if (tid == 0) {
+      int kills = 0, und = 0;
+      for (int t = 0; t < T; t++) {
+        const TileRec &h = d.inbox[(size_t)t * box_recs];
+        kills += (int)h.x;
+        und += (int)h.seq;
+      }
+      c.n_eaten_glob += kills;
+      c.n_undone_glob = und;
+      if (first) c.n_ho = 0;  // (the header holds this tick's hand-off count; the next plan counts afresh)
     }
-    c.n_eaten_glob += kills;
-    c.n_undone_glob = und;
+    return;
   }
-  if (gi < nrec) {
-    const int k = gi / d.tcap, i = gi - k * d.tcap;
-    const TileRec *box = d.inbox + (size_t)k * box_recs;
-    if (k == d.tile_id || i >= box[0].idx) return;
+  const int nrec = min(box[0].idx, d.tcap);
+  for (int i = tid; i < nrec; i += blockDim.x) {
     const TileRec r = box[1 + i];
     if (r.kind == TR_PELLET) {
       const int bx = center_bucket_coord(r.x, d.cols), by = center_bucket_coord(r.y, d.cols);
-      if (!tile_holds_bucket(d, bx, by)) return;
+      if (!tile_holds_bucket(d, bx, by)) continue;
       const Food F(d, 0);
       const int b = by * d.cols + bx, lo = min(d.pstart[b], F.n0), hi = min(d.pstart[b + 1], F.n0);
-      for (int t = lo; t < hi; t++)
+      bool found = false;
+      for (int t = lo; t < hi && !found; t++)
         if (d.pel[F.pb][F.g(t)].seq == r.seq) {
           uint8_t *pd = d.pel_dead + F.g(t);  // (flag set through its 32-bit word: the first setter notes the kill)
           unsigned *w = (unsigned *)((uintptr_t)pd & ~(uintptr_t)3);
           const unsigned sh = (unsigned)((uintptr_t)pd & 3) * 8;
           if (!((atomicOr(w, 1u << sh) >> sh) & 0xFFu)) note_kill(d, 0, t);
-          return;
+          found = true;
         }
-      for (int j = F.n0; j < F.n0 + F.nst; j++)  // this tick's blob conversions (staged)
+      for (int j = F.n0; j < F.n0 + F.nst && !found; j++)  // this tick's blob conversions (staged)
         if (d.pn[F.gs(j)].seq == r.seq) {
           d.pel_dead[F.g(j)] = 1;
-          return;
+          found = true;
         }
-      set_err(d, 0, ERR_TILE_LOOKUP);
+      if (!found) set_err(d, 0, ERR_TILE_LOOKUP);
     } else if (r.kind == TR_BLOB) {
-      if (d.b_seq[r.idx] != r.seq) return set_err(d, 0, ERR_TILE_LOOKUP);
+      if (d.b_seq[r.idx] != r.seq) {
+        set_err(d, 0, ERR_TILE_LOOKUP);
+        continue;
+      }
       d.b_flags[r.idx] = 0;
       atomicOr(&c.dirty, DIRTY_BLOB);
     } else if (r.kind == TR_CELL) {
-      if (d.c_seq[r.idx] != r.seq) return set_err(d, 0, ERR_TILE_LOOKUP);
+      if (d.c_seq[r.idx] != r.seq) {
+        set_err(d, 0, ERR_TILE_LOOKUP);
+        continue;
+      }
       d.c_m[r.idx] = r.x;
       d.c_r[r.idx] = r.y;
       d.f_done[r.idx] = 1;
       atomic_max_pos(&c.rmax_cell, r.y);
     }
-    return;
   }
-  gi -= nrec;
-  if (first) {  // hand-off slots: every tile takes the sender's history copy (k_tile_plan)
-    const int GG = d.G * d.G, per = d.nh * GG, slot_e = 1 + per, nho = T * d.hcap * slot_e;
-    if (gi >= nho) return;
-    const int k = gi / (d.hcap * slot_e), r = gi - k * d.hcap * slot_e, sl = r / slot_e, j = r - sl * slot_e;
-    const TileRec *box = d.inbox + (size_t)k * box_recs;
-    if (k == d.tile_id || sl >= (int)box[0].y) return;
-    const TileRec *slot = box + 1 + d.tcap + (size_t)sl * d.hrec;
-    const int gp = slot->idx;
-    if (slot->kind != TR_HIST || gp < 0 || gp >= d.NP) return set_err(d, 0, ERR_TILE_LOOKUP);
-    if (j == 0) {
-      d.o_lastfov[gp] = slot->x;
-    } else {
-      const int q = j - 1, g = q / GG, t = q - g * GG;
-      hist_grid(d, g)[(size_t)gp * GG + t] = ((const double *)(slot + 1))[q];
+  if (first) {  // hand-off slots: every tile takes the sender's history copy (tile_plan_thread)
+    const int GG = d.G * d.G, per = d.nh * GG, slot_e = 1 + per, ns = min((int)box[0].y, d.hcap);
+    for (int e = tid; e < ns * slot_e; e += blockDim.x) {
+      const int sl = e / slot_e, j = e - sl * slot_e;
+      const TileRec *slot = box + 1 + d.tcap + (size_t)sl * d.hrec;
+      const int gp = slot->idx;
+      if (slot->kind != TR_HIST || gp < 0 || gp >= d.NP) {
+        set_err(d, 0, ERR_TILE_LOOKUP);
+        continue;
+      }
+      if (j == 0) {
+        d.o_lastfov[gp] = slot->x;
+        d.t_holder[gp] = -1;  // every tile's copy is current again (as the sender's plan set)
+      } else {
+        const int q = j - 1, g = q / GG, t = q - g * GG;
+        hist_grid(d, g)[(size_t)gp * GG + t] = ((const double *)(slot + 1))[q];
+      }
     }
-    return;
-  }
-  if (gi < nbm) {
-    const int k = gi / d.bm_words, w = gi - k * d.bm_words;
-    if (k == d.tile_id) return;
-    unsigned long long b = ((const unsigned long long *)(d.inbox + (size_t)k * box_recs + 1 + d.tcap))[w];
-    while (b) {
-      const int t = __ffsll((long long)b) - 1;
-      b &= b - 1;
-      d.f_done[(size_t)w * 64 + t] = 1;
+  } else {  // the sender's owned cells now final
+    const unsigned long long *bmw = (const unsigned long long *)(box + 1 + d.tcap);
+    for (int w = tid; w < d.bm_words; w += blockDim.x) {
+      unsigned long long b = bmw[w];
+      while (b) {
+        const int t = __ffsll((long long)b) - 1;
+        b &= b - 1;
+        d.f_done[(size_t)w * 64 + t] = 1;
+      }
     }
   }
 }
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first) {
-  const long extra = first ? (long)d.hcap * (1 + d.nh * d.G * d.G) : d.bm_words;
-  const long n = (long)d.ntiles * (d.tcap + extra);
-  hipLaunchKernelGGL(k_tile_apply, dim3(nblk(n, 256)), dim3(256), 0, s, d, box_recs, first);
+  hipLaunchKernelGGL(k_tile_apply, dim3(d.ntiles), dim3(256), 0, s, d, box_recs, first);
 }
 
 // Field.initialize()/reset() (field.py:57-83): players first (seq 0..B-1, empty

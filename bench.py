@@ -290,7 +290,10 @@ def c4_leg(args, name, rank, world, local, seed, dist, backend):
     import torch
     from aigar_amd import _lib, tiles
     tx, ty = tiles.tile_grid(world)
-    cfg = tiles.tile_config(make_cfg(name, device=local, arenas=1), tx, ty, rank)
+    # 512 records per message (the random population's owned outcomes per tick and tile are
+    # a few dozen; an overflow is a device error, not a silent loss) and 16 hand-off slots:
+    # a 48 KB first-pass message per tile
+    cfg = tiles.tile_config(make_cfg(name, device=local, arenas=1), tx, ty, rank, cap=512)
     stp = _lib.Stepper(cfg)
     tr = tiles.TorchTransport.for_stepper(stp, staged=(backend != "nccl"))
     bots, field, pellets, virus, ps, pe, ch, ex, _ = WORKLOADS[name]

@@ -30,7 +30,7 @@ def main():
     tx, ty = tiles.tile_grid(n)
     cfg = bench.make_cfg("c3")
     bots, field, pellets, virus, ps, pe, ch, ex, _ = bench.WORKLOADS["c3"]
-    ts = [_lib.Stepper(tiles.tile_config(cfg, tx, ty, k)) for k in range(n)]
+    ts = [_lib.Stepper(tiles.tile_config(cfg, tx, ty, k, cap=512)) for k in range(n)]  # (bench.py's C4 message)
     for t in ts:
         bench.start_world(t, "c3", 1, 1)
     obs = [torch.empty((bots, t.obs_len), dtype=torch.float64, device="cuda") for t in ts]
