@@ -96,6 +96,10 @@ struct aigar_handle {
   hipGraphExec_t graph = nullptr;
   hipStream_t cap_stream = nullptr;  // private stream graphs are captured on (the caller's may be the null stream)
   bool use_graph = true;  // AIGAR_NO_GRAPH=1 disables (direct launches)
+  // C4 tile phases as graphs (AIGAR_TILE_GRAPH=1): measured no faster than direct
+  // launches on a tile's own GPU (tools/c4_tile_timing.py), and slower in the
+  // 1-GPU gloo rehearsal, so off by default
+  bool tile_graph = false;
   bool graph_failed = false;
   // aigar_run: one whole env step (policy + Field.update + observation) as a graph
   hipGraphExec_t run_graph = nullptr;
@@ -209,6 +213,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   aigar_handle *h = new aigar_handle();
   h->cfg = *cfg;
   if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
+  if (getenv("AIGAR_TILE_GRAPH")) h->tile_graph = true;
   // tuning knob; >= 2: the player-cell grid counts ride on round 1, its scatter on round 2
   if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(2, std::min(16, atoi(r)));
   Dev &d = h->d;
@@ -605,7 +610,7 @@ extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
   };
   const bool same = h->tb_graph && memcmp(&h->tb_key, p, sizeof *p) == 0 && h->tb_box[0] == h->d.outbox &&
                     h->tb_box[1] == h->d.inbox;
-  if (h->use_graph && !same) {
+  if (h->tile_graph && !same) {
     if (h->tb_graph) (void)hipGraphExecDestroy(h->tb_graph);
     h->tb_graph = capture_graph(h, issue);
     h->tb_key = *p;
@@ -614,7 +619,7 @@ extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
   }
   {
     Mark m(h, "tile_begin");
-    if (h->use_graph && h->tb_graph) HIPCHK(hipGraphLaunch(h->tb_graph, h->stream));
+    if (h->tile_graph && h->tb_graph) HIPCHK(hipGraphLaunch(h->tb_graph, h->stream));
     else issue(h->stream);
   }
   h->pass_recs = 1 + h->d.tcap + h->d.hcap * h->d.hrec;  // (+ the observation-history hand-off slots)
@@ -653,7 +658,7 @@ extern "C" int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype) {
   if (need_tiled(h)) return -1;
   if (obs_out && dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
   HIPCHK(hipSetDevice(h->cfg.device));
-  if (h->profile) {  // separate launches: the post phases and the observation timed apart
+  if (h->profile || !h->tile_graph) {  // separate launches (the post phases and the observation timed apart)
     {
       Mark m(h, "tile_end");
       launch_tick_post(h->d, h->stream, h->scr_k, h->scr_v);
