@@ -22,6 +22,7 @@ namespace aigar {
 struct ArenaCtl {
   int64_t seq_next;  // next Cell creation sequence number
   int64_t tick;      // completed Field.update() calls since reset
+  int64_t tick_sp;   // the tick spawnStuff runs in (k_pel_update advances tick beside its respawns)
   uint64_t key0, key1, ctr_pellet, ctr_virus;
   int64_t seq_base_upd;  // seq_next before updatePlayers' creations (this tick)
   int64_t seq_base_spawn;
@@ -202,7 +203,7 @@ struct Dev {
   uint8_t *f_cnt;
   uint8_t *f_done;
   // spawn staging
-  int *respawn_list;  // [NP]
+  int *resp_slot;  // [NP] a dead player's place in this tick's respawn order, -1 = waits
   // events [A*EVcap][5]: key_hi, key_lo, code, a, b
   int64_t *ev;
   // observation state

@@ -336,7 +336,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(occ, unsigned long long, A * d.occ_words); AL(occ_cnt, int, A * d.H);
   AL(dead, int, NP); AL(work, int, A * d.Wcap); AL(work2, int, A * d.Wcap);
   AL(f_list, int, C * FCAP); AL(f_cnt, uint8_t, C); AL(f_done, uint8_t, C);
-  AL(respawn_list, int, NP);
+  AL(resp_slot, int, NP);
   AL(ev, int64_t, A * d.EVcap * 5);
   AL(o_lastfov, double, NP); AL(o_self_lf, double, NP * GG); AL(o_self_slf, double, NP * GG);
   AL(o_en_lf, double, NP * GG); AL(o_en_slf, double, NP * GG); AL(o_act_cur, double, NP * 4);

@@ -184,7 +184,8 @@ __device__ __forceinline__ void tile_out(const Dev &d, int32_t kind, int32_t idx
   r.y = y;
 }
 
-__device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int code, int64_t x, int64_t y) {
+__device__ void ev_push_at(const Dev &d, int a, int64_t tick, uint32_t phase, uint64_t order, int code, int64_t x,
+                           int64_t y) {
   if (!(d.flags & 1)) return;
   // tiles: the replicated phases are logged by tile 0, the eat phases by the cell's owner
   if (d.tiled && d.tile_id != 0 && phase != PH_PELLET && phase != PH_BLOB) return;
@@ -194,11 +195,14 @@ __device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int
     return;
   }
   int64_t *e = d.ev + ((size_t)a * d.EVcap + i) * 5;
-  e[0] = (d.ctl[a].tick << 8) | phase;
+  e[0] = (tick << 8) | phase;
   e[1] = (int64_t)order;
   e[2] = code;
   e[3] = x;
   e[4] = y;
+}
+__device__ void ev_push(const Dev &d, int a, uint32_t phase, uint64_t order, int code, int64_t x, int64_t y) {
+  ev_push_at(d, a, d.ctl[a].tick, phase, order, code, x, y);
 }
 
 // centre-bucket grid iteration: every entity whose centre bucket lies in the
@@ -1023,13 +1027,16 @@ __device__ void cgrid_count_block(const Dev &d, int a, int bx) {
   const bool in = i < per;
   const int slot = in ? i / d.B : 0, p = in ? i - slot * d.B : 0;
   const size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-  const bool ok = in && (d.c_flags[g] & F_ALIVE);
+  // (the slot's position and radius load beside its flags: one round of loads)
   double x = 0, y = 0, r = 0;
-  if (ok) {
+  uint32_t fl = 0;
+  if (in) {
+    fl = d.c_flags[g];
     x = d.c_x[g];
     y = d.c_y[g];
     r = d.c_r[g];
   }
+  const bool ok = in && (fl & F_ALIVE);
   wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? r : 0.0);
   if (!ok) return;
   d.c_rank[(size_t)a * per + i] = atomicAdd(&cgrid_counts(d, a, par)[cgrid_bucket(d, x, y)], 1);
@@ -1044,14 +1051,16 @@ __device__ void cgrid_scatter_block(const Dev &d, int a, int bx) {
   const bool in = i < per;
   const int slot = in ? i / d.B : 0, p = in ? i - slot * d.B : 0;
   const size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-  bool ok = in && (d.c_flags[g] & F_ALIVE);
   double x = 0, y = 0;
   int rk = 0;
-  if (ok) {
+  uint32_t fl = 0;
+  if (in) {
+    fl = d.c_flags[g];
     x = d.c_x[g];
     y = d.c_y[g];
     rk = d.c_rank[(size_t)a * per + i];
   }
+  const bool ok = in && (fl & F_ALIVE);
   // exclusive scan of the <= 4096 counts: 16 per thread (4 aligned int4 loads)
   const int4 *c4 = reinterpret_cast<const int4 *>(cgrid_counts(d, a, d.ctl[a].tick & 1));
   int v[16], sum = 0;
@@ -1264,8 +1273,8 @@ __device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
   }
   d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + by * d.cols + bx], 1);
 }
-// mode PR_RESET: staging -> buffer 0 (the closing rebuild of a tick takes its
-// counts in k_spawn_all)
+// mode PR_RESET: staging -> buffer 0 (Field.initialize; a tick closes through
+// k_spawn_plan + k_pel_update instead)
 __global__ void k_pgrid_count(Dev d, int mode) {
   const int gi = GTID;
   const int per = d.H + d.Pcap;
@@ -2833,7 +2842,7 @@ __device__ __forceinline__ int64_t wave_sort_i64(int64_t v) {
 // closes here (the update reads pu_*): new count, staging emptied, the buffer
 // the update builds made current.  A usual tick (<= 64 staged, <= 64 kills)
 // only hands over pu_*: k_pel_update's blocks sort the short lists themselves.  The tick counter advances in k_pel_update
-// (k_spawn_all's respawns and events still key on it).  lds: 4096 free int64.
+// (its respawn threads key on tick_sp).  lds: 4096 free int64.
 constexpr int PU_LDS = 4096;
 constexpr int PU_SH = 2048;  // k_pel_update: kill / staged lists up to this length sit in LDS
 __device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
@@ -3096,11 +3105,13 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   // (the spawn occupancy is built by k_pp_active and kept by the pp pass above)
   // spawnPlayers' dead list (deadPlayers in order; respawnTime == 0 respawns):
   // partitioned by the whole block, a chunk of T players per round (a serial
-  // loop was one load chain per dead player: ~8 us per greedy tick)
+  // loop was one load chain per dead player: ~8 us per greedy tick); every dead
+  // player's respawn slot (its place in the respawn order, -1 = waits) is
+  // what k_pel_update's player threads read
   int n_resp = 0, n_wait = 0;
   if (!init) {
     const int nd = c.n_dead;
-    int *dl = d.dead + (size_t)a * d.B, *rl = d.respawn_list + (size_t)a * d.B;
+    int *dl = d.dead + (size_t)a * d.B, *rl = d.resp_slot + (size_t)a * d.B;
     for (int base = 0; base < nd; base += T) {
       const int i = base + tid;
       int p = -1;
@@ -3112,7 +3123,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
       int tr, tw;
       const int rr = block_rank(i < nd && rsp, sflag, &tr);
       const int rw = block_rank(i < nd && !rsp, sflag, &tw);  // (every read of this chunk is done)
-      if (i < nd && rsp) rl[n_resp + rr] = p;
+      if (i < nd) rl[p] = rsp ? n_resp + rr : -1;
       if (i < nd && !rsp) dl[n_wait + rw] = p;  // (n_wait + rw <= i: never ahead of an unread entry)
       n_resp += tr;
       n_wait += tw;
@@ -3165,14 +3176,12 @@ __device__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wa
   c.vir_base_spawn = c.n_vir;
   c.n_spawn_v = kv;
   c.n_vir += kv;
-  // spawnPlayers: deadPlayers in order, respawnTime == 0
-  int np = 0;
-  int *rl = d.respawn_list + (size_t)a * d.B;
-  if (init) {
-    for (int p = 0; p < d.B; p++) rl[np++] = p;
-  } else {
+  // spawnPlayers: deadPlayers in order, respawnTime == 0 (init: every player, in order)
+  int np = d.B;
+  if (!init) {
     np = n_resp;
     c.n_dead = n_wait;
+    c.tick_sp = c.tick;
   }
   c.n_spawn_pl = np;
   if (!init) c.seq_next += np;  // at initialize() players already own seqs 0..B-1
@@ -3253,17 +3262,14 @@ __device__ __forceinline__ void spawn_virus(const Dev &d, int gi) {
   d.v_flags[o] = F_ALIVE;  // addVirus: not hashed until the next rebuild
 }
 __global__ void k_spawn_viruses(Dev d) { spawn_virus(d, GTID); }
-__device__ __forceinline__ void spawn_player(const Dev &d, int gi, int init) {
-  if (gi >= d.NP) return;
-  int a = gi / d.B, j = gi - a * d.B;
+// player gp (= arena a's player p) spawns j-th in spawnPlayers' order
+__device__ __forceinline__ void spawn_player(const Dev &d, int gp, int j, int init) {
+  const int a = gp / d.B, p = gp - a * d.B;
   ArenaCtl &c = d.ctl[a];
-  if (j >= c.n_spawn_pl) return;
-  int p = d.respawn_list[(size_t)a * d.B + j];
-  int gp = a * d.B + p;
   const int NP = d.NP;
   uint64_t u[4];
   if (init) philox((uint64_t)p, ST_INIT_PLAYER, 0, 0, c.key0, c.key1, u);
-  else philox((uint64_t)p, ST_PLAYER, (uint64_t)c.tick, 0, c.key0, c.key1, u);
+  else philox((uint64_t)p, ST_PLAYER, (uint64_t)c.tick_sp, 0, c.key0, c.key1, u);
   const double sr = radius_of(kStartMass);
   double x, y;
   spawn_pos(d, a, sr, u, x, y);
@@ -3287,12 +3293,27 @@ __device__ __forceinline__ void spawn_player(const Dev &d, int gi, int init) {
   d.p_ncells[gp] = 1;
   d.p_alive[gp] = 1;
   d.p_respawn[gp] = 0;
-  if (!init) ev_push(d, a, PH_SPAWN, (uint64_t)j, 10, p, seq);
+  if (!init) ev_push_at(d, a, c.tick_sp, PH_SPAWN, (uint64_t)j, 10, p, seq);
 }
-__global__ void k_spawn_players(Dev d, int init) { spawn_player(d, GTID, init); }
+__global__ void k_spawn_players(Dev d, int init) {  // Field.initialize: every player, in order
+  const int gp = GTID;
+  if (gp < d.NP) spawn_player(d, gp, gp % d.B, init);
+}
+// the end of spawnStuff for live-or-dead player gp: a dead player whose respawn
+// slot k_spawn_plan set respawns, then the FOV cache of the end-of-tick state
+// (one thread per player, so the respawn and its cache need no ordering)
+__device__ __forceinline__ void respawn_fov_thread(const Dev &d, int gp) {
+  if (gp < d.NP && !d.p_alive[gp]) {
+    const int j = d.resp_slot[gp];
+    if (j >= 0) spawn_player(d, gp, j, 0);
+  }
+  fov_cache_thread(d, gp);
+}
 
 // step 2 of the closing pellet update (see pellet_close_prep): blocks
-// [arena][pellet blocks | bucket blocks] + the FOV cache as extra blocks.  A
+// [arena][pellet blocks | bucket blocks] + extra blocks for the rest of
+// spawnStuff, which reads nothing this launch writes: the player respawns with
+// the FOV cache (respawn_fov_thread), then the virus spawns.  A
 // pellet thread moves one buffer record (or drops an eaten one and clears its
 // flag); a bucket thread rewrites its bucket's start and count and moves its
 // staged records behind the survivors.  Every thread issues its own loads
@@ -3468,12 +3489,13 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
   d.pstart[(size_t)a * (d.H + 1) + i] = start;
   d.pbc[(size_t)a * d.H + i] = surv + nb;
 }
-__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
+__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int nbF) {
   __shared__ int s_kill[PU_SH];
   __shared__ int64_t s_stg[PU_SH];
   __shared__ int s_n[2];
   const int per = nbP + nbB, nup = d.A * per;
-  if ((int)blockIdx.x >= nup) return fov_cache_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
+  if ((int)blockIdx.x >= nup + nbF) return spawn_virus(d, (blockIdx.x - nup - nbF) * 256 + threadIdx.x);
+  if ((int)blockIdx.x >= nup) return respawn_fov_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
   const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int mode = c.pu_small, n0 = c.pu_n0, nconv = c.pu_nconv;
@@ -3571,36 +3593,6 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB) {
   }
 }
 
-// spawnStuff (field.py:256-313) in one launch, thread ranges [players | pellets
-// | viruses | pellet buckets]: the three spawn lists are independent (their
-// counts and sequence bases come from k_spawn_plan), and the survivor counts of
-// the closing pellet rebuild only read the eat-phase buffer.
-// inc (the tick): the pellets are spawned and joined by the closing update
-// (k_spawn_plan, k_pel_update): only players and viruses here
-__global__ void __launch_bounds__(256) k_spawn_all(Dev d, int inc) {
-  int gi = GTID;
-  if (gi < d.NP) return spawn_player(d, gi, 0);
-  gi -= d.NP;
-  if (inc) {
-    if (d.virus_enabled && gi < d.A * d.Vcap) spawn_virus(d, gi);
-    return;
-  }
-  if (gi < d.A * d.Pcap) {
-    const int a = gi / d.Pcap, j = gi - a * d.Pcap;
-    const ArenaCtl &c = d.ctl[a];
-    // blob conversions that survived the eat phase join the closing rebuild
-    if (j < c.n_pnew && !d.pel_dead[(size_t)a * d.Pcap + c.n_pel + j]) pgrid_rank_staged(d, a, j);
-    return spawn_pellet(d, gi, true);
-  }
-  gi -= d.A * d.Pcap;
-  if (d.virus_enabled) {
-    if (gi < d.A * d.Vcap) return spawn_virus(d, gi);
-    gi -= d.A * d.Vcap;
-  }
-  if (gi < d.A * d.H) pgrid_count_bucket(d, gi / d.H, gi % d.H, 1);
-}
-
-
 // ------------------------------------------------------------ init helpers
 __global__ void k_init_ctl(Dev d, uint64_t seed) {
   int a = GTID;
@@ -3641,7 +3633,7 @@ struct Scratch {
   int *v;
 };
 
-// counts (PR_CLOSE: already taken by k_spawn_all) -> scan (+ epilogue) -> scatter
+// counts -> scan (+ epilogue) -> scatter
 void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
   long nc = (long)d.A * (d.H + d.Pcap), ns = (long)d.A * 2 * d.Pcap;
   if (mode != PR_CLOSE) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, mode);
@@ -3699,14 +3691,13 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   // grid + the closing pellet update's sorted kill / join lists (and the pellet spawns)
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, 0, scr_k,
                      scr_v, 1, 1);
-  const long n_spawn = (long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0);
-  hipLaunchKernelGGL(k_spawn_all, dim3(nblk(n_spawn, 256)), dim3(256), 0, s, d, 1);  // players, viruses
   // the closing pellet update (survivors U joining staged records -> the new
-  // current buffer, the last block closes the tick); the FOV cache runs as extra
-  // blocks (player state is final by then: fused into the pellet threads it
-  // stretched the kernel, as separate blocks it only adds them to the grid)
-  const int nbP = nblk(d.Pcap, 256), nbB = nblk(d.H, 256);
-  hipLaunchKernelGGL(k_pel_update, dim3(d.A * (nbP + nbB) + nblk(d.NP, 256)), dim3(256), 0, s, d, nbP, nbB);
+  // current buffer) + the rest of spawnStuff as extra blocks: player respawns
+  // with the FOV cache, virus spawns (fused into the pellet threads the FOV
+  // cache stretched the kernel; as separate blocks they only add to the grid)
+  const int nbP = nblk(d.Pcap, 256), nbB = nblk(d.H, 256), nbF = nblk(d.NP, 256);
+  const int nbV = d.virus_enabled ? nblk((long)d.A * d.Vcap, 256) : 0;
+  hipLaunchKernelGGL(k_pel_update, dim3(d.A * (nbP + nbB) + nbF + nbV), dim3(256), 0, s, d, nbP, nbB, nbF);
 }
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   launch_tick_pre(d, s, scr_k, scr_v, rp);
