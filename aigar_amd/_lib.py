@@ -398,7 +398,8 @@ class Stepper:
             p = C.c_void_p(out.data_ptr())
         self._chk(self.L.aigar_tile_end(self.h, p, dt))
 
-    COUNTERS = ("vb_serial", "pv_serial", "food_serial", "pellets_eaten", "pp_serial_players", "pellets_spawned", "-",
+    COUNTERS = ("vb_serial", "pv_serial", "food_serial", "pellets_eaten", "pp_serial_players", "pellets_spawned",
+                "pp_parallel_ticks",
                 "ticks")
 
     def counters(self, arena=0):

@@ -143,6 +143,7 @@ struct Dev {
   int G, L;
   uint32_t obs_ch, obs_ex;
   int flags;
+  int pp_par;  // playerPlayerOverlap may run as independent groups (pp_pass; AIGAR_PP_SERIAL=1: never)
   ArenaCtl *ctl;
   // players [NP]
   int *p_alive, *p_respawn, *p_ncells, *p_split, *p_eject, *p_pend;

@@ -214,6 +214,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   h->cfg = *cfg;
   if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
   if (getenv("AIGAR_TILE_GRAPH")) h->tile_graph = true;
+  h->d.pp_par = getenv("AIGAR_PP_SERIAL") ? 0 : 1;
   // tuning knob; >= 2: the player-cell grid counts ride on round 1, its scatter on round 2
   if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(2, std::min(16, atoi(r)));
   Dev &d = h->d;

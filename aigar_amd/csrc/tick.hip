@@ -112,7 +112,7 @@ __device__ __forceinline__ void set_err(const Dev &d, int a, uint32_t bit) { ato
 constexpr int SG_CAP = 4096;           // cells of a coarse grid (small entity sets, player cells)
 constexpr int CG_STRIDE = SG_CAP + 4;  // per-arena, per-parity stride of Dev::cgcnt (16-byte aligned rows)
 template <int KIND>
-__device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh);
+__device__ __forceinline__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh);
 
 // Last-block ticket (cdna_hip_programming.md, the in-launch reduction recipe):
 // each of the nblocks participating blocks publishes its writes (every wave's
@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
 
 // rank of this thread among the flagged threads of the block (thread order);
 // *total = number flagged.  Ballot per wave + one pass over <= 16 wave counts.
-__device__ int block_rank(bool flag, int *sh, int *total) {
+__device__ __forceinline__ int block_rank(bool flag, int *sh, int *total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   unsigned long long b = __ballot(flag);
   int before = __popcll(b & ((1ull << lane) - 1));
@@ -934,7 +934,7 @@ __device__ __forceinline__ int block_excl_1024(int x, int *wsum, int *total) {
 // block scan, coalesced start[] store, scatter.  The virus grid also sets the
 // radius bound and the lightest mass (the block is their only writer then).
 template <int KIND>
-__device__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
+__device__ __forceinline__ void grid_small_build(const Dev &d, int a, int *cnt, int *sh) {
   __shared__ double vmin_w[32];  // per wave (<= 16): lightest mass, then largest radius
   const int tid = threadIdx.x, T = blockDim.x, s = d.cshift;
   const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
@@ -2431,7 +2431,7 @@ __device__ __forceinline__ void occ_grow_def(const Dev &d, int a, Rect old, Rect
 }
 // every wave of the block: the k-th dirty word goes to wave k % waves; its 64
 // counts are read at device scope (past L1) and the word is their ballot
-__device__ void occ_rebuild_dirty(const Dev &d, int a, const uint32_t *dirty) {
+__device__ __forceinline__ void occ_rebuild_dirty(const Dev &d, int a, const uint32_t *dirty) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   int *cnt = d.occ_cnt + (size_t)a * d.H;
   unsigned long long *occ = d.occ + (size_t)a * d.occ_words;
@@ -2503,7 +2503,10 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
 }
 
 // removes cell e (pool index) from its player's list; returns true if the player died
-__device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool writer = true) {
+// (dkey: a parallel pp group -- the death takes a dead-list slot by atomic and
+// records its turn key there, for the sort into turn order after the pass)
+__device__ __forceinline__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool writer = true,
+                            int64_t *dkey = nullptr, int n_dead0 = 0) {
   const int NP = d.NP;
   int gp = (int)(e % NP);
   uint8_t slot = (uint8_t)(e / NP);
@@ -2523,7 +2526,17 @@ __device__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool
     ArenaCtl &c = d.ctl[a];
     d.p_alive[gp] = 0;
     d.p_respawn[gp] = 1;
-    d.dead[(size_t)a * d.B + c.n_dead++] = gp - a * d.B;
+    if (dkey) {
+      int sl = 0;
+      if ((threadIdx.x & 63) == 0) sl = atomicAdd(&c.n_dead, 1);
+      sl = __shfl(sl, 0);
+      if ((threadIdx.x & 63) == 0) {
+        d.dead[(size_t)a * d.B + sl] = gp - a * d.B;
+        dkey[sl - n_dead0] = (int64_t)order;
+      }
+    } else {
+      d.dead[(size_t)a * d.B + c.n_dead++] = gp - a * d.B;
+    }
     if (writer) ev_push(d, a, PH_PP, order, 9, gp - a * d.B, d.c_seq[e]);
     order++;
     return true;
@@ -2545,38 +2558,30 @@ __device__ __forceinline__ void active_st(const Dev &d, size_t i, uint8_t v) {
 // stores, so program order alone orders them -- while the grid queries
 // (candidate gathering, re-activation after growth) are spread over the lanes.
 // Cross-lane data: the LDS candidate lists, the pending bitmap and c_active.
+// Event / death order keys are (player << 32 | step of its turn): turns run in
+// increasing player order, so the keys sort into the serial order whether the
+// turns ran in one wave or in independent groups (pp_pass).
 constexpr int PP_LCAP = 512;
+struct PPL {  // a turn's candidate lists (LDS) and their capacity
+  int64_t *key;
+  int *val, *srt;
+  double *x, *y, *m, *r;
+  int cap;
+};
 // odirty: the deferred occupancy's dirty-word bitmap (LDS, zeroed), or NULL for
-// immediate updates
-__device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend, uint32_t *odirty) {
-  // pend: pending-player bitmap (B bits, LDS)
-  // candidates of the current turn, with their state at turn start (only the
-  // turn's own cell changes them: what it eats dies, and it stops when eaten)
-  __shared__ int64_t s_key[PP_LCAP];
-  __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
-  __shared__ double s_x[PP_LCAP], s_y[PP_LCAP], s_m[PP_LCAP], s_r[PP_LCAP];
+// immediate updates; dkey / n_dead0: a parallel group (see remove_cell)
+__device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, const PPL &L, uint32_t *odirty, double &rmax,
+                         int64_t *dkey, int n_dead0) {
   const int lane = threadIdx.x & 63;
   PA_DECL;
-  ArenaCtl &c = d.ctl[a];
   const int B = d.B, NW = (B + 31) / 32;
-  const int nw = min(c.n_pend, d.Wcap);
-  for (int i = lane; i < NW; i += 64) pend[i] = 0;
-  wave_fence();
-  for (int i = lane; i < nw; i += 64) {
-    int p = d.work[(size_t)a * d.Wcap + i];
-    atomicOr(&pend[p >> 5], 1u << (p & 31));
-  }
-  wave_fence();
-  c.n_pend = 0;
-  c.stat[4] += nw;
-  c.stat[7] += 1;
-  if (nw == 0) return;
   const int NP = d.NP;
   const int *st = d.cstart + (size_t)a * (d.H + 1);
   const int *it = d.citems + (size_t)a * kMaxCells * B;
   const unsigned long long lt = (1ull << lane) - 1;
-  uint64_t order = 0;
-  double rmax = c.rmax_cell;
+  int64_t *s_key = L.key;
+  int *s_val = L.val, *s_srt = L.srt;
+  double *s_x = L.x, *s_y = L.y, *s_m = L.m, *s_r = L.r;
   PA_T(0);
   int P = -1;
   for (;;) {
@@ -2602,6 +2607,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
     if (lane == 0) pend[P >> 5] &= ~(1u << (P & 31));
     wave_fence();
     const int gp = a * B + P;
+    uint64_t order = (uint64_t)P << 32;  // this turn's event / death keys
     PA_C(0);
     // liveness, count and the list's first row in one load round
     const int s_first = d.p_list[gp];
@@ -2632,7 +2638,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         }
         unsigned long long bal = __ballot(keep);
         int slot = nc + __popcll(bal & lt);
-        if (keep && slot < PP_LCAP) {
+        if (keep && slot < L.cap) {
           s_key[slot] = d.c_seq[e];
           s_val[slot] = e;
           s_x[slot] = ex;
@@ -2642,9 +2648,9 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
         }
         nc += __popcll(bal);
       }, d.cshift_c);
-      if (nc > PP_LCAP) {
+      if (nc > L.cap) {
         set_err(d, a, ERR_CAND_CAP);
-        nc = PP_LCAP;
+        nc = L.cap;
       }
       PA_T(2);
       PA_C(1);
@@ -2697,7 +2703,7 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
           pr = mr;
         }
         rmax = fmax(rmax, mr);
-        remove_cell(d, a, v, order, lane == 0);
+        remove_cell(d, a, v, order, lane == 0, dkey, n_dead0);
         // re-activate every later turn whose outcome the growth of g may change
         const int gpl = (int)(g % NP);
         const double gx = pc_eats ? px : ox, gy = pc_eats ? py : oy, gm = m, gr = mr;
@@ -2743,8 +2749,253 @@ __device__ void pp_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, 
     }
   }
   PA_T(7);
-  PA_STORE(a);
+  if (!dkey) PA_STORE(a);
+}
+// the whole pass in one wavefront (nw pending players in d.work)
+__device__ __forceinline__ void pp_serial_body(const Dev &d, int a, uint32_t *pend, uint32_t *odirty, int nw) {
+  // candidates of the current turn, with their state at turn start (only the
+  // turn's own cell changes them: what it eats dies, and it stops when eaten)
+  __shared__ int64_t s_key[PP_LCAP];
+  __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
+  __shared__ double s_x[PP_LCAP], s_y[PP_LCAP], s_m[PP_LCAP], s_r[PP_LCAP];
+  const int lane = threadIdx.x & 63, NW = (d.B + 31) / 32;
+  for (int i = lane; i < NW; i += 64) pend[i] = 0;
+  wave_fence();
+  for (int i = lane; i < nw; i += 64) {
+    int p = d.work[(size_t)a * d.Wcap + i];
+    atomicOr(&pend[p >> 5], 1u << (p & 31));
+  }
+  wave_fence();
+  if (nw == 0) return;
+  ArenaCtl &c = d.ctl[a];
+  double rmax = c.rmax_cell;
+  pp_turns(d, a, pend, PPL{s_key, s_val, s_srt, s_x, s_y, s_m, s_r, PP_LCAP}, odirty, rmax, nullptr, 0);
   c.rmax_cell = rmax;
+}
+
+// ---- independent pp groups
+// A turn reads and changes only cells near the turning player's cells, but a
+// growth re-activates the partners of the grown cell, whose turns walk their
+// whole lists, and so on.  The closure of a seed player bounds that: no cell
+// of a group eats outside it, so no radius in it exceeds R = radius_of(min(cap,
+// group mass)) (or a cell's own, possibly stale, radius); every cell whose
+// footprint at max(its radius, R) meets the union U of the group cells'
+// footprints at R could be a candidate, a victim, an eater or a re-activated
+// partner, so its player joins -- with all its cells, which its turn walks --
+// and R, U are recomputed, to a fixed point.  Seeds whose closures share no
+// player commute: cells of two such groups never meet, so each group can run
+// its turns in its own wavefront, in player order, on the pass's state.  (A cell
+// of another group can only be read while a grid walk filters it out: its
+// footprint misses every footprint of this group, whatever its current radius.)
+#ifdef AIGAR_PP_DIAG  // diagnostics build: why the parallel pass fell back (tools/var/pp_diag.py)
+__device__ unsigned long long g_ppdiag[16];
+#define PP_DIAG(k) atomicAdd(&g_ppdiag[k], 1ull)
+extern "C" int aigar_debug_ppdiag(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ppdiag), sizeof(g_ppdiag)) == hipSuccess ? 0 : -1;
+}
+#else
+#define PP_DIAG(k)
+#endif
+constexpr int PPG_SEEDS = 64;  // most pending players for the parallel pass
+constexpr int PPG_PL = 16;     // players per closure
+constexpr int PPG_CELLS = 64;  // cells per closure (also the turn candidate cap)
+constexpr int PPG_WAVES = 8;   // wavefronts running groups
+constexpr int PPG_MIN = 3;     // fewer pending players: the serial pass (closures cost ~10 us)
+__device__ __forceinline__ bool pp_closure(const Dev &d, int a, int P, int *pl, int &npl) {
+  const int lane = threadIdx.x & 63, NP = d.NP, B = d.B;
+  const int *st = d.cstart + (size_t)a * (d.H + 1);
+  const int *it = d.citems + (size_t)a * kMaxCells * B;
+  const double rmax0 = d.ctl[a].rmax_cell;
+  if (lane == 0) pl[0] = P;
+  npl = 1;
+  wave_fence();
+  for (int iter = 0; iter < 8; iter++) {
+    // the group's cells: (player j, slot k) pairs, four per lane, one load round
+    uint32_t fl[4];
+    double cx[4], cy[4], cm[4], cr[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int pr = lane + 64 * k, j = pr >> 4;
+      fl[k] = 0;
+      cx[k] = cy[k] = cm[k] = cr[k] = 0;
+      if (j < npl) {
+        const size_t ci = (size_t)(pr & 15) * NP + (size_t)a * B + pl[j];
+        fl[k] = d.c_flags[ci];
+        cx[k] = d.c_x[ci];
+        cy[k] = d.c_y[ci];
+        cm[k] = d.c_m[ci];
+        cr[k] = d.c_r[ci];
+      }
+    }
+    double M = 0, rr = 0;
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (fl[k] & F_ALIVE) {
+        M += cm[k];
+        rr = fmax(rr, cr[k]);
+        n++;
+      }
+    M = wave_sum(M);
+    for (int o = 32; o > 0; o >>= 1) {
+      rr = fmax(rr, __shfl_xor(rr, o));
+      n += __shfl_xor(n, o);
+    }
+    if (n > PPG_CELLS) {
+      if (lane == 0) PP_DIAG(3);
+      return false;
+    }
+    const double R = fmax(radius_of(py_min(kMaxMass, M)), rr) * (1 + 1e-9) + 1e-9;
+    Rect U{INT_MAX, -1, INT_MAX, -1};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (fl[k] & F_ALIVE) {
+        const Rect q = footprint(cx[k], cy[k], R, d.size);
+        U.x0 = min(U.x0, q.x0);
+        U.x1 = max(U.x1, q.x1);
+        U.y0 = min(U.y0, q.y0);
+        U.y1 = max(U.y1, q.y1);
+      }
+    for (int o = 32; o > 0; o >>= 1) {
+      U.x0 = min(U.x0, __shfl_xor(U.x0, o));
+      U.x1 = max(U.x1, __shfl_xor(U.x1, o));
+      U.y0 = min(U.y0, __shfl_xor(U.y0, o));
+      U.y1 = max(U.y1, __shfl_xor(U.y1, o));
+    }
+    bool added = false;
+    wave_grid_for(st, it, d.cols, U, expand_for(fmax(rmax0, R)), [&](bool valid, int e) {
+      int q = -1;
+      if (valid && (d.c_flags[e] & F_ALIVE) &&
+          rect_hit(footprint(d.c_x[e], d.c_y[e], fmax(d.c_r[e], R), d.size), U)) {
+        q = e % NP - a * B;
+        for (int j = 0; j < min(npl, PPG_PL) && q >= 0; j++)
+          if (pl[j] == q) q = -1;  // already in
+      }
+      unsigned long long nb = __ballot(q >= 0);
+      while (nb) {  // new players, deduplicated in lane order
+        const int l = __ffsll((long long)nb) - 1;
+        nb &= nb - 1;
+        const int qq = __builtin_amdgcn_readlane(q, l);
+        bool dup = false;
+        for (int j = 0; j < min(npl, PPG_PL); j++) dup |= pl[j] == qq;
+        if (dup) continue;
+        if (npl < PPG_PL && lane == 0) pl[npl] = qq;
+        npl++;
+        added = true;
+        wave_fence();
+      }
+    }, d.cshift_c);
+    if (npl > PPG_PL) {
+      if (lane == 0) PP_DIAG(2);
+      return false;
+    }
+    if (!added) {
+      if (lane == 0) PP_DIAG(8 + min(npl, 7));
+      return true;
+    }
+  }
+  if (lane == 0) PP_DIAG(4);
+  return false;
+}
+// playerPlayerOverlap for the block: the serial pass in wave 0, or -- with at
+// least PPG_MIN pending players whose closures are pairwise disjoint -- one
+// group per seed, PPG_WAVES wavefronts each running its seeds' turns (their
+// pending bits together: disjoint groups interleave freely), then the pass's
+// deaths sorted into turn order by their keys.  Called by every thread.
+__device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend, uint32_t *odirty) {
+  __shared__ int s_nw, s_dead0, s_bad;
+  __shared__ int s_pl[PPG_SEEDS][PPG_PL], s_npl[PPG_SEEDS];
+  __shared__ double s_rmax[PPG_WAVES];
+  __shared__ int64_t g_key[PPG_WAVES][PPG_CELLS];
+  __shared__ int g_val[PPG_WAVES][PPG_CELLS], g_srt[PPG_WAVES][PPG_CELLS];
+  __shared__ double g_x[PPG_WAVES][PPG_CELLS], g_y[PPG_WAVES][PPG_CELLS], g_m[PPG_WAVES][PPG_CELLS],
+      g_r[PPG_WAVES][PPG_CELLS];
+  ArenaCtl &c = d.ctl[a];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nwv = blockDim.x >> 6, T = blockDim.x;
+  if (tid == 0) {  // (every thread reads the count before it is reset)
+    s_nw = min(c.n_pend, d.Wcap);
+    s_dead0 = c.n_dead;
+    s_bad = 0;
+    c.n_pend = 0;
+    c.stat[4] += s_nw;
+    c.stat[7] += 1;
+  }
+  __syncthreads();
+  const int nw = s_nw, dead0 = s_dead0;
+  const bool par = d.pp_par && odirty && nw >= PPG_MIN && nw <= PPG_SEEDS && nwv >= PPG_WAVES;
+  if (!par) {
+    if (tid == 0 && nw > 0) PP_DIAG(nw < PPG_MIN ? 0 : 1);
+    if (tid < 64) pp_serial_body(d, a, pend, odirty, nw);
+    return;
+  }
+  // closures; per player the lowest seed whose closure holds it
+  int *pown = scr_v + (size_t)a * d.Wcap;
+  for (int i = tid; i < d.B; i += T) __hip_atomic_store(&pown[i], INT_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int sd = w; sd < nw; sd += nwv) {
+    const int P = d.work[(size_t)a * d.Wcap + sd];
+    int npl = 0;
+    const bool ok = pp_closure(d, a, P, s_pl[sd], npl);
+    if (lane == 0) s_npl[sd] = ok ? npl : 0;
+    if (!ok) {
+      if (lane == 0) s_bad = 1;
+      continue;
+    }
+    for (int j = lane; j < npl; j += 64) atomicMin(&pown[s_pl[sd][j]], sd);
+  }
+  __syncthreads();
+  if (!s_bad)
+    for (int sd = w; sd < nw; sd += nwv)
+      for (int j = lane; j < s_npl[sd]; j += 64)
+        if (__hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sd) s_bad = 1;
+  __syncthreads();
+  if (tid == 0) PP_DIAG(s_bad ? 5 : 6);
+  if (s_bad) {  // a closure overflowed, or two groups may meet: the serial pass
+    if (tid < 64) pp_serial_body(d, a, pend, odirty, nw);
+    return;
+  }
+  if (w < PPG_WAVES) {
+    const int NW = (d.B + 31) / 32;
+    uint32_t *mine = pend + (size_t)w * NW;
+    for (int i = lane; i < NW; i += 64) mine[i] = 0;
+    wave_fence();
+    for (int sd = w; sd < nw; sd += PPG_WAVES) {
+      const int P = d.work[(size_t)a * d.Wcap + sd];
+      if (lane == 0) mine[P >> 5] |= 1u << (P & 31);
+    }
+    wave_fence();
+    double rmax = c.rmax_cell;
+    pp_turns(d, a, mine, PPL{g_key[w], g_val[w], g_srt[w], g_x[w], g_y[w], g_m[w], g_r[w], PPG_CELLS}, odirty,
+             rmax, scr_k + (size_t)a * d.Wcap, dead0);
+    if (lane == 0) s_rmax[w] = rmax;
+  }
+  __syncthreads();
+  // the pass's deaths (appended by atomics) into turn order: rank by key
+  const int nd = __hip_atomic_load(&c.n_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - dead0;
+  const int64_t *dk = scr_k + (size_t)a * d.Wcap;
+  int *dl = d.dead + (size_t)a * d.B + dead0;
+  int rk[2], pv[2];
+  for (int k = 0; k < 2; k++) {
+    const int i = tid + k * T;
+    rk[k] = -1;
+    if (i < nd) {
+      const int64_t key = dk[i];
+      int r = 0;
+      for (int j = 0; j < nd; j++) r += dk[j] < key;
+      rk[k] = r;
+      pv[k] = dl[i];
+    }
+  }
+  if (nd > 2 * T && tid == 0) set_err(d, a, ERR_WORK_CAP);
+  __syncthreads();
+  for (int k = 0; k < 2; k++)
+    if (rk[k] >= 0) dl[rk[k]] = pv[k];
+  if (tid == 0) {
+    double r = c.rmax_cell;
+    for (int k = 0; k < PPG_WAVES; k++) r = fmax(r, s_rmax[k]);
+    c.rmax_cell = r;
+    c.stat[6] += 1;
+  }
 }
 
 // ------------------------------------------------------------ T18 spawn
@@ -2783,7 +3034,7 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
   oy = (double)yp;
 }
 
-__device__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait);
+__device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait);
 // ---------------------------------------------------- closing pellet update
 // Pellets never move and only a few change per tick (eaten, spawned, converted
 // from blobs), so the end-of-tick pellet layout (bucket-sorted, double buffered)
@@ -2845,7 +3096,7 @@ __device__ __forceinline__ int64_t wave_sort_i64(int64_t v) {
 // (its respawn threads key on tick_sp).  lds: 4096 free int64.
 constexpr int PU_LDS = 4096;
 constexpr int PU_SH = 2048;  // k_pel_update: kill / staged lists up to this length sit in LDS
-__device__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
+__device__ __forceinline__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
   ArenaCtl &c = d.ctl[a];
   const int T = blockDim.x, tid = threadIdx.x;
   const int n0 = c.n_pel, nconv = c.n_pnew, nsp = c.n_spawn_p, nst = nconv + nsp;
@@ -3032,7 +3283,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
     __syncthreads();
     // (the barrier's workgroup release waits for wave 0's count atomics; the
     // rebuild reads the counts at device scope, from L2)
-    if (threadIdx.x < 64) pp_serial_body(d, a, scr_k, scr_v, pend, defer ? s_odirty : nullptr);
+    pp_pass(d, a, scr_k, scr_v, pend, defer ? s_odirty : nullptr);
     __syncthreads();
     if (defer) occ_rebuild_dirty(d, a, s_odirty);
     __syncthreads();
@@ -3141,7 +3392,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
 
 // spawnStuff's counts (field.py:227-280): pellets and viruses to add, players to respawn
 // (n_resp / n_wait: the dead list's partition, done by the caller's block when !init)
-__device__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait) {
+__device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait) {
   ArenaCtl &c = d.ctl[a];
   c.dirty = 0;
   // spawnPellets: while len(pellets) < maxCollectibleCount
@@ -3689,8 +3940,8 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   // playerPlayerOverlap's serial pass + spawnStuff's plan + the end-of-tick virus
   // grid + the closing pellet update's sorted kill / join lists (and the pellet spawns)
-  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), sizeof(uint32_t) * ((d.B + 31) / 32), s, d, 0, scr_k,
-                     scr_v, 1, 1);
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), sizeof(uint32_t) * ((d.B + 31) / 32) * PPG_WAVES, s, d, 0,
+                     scr_k, scr_v, 1, 1);  // (pending bitmaps: one per parallel pp group wave)
   // the closing pellet update (survivors U joining staged records -> the new
   // current buffer) + the rest of spawnStuff as extra blocks: player respawns
   // with the FOV cache, virus spawns (fused into the pellet threads the FOV

@@ -373,7 +373,8 @@ int aigar_kernel_time(aigar_handle *h, const char *kernel, double *ms, int *laun
 /* Diagnostics: per-arena work counters accumulated since reset/load_state --
  * out[0..n) of: serial work-list entries of virusBlobOverlap, playerVirusOverlap,
  * pellet + blob eating (cells), pellets eaten, playerPlayerOverlap (players),
- * pellets respawned, -, ticks.  n <= 8. */
+ * pellets respawned, ticks whose playerPlayerOverlap ran as independent
+ * groups (see tick.hip pp_pass), ticks.  n <= 8. */
 int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n);
 
 /* Diagnostics: evaluate the device's pow (aigar_math.h: glibc 2.35's pow, bit

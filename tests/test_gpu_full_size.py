@@ -139,3 +139,44 @@ def test_c5_gpu_slice_matches_eight_oracles():
     g.close()
     for o in orcs:
         o.close()
+
+
+def test_parallel_pp_groups_match_the_serial_pass_and_the_oracle():
+    """playerPlayerOverlap as independent groups (tick.hip pp_pass: seeds whose
+    closures share no player run their turns in separate wavefronts, deaths
+    re-sorted into turn order): the bench's tick-50 C3 world with the
+    reference's Greedy bots (~6 pending players per tick), 40 ticks -- every
+    event and the state against the oracle and against the same device forced
+    to the serial pass (AIGAR_PP_SERIAL), and most ticks must have taken the
+    parallel path.  (The tick-600 world's greedy ticks, ~33 pending players,
+    mostly fall back to the serial pass: test_c3_matured_world_matches_oracle.)"""
+    import os
+    cfg = c3()
+    snap = parity.load_snapshot("c3_t50")
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    os.environ["AIGAR_PP_SERIAL"] = "1"
+    try:
+        s = _lib.Stepper(cfg)
+    finally:
+        del os.environ["AIGAR_PP_SERIAL"]
+    for x in (g, o, s):
+        x.load_state(snap)
+    w0, s0 = g.counters(), s.counters()
+    for t in range(40):
+        o.policy_greedy(True)
+        cmd = o.commands()
+        for x in (g, o, s):
+            x.set_commands(cmd)
+            x.step(1)
+        eo = o.events()
+        assert np.array_equal(g.events(), eo), "tick %d: parallel groups vs oracle" % t
+        assert np.array_equal(s.events(), eo), "tick %d: serial pass vs oracle" % t
+    for x in (g, s):
+        dif = parity.diff_states(x.get_state(), o.get_state())
+        assert not dif, dif[:3]
+    w1, s1 = g.counters(), s.counters()
+    assert s1["pp_parallel_ticks"] == s0["pp_parallel_ticks"]
+    par = w1["pp_parallel_ticks"] - w0["pp_parallel_ticks"]
+    assert par >= 20, "only %d of 40 ticks ran the groups in parallel" % par
+    for x in (g, o, s):
+        x.close()
