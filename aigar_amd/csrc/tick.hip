@@ -1838,6 +1838,15 @@ struct Food {
   __device__ double rad(int j, double m) const { return blob(j) ? d.b_r[gb(j)] : radius_of(m); }
   __device__ bool alive(int j) const { return blob(j) ? (d.b_flags[gb(j)] & F_ALIVE) != 0 : !d.pel_dead[g(j)]; }
   __device__ int64_t ej(int j) const { return blob(j) ? d.b_ej[gb(j)] : -2; }
+  // the dead flag alone (food_eat_loop notes its pellet kills in batches)
+  __device__ void mark_dead(int j) const {
+    if (!blob(j)) {
+      d.pel_dead[g(j)] = 1;
+    } else {
+      d.b_flags[gb(j)] = 0;
+      atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
+    }
+  }
   __device__ void kill(int j) const {
     if (!blob(j)) {
       d.pel_dead[g(j)] = 1;
@@ -2093,32 +2102,98 @@ __device__ __forceinline__ void food_eat(const Dev &d, const Food &F, int a, int
   F.kill(j);
   eaten += bl ? 0 : 1;
 }
-__device__ bool food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, uint32_t prio, const int *lst,
-                              int cnt) {
+// A committing cell's foods, kTailRegs at a time: the liveness and record of a
+// batch in one round of loads (the cell holds every reservation, so nothing
+// else eats them this round), the eats decided in list order on registers,
+// and the batch's pellet kills noted with one atomic (the kill list takes them
+// in any order: k_spawn_plan sorts it).  The first batch arrives preloaded.
+struct FoodBatch {
+  int j[kTailRegs];
+  bool al[kTailRegs];
+  double x[kTailRegs], y[kTailRegs], m[kTailRegs], r[kTailRegs];
+  int64_t sq[kTailRegs];
+  __device__ void load(const Dev &d, const Food &F, const int *jv, int n) {
+#pragma unroll
+    for (int k = 0; k < kTailRegs; k++) {
+      j[k] = jv[k];
+      al[k] = false;
+      x[k] = y[k] = m[k] = r[k] = 0;
+      sq[k] = 0;
+      if (k < n) {
+        al[k] = F.alive(j[k]);
+        F.load(j[k], x[k], y[k], m[k], sq[k]);
+        r[k] = Food::blob(j[k]) ? d.b_r[F.gb(j[k])] : 0.0;  // (a pellet's radius follows from its mass)
+      }
+    }
+  }
+};
+// returns the cell's radius if it ate, else 0
+__device__ double food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, uint32_t prio, const int *lst,
+                                int cnt, FoodBatch &fb) {
   double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
   int64_t cseq = d.c_seq[ci];
   const bool own = tile_owns(d, x, y);
   int eaten = 0;
   bool blobs = false, ate = false;
   Rect qb{};
-  for (int t = 0; t < cnt; t++) {
-    int j = lst[t];
-    if (Food::blob(j) && !blobs) {  // the blob turn: candidates from the box after the pellet turn
-      blobs = true;
-      qb = footprint(x, y, r, d.size);
+  for (int t0 = 0; t0 < cnt; t0 += kTailRegs) {
+    if (t0 > 0) {
+      int jv[kTailRegs];
+#pragma unroll
+      for (int k = 0; k < kTailRegs; k++) jv[k] = t0 + k < cnt ? lst[t0 + k] : 0;
+      fb.load(d, F, jv, cnt - t0);
     }
-    if (!F.alive(j)) continue;
-    double fm = F.m(j), fx = F.x(j), fy = F.y(j), fr = F.r(j);
-    if (blobs && !rect_hit(footprint(fx, fy, fr, d.size), qb)) continue;
-    if (!(overlap(x, y, m, r, fx, fy, fm, fr) && can_eat(m, fm))) continue;
-    food_eat(d, F, a, j, prio, t, cseq, F.seq(j), fm, m, r, eaten, own, fx, fy);
-    ate = true;
+    int kp[kTailRegs], nkp = 0;
+#pragma unroll
+    for (int k = 0; k < kTailRegs; k++) {
+      kp[k] = -1;
+      const int t = t0 + k, j = fb.j[k];
+      if (t >= cnt) continue;
+      if (Food::blob(j) && !blobs) {  // the blob turn: candidates from the box after the pellet turn
+        blobs = true;
+        qb = footprint(x, y, r, d.size);
+      }
+      if (!fb.al[k]) continue;
+      const double fm = fb.m[k], fx = fb.x[k], fy = fb.y[k], fr = Food::blob(j) ? fb.r[k] : radius_of(fm);
+      if (blobs && !rect_hit(footprint(fx, fy, fr, d.size), qb)) continue;
+      if (!(overlap(x, y, m, r, fx, fy, fm, fr) && can_eat(m, fm))) continue;
+      // eatCell (field.py:337-344): the event, the kill, the growth
+      if (own) {
+        const bool bl = Food::blob(j);
+        ev_push(d, a, bl ? PH_BLOB : PH_PELLET, ((uint64_t)prio << 16) | (uint64_t)t, bl ? 7 : 6, cseq, fb.sq[k]);
+        if (d.tiled) {
+          if (bl) tile_out(d, TR_BLOB, j & ~kBlobBit, fb.sq[k], 0.0, 0.0);
+          else tile_out(d, TR_PELLET, 0, fb.sq[k], fx, fy);
+        }
+      }
+      m = grow_mass(m, fm);
+      r = radius_of(m);
+      F.mark_dead(j);
+      if (!Food::blob(j)) {
+        eaten++;
+        if (j < F.n0) {
+          kp[k] = j;
+          nkp++;
+        }
+      }
+      ate = true;
+    }
+    if (nkp) {  // note_kill for the batch
+      int b = atomicAdd(&d.ctl[a].n_kill, nkp);
+#pragma unroll
+      for (int k = 0; k < kTailRegs; k++)
+        if (kp[k] >= 0) {
+          if (b < d.Pcap) d.kill_list[(size_t)a * d.Pcap + b] = kp[k];
+          else set_err(d, a, ERR_PELLET_CAP);
+          b++;
+        }
+    }
   }
   d.c_m[ci] = m;
   d.c_r[ci] = r;
   if (d.tiled && own && ate) tile_out(d, TR_CELL, (int32_t)ci, cseq, m, r);
   if (eaten) atomicAdd(&d.ctl[a].n_pel_eaten, eaten);
-  return ate;
+  return ate ? r : 0.0;
 }
 // one player's cells in reservation round `round`; returns the largest radius
 // of its cells that ate (0: none) -- the player-cell grid's radius bound
@@ -2150,15 +2225,20 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last) 
     uint32_t prio = (uint32_t)p * kMaxCells + k;
     if (cnt == kOverflow) continue;  // already in the serial work list (k_food_prep)
     bool own = true;
-    {  // every reservation key of the list at once (one load round for the first entries)
+    FoodBatch fb;
+    {  // every reservation key of the list at once (one load round for the first
+       // entries) -- with the first entries' records, which the eats use if it won
       uint64_t key = food_key(d.ctl[a].food_round + round, prio);
+      uint64_t kw[kTailRegs];
 #pragma unroll
-      for (int t = 0; t < kTailRegs; t++)
-        if (t < cnt) own &= (*F.owner(l4[t]) == key);
+      for (int t = 0; t < kTailRegs; t++) kw[t] = t < cnt ? *F.owner(l4[t]) : key;
+      fb.load(d, F, l4, cnt);
+#pragma unroll
+      for (int t = 0; t < kTailRegs; t++) own &= kw[t] == key;
       for (int t = kTailRegs; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
     }
     if (own) {
-      if (food_eat_loop(d, F, a, ci, prio, lst, cnt)) rgrow = fmax(rgrow, d.c_r[ci]);
+      rgrow = fmax(rgrow, food_eat_loop(d, F, a, ci, prio, lst, cnt, fb));
       d.f_done[ci] = 1;
     } else if (!last) {
       // reserve for the next round right away.  Safe without a separate pass: a
