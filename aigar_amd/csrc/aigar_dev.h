@@ -19,6 +19,22 @@
 
 namespace aigar {
 
+// Timing experiments only (tools/floor_variants.sh, results invalid): a kernel
+// whose bit is set in AIGAR_FLOOR returns at entry.  With AIGAR_FLOOR_OPAQUE the
+// test reads a kernel argument, so the compiler keeps the body (same registers,
+// LDS and code size); without it the body is compiled out.  Product builds: nothing.
+#ifdef AIGAR_FLOOR
+#ifdef AIGAR_FLOOR_OPAQUE
+#define FLOOR(k) \
+  if ((((AIGAR_FLOOR) >> (k)) & 1) && d.A > 0) return
+#else
+#define FLOOR(k) \
+  if (((AIGAR_FLOOR) >> (k)) & 1) return
+#endif
+#else
+#define FLOOR(k)
+#endif
+
 struct ArenaCtl {
   int64_t seq_next;  // next Cell creation sequence number
   int64_t tick;      // completed Field.update() calls since reset

@@ -230,6 +230,7 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 #endif
 template <typename OutT>
 __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch, const uint8_t *mask) {
+  FLOOR(9);
   // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
   // masks in creation order (no indirection in the per-square sums)
   __shared__ union {
@@ -267,14 +268,18 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // (the history grids too: read and rewritten once per observation, ~100 us
   // apart -- AIGAR_OBS_HIST_NT, measured)
   auto hist_st = [](double *p, double v) __attribute__((always_inline)) {
-#ifdef AIGAR_OBS_HIST_NT
+#if defined(AIGAR_OBS_HIST_WT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif defined(AIGAR_OBS_HIST_NT)
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
 #endif
   };
   auto row_st = [&](int i, OutT v) __attribute__((always_inline)) {
-#ifdef AIGAR_OBS_NO_NT
+#if defined(AIGAR_OBS_WT)  // write-through (sc1): the line leaves L2 with the store
+    __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif defined(AIGAR_OBS_NO_NT)
     row[i] = v;
 #else
     __builtin_nontemporal_store(v, row + i);

@@ -645,6 +645,7 @@ __device__ void tile_plan_thread(const Dev &d, int gp) {
   }
 }
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
+  FLOOR(0);
   PT_BEGIN(2);
   int gi = GTID;
   if (gi < kMaxCells * d.NP) {
@@ -744,6 +745,7 @@ __device__ __forceinline__ unsigned long long pl_word(unsigned long long st, uin
 // extra block per arena -- viruses are final after k_tick_begin -- the blob
 // grid in the arena's last block, once every tile's blobs are appended).
 __global__ void __launch_bounds__(256) k_players(Dev d) {
+  FLOOR(1);
   __shared__ int ws[4], wb[4];
   __shared__ int s_ps, s_pb, s_ts, s_tb, s_blob0;
   __shared__ int64_t s_seq0;
@@ -1555,6 +1557,7 @@ __device__ void vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 // in one launch: merging touches only player cells, the test only viruses/blobs
 // fold: virusBlobOverlap's serial pass runs in the last block (one wave per arena)
 __global__ void __launch_bounds__(256) k_merge_vb(Dev d, int64_t *scr_k, int *scr_v, int fold) {
+  FLOOR(2);
   const int gi = GTID;
   if (gi < d.NP) merge_player(d, gi);
   else if (d.virus_enabled) vb_active(d, gi - d.NP);
@@ -1667,6 +1670,7 @@ __device__ void pv_player(const Dev &d, int gp) {
 }
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
 __global__ void __launch_bounds__(256) k_pv_active(Dev d, int64_t *scr_k, int *scr_v, int fold) {
+  FLOOR(3);
   const int gp = GTID;
   if (gp < d.NP) pv_player(d, gp);
   if (fold && last_block(d.ticket + 2, gridDim.x))
@@ -1908,6 +1912,7 @@ constexpr int PREP_WAVES = 1;  // wavefronts per player (wave h takes cells h, h
 // are skipped.  resume: only cells not yet final (f_done != 1) are prepared.
 __device__ __forceinline__ double tile_rall() { return sqrt(kMaxMass / kPi) * (1 + 1e-9); }  // any cell's radius bound
 __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int resume) {
+  FLOOR(4);
   TILE_GATE(d);
   __shared__ int64_t s_seq[4][PREP_CAND];
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
@@ -2266,6 +2271,7 @@ __device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v
 // (wave 0, arena after arena; the grid's extra blocks do not take part)
 __global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last, int64_t *scr_k, int *scr_v,
                                                      int rounds, int fold) {
+  FLOOR(5);
   TILE_GATE(d);
   const int ncommit = (d.NP + 255) / 256;
   if ((int)blockIdx.x >= ncommit) {  // extra blocks: player-cell grid counts (round 1), scatter (round 2)
@@ -2538,6 +2544,7 @@ __device__ __forceinline__ void occ_rebuild_dirty(const Dev &d, int a, const uin
 // one wavefront per player: cells with an overlapping enemy cell at phase start
 // (+ the player's cells into the spawn occupancy)
 __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
+  FLOOR(6);
   PT_BEGIN(3);
   const int lane = threadIdx.x & 63;
   const int gp = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
@@ -3350,6 +3357,7 @@ __device__ __forceinline__ void pellet_close_prep(const Dev &d, int a, int64_t *
 // close (tick only): then the closing pellet update's step 1 (pellet_close_prep)
 __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *scr_k, int *scr_v, int pp,
                                                      int close) {
+  FLOOR(7);
   __shared__ int sflag[1024];
   __shared__ int gcnt[SG_CAP + 1];
   __shared__ int64_t s_sort[PU_LDS];
@@ -3821,6 +3829,7 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
   d.pbc[(size_t)a * d.H + i] = surv + nb;
 }
 __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int nbF) {
+  FLOOR(8);
   __shared__ int s_kill[PU_SH];
   __shared__ int64_t s_stg[PU_SH];
   __shared__ int s_n[2];
