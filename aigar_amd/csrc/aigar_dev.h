@@ -19,7 +19,7 @@
 
 namespace aigar {
 
-// Timing experiments only (tools/floor_variants.sh, results invalid): a kernel
+// Timing experiments only (tools/build_variant.sh + prof_ab.sh, results invalid): a kernel
 // whose bit is set in AIGAR_FLOOR returns at entry.  With AIGAR_FLOOR_OPAQUE the
 // test reads a kernel argument, so the compiler keeps the body (same registers,
 // LDS and code size); without it the body is compiled out.  Product builds: nothing.
@@ -128,6 +128,17 @@ struct alignas(32) PelRec {
   int64_t seq;
 };
 constexpr int kPelStride = 4;  // PelRec in 8-byte words (per-lane strided loads of one field)
+// the closing pellet update's record store (AIGAR_PEL_WT: write-through, timing variant)
+__device__ __forceinline__ void pel_store(PelRec *p, const PelRec &r) {
+#ifdef AIGAR_PEL_WT
+  __hip_atomic_store(&p->x, r.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&p->y, r.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&p->m, r.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&p->seq, r.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = r;
+#endif
+}
 
 struct Dev {
   int A, B, NP, size, cols, H;
@@ -177,6 +188,11 @@ struct Dev {
   uint32_t *c_flags;
   int64_t *c_seq;
   uint8_t *c_active;
+  // Cell.split geometry of a splitting player's cells [16*NP], computed by the
+  // cell's own k_tick_begin thread (the new cell's radius and momentum): the
+  // split in k_players' per-player chain then loads it instead of evaluating
+  // two atan2 / sincos pairs per cell
+  double *sp_r, *sp_svx, *sp_svy;
   // per-player blob staging [16][NP]
   double *sb_x, *sb_y, *sb_svx, *sb_svy;
   uint8_t *sb_slot;

@@ -87,17 +87,22 @@ AIGAR_D void update_pos(double &x, double &y, double vx, double vy, double &svx,
   if ((svc != 0 && y == my) || y == 0) svy *= -1;
 }
 // cell.py:47-57
+// (c, s: cos / sin of the angle to the command point -- Cell.split's angle too, cell.py:76-78)
 AIGAR_D void set_move_direction(double x, double y, double m, double r, double cpx, double cpy, double &vx,
-                                double &vy) {
+                                double &vy, double &c, double &s) {
   double xd = cpx - x, yd = cpy - y;
   double hyp = xd * xd + yd * yd, r2 = r * r;
   double mod = py_min(hyp, r2) / r2;
   double ang = aigar_math::trig_atan2(yd, xd);  // correctly rounded (aigar_trig.h)
   double sp = kMoveSpeed * aigar_math::pow_glibc(m, -0.35);  // glibc pow, bit for bit (aigar_math.h)
-  double c, s;
   aigar_math::trig_sincos(ang, s, c);
   vx = sp * mod * c;
   vy = sp * mod * s;
+}
+AIGAR_D void set_move_direction(double x, double y, double m, double r, double cpx, double cpy, double &vx,
+                                double &vy) {
+  double c, s;
+  set_move_direction(x, y, m, r, cpx, cpy, vx, vy, c, s);
 }
 // cell.py:96-103 (orig_r = radius of the originating cell)
 AIGAR_D void add_momentum(double x, double y, double cpx, double cpy, double w, double h, double orig_r,

@@ -76,6 +76,9 @@ struct aigar_handle {
   uint8_t *d_pix_ovf = nullptr;  // per player: frame left to the pixel kernel's second pass
   size_t pix_bytes = 0;
   std::vector<void *> allocs;
+  char *arena = nullptr;  // aigar_create's arrays (dalloc); freed through allocs
+  size_t arena_size = 0, arena_used = 0;
+  bool arena_sizing = false;
   int box_recs = 0;   // C4: TileRec slots of a full exchange message (header + records + bitmap)
   int pass_recs = 0;  // ... of the current pass's message (the first pass sends no bitmap)
   int first_pass = 0;  // the current pass is the tick's first (its message carries the history hand-off)
@@ -122,10 +125,28 @@ struct aigar_handle {
 extern "C" const char *aigar_last_error(void) { return g_err.c_str(); }
 extern "C" int aigar_abi_version(void) { return AIGAR_ABI_VERSION; }
 
+// Device arrays.  aigar_create carves the world's ~120 arrays out of ONE
+// allocation (arena_*: a sizing pass, one hipMalloc, a carving pass) instead of a
+// hipMalloc each: one large allocation is mapped with large pages, so the tick's
+// kernels, which touch tens of arrays per load round, need far fewer address
+// translations.  Every array starts on a 256-byte boundary.  Later allocations
+// (pixel buffers) are separate.
 template <class T>
 static T *dalloc(aigar_handle *h, size_t n) {
   void *p = nullptr;
   if (n == 0) n = 1;
+  const size_t bytes = (n * sizeof(T) + 255) & ~(size_t)255;
+  if (h->arena_sizing) {  // sizing pass: a placeholder (never dereferenced)
+    const size_t off = h->arena_used;
+    h->arena_used += bytes;
+    return (T *)(uintptr_t)(256 + off);
+  }
+  if (h->arena) {
+    if (h->arena_used + bytes > h->arena_size) return nullptr;
+    p = h->arena + h->arena_used;
+    h->arena_used += bytes;
+    return (T *)p;  // (zeroed with the whole arena)
+  }
   if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
   (void)hipMemset(p, 0, n * sizeof(T));
   h->allocs.push_back(p);
@@ -307,6 +328,22 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
     d.field = dalloc<T>(h, (n));            \
     ok = ok && d.field != nullptr;          \
   } while (0)
+#ifndef AIGAR_NO_ARENA
+  for (int pass = 0; pass < 2; pass++) {  // 0: size the arena, 1: carve it
+    h->arena_sizing = pass == 0;
+    if (pass == 1) {
+      h->arena_size = h->arena_used;
+      h->arena_used = 0;
+      void *base = nullptr;
+      if (hipMalloc(&base, h->arena_size) != hipSuccess) {
+        ok = false;
+        break;
+      }
+      h->allocs.push_back(base);
+      (void)hipMemset(base, 0, h->arena_size);
+      h->arena = (char *)base;
+    }
+#endif
   AL(ctl, ArenaCtl, A);
   AL(p_alive, int, NP); AL(p_respawn, int, NP); AL(p_ncells, int, NP); AL(p_split, int, NP); AL(p_eject, int, NP);
   AL(p_pend, int, NP); AL(p_cmdx, double, NP); AL(p_cmdy, double, NP); AL(p_list, uint8_t, C);
@@ -314,6 +351,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(c_x, double, C); AL(c_y, double, C); AL(c_m, double, C); AL(c_r, double, C); AL(c_vx, double, C);
   AL(c_vy, double, C); AL(c_svx, double, C); AL(c_svy, double, C); AL(c_mt, double, C); AL(c_svc, int, C);
   AL(c_flags, uint32_t, C); AL(c_seq, int64_t, C); AL(c_active, uint8_t, C);
+  AL(sp_r, double, C); AL(sp_svx, double, C); AL(sp_svy, double, C);
   AL(sb_x, double, C); AL(sb_y, double, C); AL(sb_svx, double, C); AL(sb_svy, double, C); AL(sb_slot, uint8_t, C);
   const size_t P = A * d.Pcap;
   for (int b = 0; b < 2; b++) {
@@ -375,6 +413,11 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   h->d_stats = dalloc<double>(h, NP * 5);
   h->d_obs = dalloc<double>(h, NP * (size_t)d.L);
   ok = ok && h->scr_k && h->scr_v && h->d_cmd && h->d_stats && h->d_obs && h->d_mask && h->d_nnmask;
+#ifndef AIGAR_NO_ARENA
+  }
+  h->arena_sizing = false;
+  h->arena = nullptr;  // later dalloc calls (pixel buffers) allocate on their own
+#endif
   if (ok) (void)hipMemset(h->d_nnmask, 1, NP);  // every player is NN until aigar_set_roles
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);

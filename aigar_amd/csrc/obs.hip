@@ -263,26 +263,28 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   OBS_STAMP(0);
   OutT *row = out + (size_t)gp * L;
   // the output row is written once and read by the host / learner, never by
-  // the next tick: non-temporal stores keep it from evicting the world state
-  // (the next tick's working set) out of the L2s
-  // (the history grids too: read and rewritten once per observation, ~100 us
-  // apart -- AIGAR_OBS_HIST_NT, measured)
+  // the next tick, and the history grids are read back one observation later:
+  // both are stored write-through (sc1: the line leaves the XCD's L2 with the
+  // store), so they neither evict the world state (the next tick's working set)
+  // from the L2s nor leave dirty lines for the end-of-launch write-back.
+  // A/B on MI355X (profiles/r03_ab_notes.txt): against non-temporal row stores
+  // and plain history stores, +6.5 % per step (tick 96 -> 92 us, observe -0.6 us).
   auto hist_st = [](double *p, double v) __attribute__((always_inline)) {
-#if defined(AIGAR_OBS_HIST_WT)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif defined(AIGAR_OBS_HIST_NT)
+#if defined(AIGAR_OBS_HIST_NT)
     __builtin_nontemporal_store(v, p);
-#else
+#elif defined(AIGAR_OBS_HIST_PLAIN)
     *p = v;
+#else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
   };
   auto row_st = [&](int i, OutT v) __attribute__((always_inline)) {
-#if defined(AIGAR_OBS_WT)  // write-through (sc1): the line leaves L2 with the store
-    __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif defined(AIGAR_OBS_NO_NT)
+#if defined(AIGAR_OBS_NO_NT)
     row[i] = v;
-#else
+#elif defined(AIGAR_OBS_NT)
     __builtin_nontemporal_store(v, row + i);
+#else
+    __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
   };
   // one round of independent loads: liveness, the FOV cache written at the end
@@ -295,7 +297,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const double rmax_c = ctl.rmax_cell, rmax_v = ctl.rmax_virus;  // (the walk's grid expansions)
   const int pcur = ctl.pcur;                                      // current pellet buffer
   if (!alive) {  // getStateRepresentation returns None for dead players
-    for (int i = lane; i < L; i += 64) row[i] = (OutT)__builtin_nan("");
+    for (int i = lane; i < L; i += 64) row_st(i, (OutT)__builtin_nan(""));
     return;
   }
   if (d.tiled) {  // C4: one tile observes the bot -- its history holder, else its view centre's tile (tile_plan_thread)

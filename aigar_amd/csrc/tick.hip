@@ -283,6 +283,7 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   const double x = d.c_x[ci], y = d.c_y[ci];
   int svc = d.c_svc[ci];
   double cmdx, cmdy;
+  bool split;
   PT_MARK(2, 2);
   if (rp.on) {
     const Command c = random_command(d, gp, rp);  // (the player's live cells and slot 0 only)
@@ -296,9 +297,11 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
     if (!live) return;
     cmdx = c.x;
     cmdy = c.y;
+    split = c.split;
   } else {
     cmdx = d.p_cmdx[gp];
     cmdy = d.p_cmdy[gp];
+    split = d.p_split[gp] != 0;
   }
   if (m >= 4) {  // Cell.decayMass (cell.py:123-126)
     m = m * kDecay;
@@ -311,12 +314,22 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   d.c_svx[ci] = svx;
   d.c_svy[ci] = svy;
   if (mt > 0) d.c_mt[ci] = mt - 1;
-  double vx, vy;
+  double vx, vy, ca, sa;
   PT_MARK(2, 4);
-  set_move_direction(x, y, m, r, cmdx, cmdy, vx, vy);
+  set_move_direction(x, y, m, r, cmdx, cmdy, vx, vy, ca, sa);
   PT_MARK(2, 5);
   d.c_vx[ci] = vx;
   d.c_vy[ci] = vy;
+  if (split && m > 36) {  // Cell.split's geometry (cell.py:72-85), for update_player's split
+    const double W = (double)d.size, nr = radius_of(m / 2);
+    const double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
+    double svx2, svy2;
+    int svc2;
+    add_momentum(x, y, xp, yp, W, W, r, svx2, svy2, svc2);
+    d.sp_r[ci] = nr;
+    d.sp_svx[ci] = svx2;
+    d.sp_svy[ci] = svy2;
+  }
 }
 
 // adjustCellPositions (field.py:161-181) for the pair (a, b), a the bigger
@@ -340,7 +353,7 @@ __device__ __forceinline__ void adjust_pair(double &bx, double &by, double bm, d
 constexpr int kTailRegs = 4;
 template <int N>
 __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint8_t *lst, int n, bool eject,
-                                                double cpx, double cpy, double W) {
+                                                double cpx, double cpy, double W PT_PARAMS) {
   const int NP = d.NP;
   double x[N], y[N], vx[N], vy[N], svx[N], svy[N], m[N], r[N], mt[N];
   int svc[N];
@@ -366,6 +379,7 @@ __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint
       fl[k] = d.c_flags[ci];
     }
   }
+  PT_MARK(1, 2);
 #pragma unroll
   for (int k = 0; k < N; k++) {
     if (eject && k < n && m[k] >= 35) fl[k] |= F_EJECT;  // Player.eject (player.py:54-58)
@@ -425,7 +439,7 @@ __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint
 // the rest of Player.update (split, eject, move) + performEjections +
 // handlePlayerCollisions, one thread per player (list order matters)
 // nn / nb_out: the new cells and blobs it made (k_players' scans take them from registers)
-__device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int &nb_out) {
+__device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int &nb_out PT_PARAMS) {
   const int NP = d.NP;
   // the cell arrays never alias: let the compiler keep values in registers across stores
   double *__restrict__ cx = d.c_x, *__restrict__ cy = d.c_y, *__restrict__ cm = d.c_m, *__restrict__ cr = d.c_r;
@@ -448,6 +462,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
   const double W = (double)d.size;
   const double cpx = d.p_cmdx[gp], cpy = d.p_cmdy[gp];
   for (int k = kTailRegs; k < n; k++) lst[k] = d.p_list[k * NP + gp];
+  PT_MARK(1, 1);
   // (decay, momentum, merge timer and direction already ran per cell: update_cell)
   int n_new = 0;
   if (d.p_split[gp]) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
@@ -472,16 +487,12 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
       int slot = __ffs(~used) - 1;
       used |= 1u << slot;
       size_t ni = (size_t)slot * NP + gp;
-      // Cell.split (cell.py:72-85)
+      // Cell.split (cell.py:72-85); its angle, radius and momentum were computed by
+      // the cell's k_tick_begin thread (update_cell: the same values, bit for bit)
       double x = cx[ci], y = cy[ci];
-      double nm = cm[ci] / 2, nr = radius_of(nm);
-      double ang = aigar_math::trig_atan2(cpy - y, cpx - x);
-      double ca, sa;
-      aigar_math::trig_sincos(ang, sa, ca);
-      double xp = ca * nr * 4.5 + x, yp = sa * nr * 4.5 + y;
-      double svx, svy;
-      int svc;
-      add_momentum(x, y, xp, yp, W, W, cr[ci], svx, svy, svc);
+      double nm = cm[ci] / 2, nr = d.sp_r[ci];
+      double svx = d.sp_svx[ci], svy = d.sp_svy[ci];
+      int svc = 15;
       cx[ni] = x;
       cy[ni] = y;
       cm[ni] = nm;
@@ -493,15 +504,15 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
       csvc[ni] = svc;
       cmt[ni] = merge_time_for(1, nm);
       cfl[ni] = F_ALIVE | F_NEW;
-      double pm = cm[ci] / 2;
-      cm[ci] = pm;
-      cr[ci] = radius_of(pm);
+      cm[ci] = nm;  // (the parent keeps the other half: the same mass and radius)
+      cr[ci] = nr;
       lst[n++] = (uint8_t)slot;
       n_new++;
     }
   }
   if (n <= kTailRegs) {  // the common case: the rest runs on registers, one load round
-    const int nb = player_tail_regs<kTailRegs>(d, gp, lst, n, d.p_eject[gp] != 0, cpx, cpy, W);
+    const int nb = player_tail_regs<kTailRegs>(d, gp, lst, n, d.p_eject[gp] != 0, cpx, cpy, W PT_ARGS);
+    PT_MARK(1, 3);
     for (int k = 0; k < n; k++) d.p_list[k * NP + gp] = lst[k];
     d.p_ncells[gp] = n;
     nn = n_new;
@@ -772,9 +783,9 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
   const int p = tile * 256 + tid, gp = a * d.B + p;
   int nn = 0, nb = 0;
   if (p < d.B) {
-    update_player(d, gp, nn, nb);  // (its counts from registers, not re-loaded)
+    update_player(d, gp, nn, nb PT_ARGS);  // (its counts from registers, not re-loaded)
   }
-  PT_MARK(1, 1);
+  PT_MARK(1, 4);
   const int vs = nn + nb, vb = nb;
   int is = vs, ib = vb;
 #pragma unroll
@@ -850,7 +861,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     }
   }
   __syncthreads();
-  PT_MARK(1, 2);
+  PT_MARK(1, 5);
   const int64_t seq0 = s_seq0;
   const int blob0 = s_blob0;
   if (tile == ntiles - 1 && tid == 0) {  // arena totals are known: advance the bases
@@ -894,7 +905,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
       d.b_flags[g] = F_ALIVE;
     }
   }
-  PT_MARK(1, 3);
+  PT_MARK(1, 6);
   if (last_block(&c.pl_ticket, ntiles)) {  // the arena's last block: look-back epoch, blob grid
     if (tid == 0) __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     grid_small_build<1>(d, a, g_cnt, g_sh);
@@ -3795,7 +3806,7 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
         const int pos = i - kb + sb;
         if (pos < d.Pcap) {
           const size_t o = P0 + pos;
-          d.pel[dst][o] = PelRec{x, y, m, sq};
+          pel_store(&d.pel[dst][o], PelRec{x, y, m, sq});
           d.pel_col[dst][o] = col;
         }
       }
@@ -3822,7 +3833,7 @@ __device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel
     const int pos = start + surv + r;
     if (pos >= d.Pcap) continue;
     const size_t o = P0 + pos, gs = P0 + (int)(ls[t] & 0xFFFFFFFFll);
-    d.pel[dst][o] = d.pn[gs];
+    pel_store(&d.pel[dst][o], d.pn[gs]);
     d.pel_col[dst][o] = d.pn_col[gs];
   }
   d.pstart[(size_t)a * (d.H + 1) + i] = start;
@@ -3903,7 +3914,7 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
         const int pos = i - count_below_i32(K, nk, i) + count_below_i64(S, ns, (int64_t)b << 32);
         if (pos < d.Pcap) {
           const size_t o = P0 + pos;
-          d.pel[dst][o] = PelRec{x, y, m, sq};
+          pel_store(&d.pel[dst][o], PelRec{x, y, m, sq});
           d.pel_col[dst][o] = col;
         }
       }
@@ -3920,12 +3931,12 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
       const size_t o = P0 + pos;
       if (small && js >= nconv) {  // a spawn, drawn by k_tick_begin (k_spawn_plan did not stage it)
         const size_t so = (size_t)a * kSpawnAhead + js - nconv;
-        d.pel[dst][o] = PelRec{d.spec_x[so], d.spec_y[so], d.spec_m[so], c.seq_base_spawn + (js - nconv)};
+        pel_store(&d.pel[dst][o], PelRec{d.spec_x[so], d.spec_y[so], d.spec_m[so], c.seq_base_spawn + (js - nconv)});
         d.pel_col[dst][o] = -1;
         continue;
       }
       const size_t gs = P0 + js;
-      d.pel[dst][o] = d.pn[gs];
+      pel_store(&d.pel[dst][o], d.pn[gs]);
       d.pel_col[dst][o] = d.pn_col[gs];
     }
     d.pstart[(size_t)a * (d.H + 1) + i] = start;
