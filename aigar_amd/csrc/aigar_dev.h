@@ -90,7 +90,8 @@ enum : uint32_t {
   ERR_PELLET_CAP = 1, ERR_BLOB_CAP = 2, ERR_VIRUS_CAP = 4, ERR_EVENT_CAP = 8, ERR_WORK_CAP = 16,
   ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256, ERR_TILE_CAP = 512, ERR_TILE_LOOKUP = 1024,
   ERR_TILE_OBS = 2048,    // a tile observed a bot whose view reaches beyond its held pellets
-  ERR_TILE_PASSES = 4096  // a device-bounded tiled tick ended with owned cells undone
+  ERR_TILE_PASSES = 4096,  // a device-bounded tiled tick ended with owned cells undone
+  ERR_PREDICT = 8192       // updatePlayers made other counts than k_tick_begin predicted (head_counts)
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
@@ -182,6 +183,7 @@ struct Dev {
   double *o_last_mass;  // NN bots' lastMass (bot.py:229-230); NaN = None
   uint8_t *p_list;  // [16][NP]
   int *p_newc, *p_newb, *p_seqoff, *p_bloboff;
+  int *p_heavy;  // per player: classes of its heavy cells this tick (update_cell -> k_players)
   // cells [16*NP]
   double *c_x, *c_y, *c_m, *c_r, *c_vx, *c_vy, *c_svx, *c_svy, *c_mt;
   int *c_svc;

@@ -347,7 +347,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(ctl, ArenaCtl, A);
   AL(p_alive, int, NP); AL(p_respawn, int, NP); AL(p_ncells, int, NP); AL(p_split, int, NP); AL(p_eject, int, NP);
   AL(p_pend, int, NP); AL(p_cmdx, double, NP); AL(p_cmdy, double, NP); AL(p_list, uint8_t, C);
-  AL(p_newc, int, NP); AL(p_newb, int, NP); AL(p_seqoff, int, NP); AL(p_bloboff, int, NP);
+  AL(p_newc, int, NP); AL(p_heavy, int, NP); AL(p_newb, int, NP); AL(p_seqoff, int, NP); AL(p_bloboff, int, NP);
   AL(c_x, double, C); AL(c_y, double, C); AL(c_m, double, C); AL(c_r, double, C); AL(c_vx, double, C);
   AL(c_vy, double, C); AL(c_svx, double, C); AL(c_svy, double, C); AL(c_mt, double, C); AL(c_svc, int, C);
   AL(c_flags, uint32_t, C); AL(c_seq, int64_t, C); AL(c_active, uint8_t, C);
@@ -453,7 +453,7 @@ static int check_device_errors(aigar_handle *h) {
       return fail("device error bits 0x%x in arena %d (1 pellet cap, 2 blob cap, 4 virus cap, 8 event cap, "
                   "16 worklist cap, 32 observation cap, 64 candidate cap, 128 slot, 256 pixel-frame object cap, "
                   "512 tile message cap, 1024 tile record lookup, 2048 tile view beyond the held pellets, "
-                  "4096 tiled tick ended with undone cells)",
+                  "4096 tiled tick ended with undone cells, 8192 new-cell / blob counts not as predicted)",
                   ctl[a].err, a);
   return 0;
 }

@@ -410,6 +410,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   };
   int np, nc, nv;
   OBS_STAMP(1);
+#if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 1  // per-phase cost variants (timing only, results invalid)
+  if (fx + fy + fs + left + ox + h_slf0 + h_elf0 == -1.2345) row_st(0, (OutT)0);
+  return;
+#endif
   {  // (lists known to be the LDS arrays here: ds_write appends)
     ObjList P0{&p_sx[0].seq, p_m, nullptr, p_mask, nullptr, nullptr};
     ObjList C0{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
@@ -417,6 +421,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     walk(P0, OBS_PCAP, C0, OBS_CCAP, V0, OBS_VCAP, np, nc, nv);
   }
   OBS_STAMP(2);
+#if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 2
+  if (np + nc + nv == -12345 || h_slf0 + h_elf0 == -1.2345) row_st(0, (OutT)0);
+  return;
+#endif
   ObjList PL{&p_sx[0].seq, p_m, nullptr, p_mask, nullptr, &p_px[0].perm};
   ObjList CL{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
   ObjList VL{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
@@ -494,6 +502,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   }
   wave_fence();
   OBS_STAMP(3);
+#if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 3
+  if (np + nc + nv == -12345 || h_slf0 + h_elf0 == -1.2345 || (sm && sm[0] == -1.0)) row_st(0, (OutT)0);
+  return;
+#endif
 #ifdef AIGAR_OBS_TIMING
   if (lane == 0) obs_ts_l[6] = (unsigned long long)np | ((unsigned long long)nc << 20) | ((unsigned long long)nv << 40);
 #endif

@@ -270,13 +270,29 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
 // rp.on: the synthetic population's policy is evaluated here (every cell of a
 // player computes the same command; slot 0 stores it for k_players), which
 // saves the policy launch of aigar_run's step
+// What update_player will create (k_players' look-back scan publishes it before
+// the player chains run): Cell.split makes a cell of every cell heavier than 36
+// after decay, the heaviest first, while the player has fewer than 16 cells
+// (player.py:46-52), and Player.eject then ejects from every cell of at least 35
+// (player.py:54-58; a split cell weighs half, m / 2 exactly).  Every live cell of
+// at least 35 after decay adds its class to its player's word p_heavy (update_cell,
+// one atomic per heavy cell): bits 0-7 cells > 36, 8-15 cells >= 70 (both halves
+// eject), 16-23 cells in [35, 36].  Ties split in list order, but tied cells weigh
+// the same, so the counts do not depend on which.  k_players reads and clears the
+// word and checks the chain's own counts against it (ERR_PREDICT).
+__device__ __forceinline__ void predicted_counts(int heavy, int n0, bool split, bool eject, int &nsplit, int &nb) {
+  const int c36 = heavy & 0xFF, c70 = (heavy >> 8) & 0xFF, c35 = (heavy >> 16) & 0xFF;
+  nsplit = split ? min(c36, kMaxCells - n0) : 0;
+  nb = eject ? 2 * min(nsplit, c70) + (c36 - nsplit) + c35 : 0;
+}
 __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPolicy &rp PT_PARAMS) {
   const int NP = d.NP;
   if (gi >= kMaxCells * NP) return;
   const int gp = gi % NP;
   const size_t ci = (size_t)gi;
+  const bool head = gi < NP;  // the player's slot-0 thread
   const bool live = d.c_flags[ci] & F_ALIVE;
-  if (!d.p_alive[gp] || (!live && !(rp.on && gi < NP))) return;  // (dead players keep their command: makeMove)
+  if (!d.p_alive[gp] || (!live && !(rp.on && head))) return;  // (dead players keep their command: makeMove)
   // every load of the cell up front, before any store: one memory round trip,
   // not one per store the compiler cannot prove disjoint
   double m = d.c_m[ci], r = d.c_r[ci], svx = d.c_svx[ci], svy = d.c_svy[ci], mt = d.c_mt[ci];
@@ -288,7 +304,7 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
   if (rp.on) {
     const Command c = random_command(d, gp, rp);  // (the player's live cells and slot 0 only)
     PT_MARK(2, 3);
-    if (gi < NP) {  // slot 0 stores the player's command
+    if (head) {  // slot 0 stores the player's command
       d.p_cmdx[gp] = c.x;
       d.p_cmdy[gp] = c.y;
       d.p_split[gp] = c.split;
@@ -309,6 +325,8 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
     d.c_m[ci] = m;
     d.c_r[ci] = r;
   }
+  if (m >= 35)  // k_players' predicted counts (predicted_counts)
+    atomicAdd(&d.p_heavy[gp], (m > 36 ? 1 : 0) | (m >= 70 ? 1 << 8 : 0) | (m > 36 ? 0 : 1 << 16));
   update_momentum(svc, svx, svy);
   d.c_svc[ci] = svc;
   d.c_svx[ci] = svx;
@@ -428,10 +446,10 @@ __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint
     d.c_y[ci] = y[k];
     d.c_svx[ci] = svx[k];
     d.c_svy[ci] = svy[k];
-    if (ej[k]) {
-      d.c_m[ci] = m[k];
-      d.c_flags[ci] = fl[k] & ~F_EJECT;
-    }
+    if (ej[k]) d.c_m[ci] = m[k];
+    // the flags as k_players leaves them: updateHashTables inserts every cell, and a
+    // new cell stops being new (the seq pass then only numbers the new cells)
+    d.c_flags[ci] = (fl[k] & ~(F_EJECT | F_NEW)) | F_INHASH;
   }
   return nb;
 }
@@ -439,7 +457,10 @@ __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint
 // the rest of Player.update (split, eject, move) + performEjections +
 // handlePlayerCollisions, one thread per player (list order matters)
 // nn / nb_out: the new cells and blobs it made (k_players' scans take them from registers)
-__device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int &nb_out PT_PARAMS) {
+// fast: the player took the register tail, its flags are final and its list is
+// in lst_out (n_out cells; k_players' seq pass then needs no loads)
+__device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int &nb_out, bool &fast,
+                                              uint8_t (&lst_out)[kTailRegs], int &n_out PT_PARAMS) {
   const int NP = d.NP;
   // the cell arrays never alias: let the compiler keep values in registers across stores
   double *__restrict__ cx = d.c_x, *__restrict__ cy = d.c_y, *__restrict__ cm = d.c_m, *__restrict__ cr = d.c_r;
@@ -455,6 +476,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
   const bool alive = d.p_alive[gp];
   int n = d.p_ncells[gp];
   nn = nb_out = 0;
+  fast = false;
   if (!alive) {  // updateRespawnTime (player.py:74-75)
     d.p_respawn[gp] -= 1;
     return;
@@ -517,6 +539,10 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
     d.p_ncells[gp] = n;
     nn = n_new;
     nb_out = nb;
+    fast = true;
+    n_out = n;
+#pragma unroll
+    for (int k = 0; k < kTailRegs; k++) lst_out[k] = lst[k];
     return;
   }
   if (d.p_eject[gp])  // Player.eject (player.py:54-58)
@@ -781,12 +807,17 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     }
   }
   const int p = tile * 256 + tid, gp = a * d.B + p;
-  int nn = 0, nb = 0;
+  // the new cells / blobs each player will create, predicted by its k_tick_begin
+  // threads (predicted_counts): the block scan and the tile's aggregate for the
+  // look-back are published before the player chains run, so the look-back after
+  // them finds every predecessor's aggregate instead of waiting for the slowest tile
+  int pn = 0, pb = 0;
   if (p < d.B) {
-    update_player(d, gp, nn, nb PT_ARGS);  // (its counts from registers, not re-loaded)
+    const int heavy = d.p_heavy[gp];
+    if (d.p_alive[gp]) predicted_counts(heavy, d.p_ncells[gp], d.p_split[gp] != 0, d.p_eject[gp] != 0, pn, pb);
+    if (heavy) d.p_heavy[gp] = 0;  // (the next tick's k_tick_begin adds to it again)
   }
-  PT_MARK(1, 4);
-  const int vs = nn + nb, vb = nb;
+  const int vs = pn + pb, vb = pb;
   int is = vs, ib = vb;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -815,16 +846,26 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
   }
   __syncthreads();
   const uint32_t ep = s_epoch;
-  if (w == 0) {
+  if (w == 0 && lane == 0) {
     const uint32_t ts = s_ts, tb = s_tb;
     if (tile == 0) {
-      if (lane == 0) {
-        __hip_atomic_store(&st[0], pl_word(PL_INC, ep, ts, tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_ps = s_pb = 0;
-      }
+      __hip_atomic_store(&st[0], pl_word(PL_INC, ep, ts, tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ps = s_pb = 0;
     } else {
-      if (lane == 0)
-        __hip_atomic_store(&st[tile], pl_word(PL_AGG, ep, ts, tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&st[tile], pl_word(PL_AGG, ep, ts, tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  int nn = 0, nb = 0, fn = 0;
+  bool fast = false;
+  uint8_t flst[kTailRegs];
+  if (p < d.B) {
+    update_player(d, gp, nn, nb, fast, flst, fn PT_ARGS);  // (its counts from registers, not re-loaded)
+    if (nn != pn || nb != pb) set_err(d, a, ERR_PREDICT);
+  }
+  PT_MARK(1, 4);
+  if (w == 0) {
+    const uint32_t ts = s_ts, tb = s_tb;
+    if (tile != 0) {
       int run_s = 0, run_b = 0, hi = tile - 1;
       for (;;) {
         int t = hi - lane;
@@ -876,14 +917,22 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
       c.n_blob = blob0 + totb;
     }
   }
-  if (p < d.B && d.p_alive[gp]) {
+  // the seq pass: a register-tail player's flags are final already and its list
+  // is in flst (fn cells): only its new cells (the last nn) are numbered here
+  if (p < d.B && (fast ? nb > 0 || nn > 0 : d.p_alive[gp] != 0)) {
     const int64_t s0 = seq0 + s_ps + ws[w] + (is - vs);
     const int boff = s_pb + wb[w] + (ib - vb);
-    const int n = d.p_ncells[gp];
-    for (int k = 0; k < n; k++) {
-      size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
-      if (k >= n - nn) d.c_seq[ci] = s0 + (k - (n - nn));
-      d.c_flags[ci] = (d.c_flags[ci] & ~F_NEW) | F_INHASH;  // updateHashTables inserts every cell
+    if (fast) {
+#pragma unroll
+      for (int k = 0; k < kTailRegs; k++)
+        if (k >= fn - nn && k < fn) d.c_seq[(size_t)flst[k] * NP + gp] = s0 + (k - (fn - nn));
+    } else {
+      const int n = d.p_ncells[gp];
+      for (int k = 0; k < n; k++) {
+        size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+        if (k >= n - nn) d.c_seq[ci] = s0 + (k - (n - nn));
+        d.c_flags[ci] = (d.c_flags[ci] & ~F_NEW) | F_INHASH;  // updateHashTables inserts every cell
+      }
     }
     for (int j = 0; j < nb; j++) {
       int bi = blob0 + boff + j;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# usage (GPU box): bash tools/gpu_iter4.sh TAG SO_B -- GPU suite, A/B against SO_B, kernel trace, observe phase costs
+set -o pipefail
+TAG=$1; B=$2
+R=$GRAFT_REPO_ROOT; [ -z "$R" ] && R=$(pwd)
+mkdir -p $R/gpurun_out; cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -30 gpurun_out/${TAG}_pytest_gpu.log; exit 1; }
+tail -n 1 gpurun_out/${TAG}_pytest_gpu.log
+bash tools/ab.sh ${TAG} $B 3 || exit 1
+bash tools/obs_phase_cost.sh $TAG || exit 1
+grep -E "^==|k_observe" gpurun_out/${TAG}_obs_prof.txt
+timeout -k 10 200 python tools/phase_timing.py run 50 random > gpurun_out/${TAG}_pt_random.txt 2>&1 || { echo "pt rc=$?"; exit 1; }
+echo done
