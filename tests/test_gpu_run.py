@@ -94,3 +94,24 @@ def test_run_rejects_host_buffers_and_bad_policy():
     with pytest.raises(KeyError):
         g.run(1, "bogus")
     g.close()
+
+
+def test_run_many_steps_in_one_call():
+    """Many steps in ONE aigar_run call (graph replays back to back): the last
+    rows (whose last-frame channels chain through every step's history) and the
+    world must equal the separate calls'."""
+    cfg = _cfg(bots=512)
+    fused, sep = _pair(cfg, 12)
+    oa = torch.zeros((fused.NP, fused.obs_len), dtype=torch.float64, device="cuda")
+    ob = torch.zeros_like(oa)
+    for n in (1, 7, 24):
+        fused.run(n, "random", oa, p_split=0.05, p_eject=0.05, seed=5)
+        for _ in range(n):
+            sep.policy_random(0.05, 0.05, 5)
+            sep.step(1)
+            sep.observe(ob)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0)), n
+    assert parity.diff_states(fused.get_state(), sep.get_state(), ftol=0.0) == []
+    fused.close()
+    sep.close()
