@@ -456,11 +456,31 @@ __device__ __forceinline__ int player_tail_regs(const Dev &d, int gp, const uint
 
 // the rest of Player.update (split, eject, move) + performEjections +
 // handlePlayerCollisions, one thread per player (list order matters)
+// The player's fields update_player starts from, loaded by k_players in the
+// kernel's first round (beside the predicted counts, before the block scan)
+struct PlayerHead {
+  uint8_t lst[kTailRegs];  // the list's first rows (the rows past the count exist, unused)
+  bool alive, split, eject;
+  int n;
+  double cpx, cpy;
+};
+__device__ __forceinline__ PlayerHead player_head(const Dev &d, int gp) {
+  PlayerHead h;
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) h.lst[k] = d.p_list[k * d.NP + gp];
+  h.alive = d.p_alive[gp] != 0;
+  h.n = d.p_ncells[gp];
+  h.split = d.p_split[gp] != 0;
+  h.eject = d.p_eject[gp] != 0;
+  h.cpx = d.p_cmdx[gp];
+  h.cpy = d.p_cmdy[gp];
+  return h;
+}
 // nn / nb_out: the new cells and blobs it made (k_players' scans take them from registers)
 // fast: the player took the register tail, its flags are final and its list is
 // in lst_out (n_out cells; k_players' seq pass then needs no loads)
-__device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int &nb_out, bool &fast,
-                                              uint8_t (&lst_out)[kTailRegs], int &n_out PT_PARAMS) {
+__device__ __forceinline__ void update_player(const Dev &d, int gp, const PlayerHead &ph, int &nn, int &nb_out,
+                                              bool &fast, uint8_t (&lst_out)[kTailRegs], int &n_out PT_PARAMS) {
   const int NP = d.NP;
   // the cell arrays never alias: let the compiler keep values in registers across stores
   double *__restrict__ cx = d.c_x, *__restrict__ cy = d.c_y, *__restrict__ cm = d.c_m, *__restrict__ cr = d.c_r;
@@ -472,22 +492,21 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
   // rows past the cell count are allocated and simply unused)
   uint8_t lst[kMaxCells];
 #pragma unroll
-  for (int k = 0; k < kTailRegs; k++) lst[k] = d.p_list[k * NP + gp];
-  const bool alive = d.p_alive[gp];
-  int n = d.p_ncells[gp];
+  for (int k = 0; k < kTailRegs; k++) lst[k] = ph.lst[k];
+  int n = ph.n;
   nn = nb_out = 0;
   fast = false;
-  if (!alive) {  // updateRespawnTime (player.py:74-75)
+  if (!ph.alive) {  // updateRespawnTime (player.py:74-75)
     d.p_respawn[gp] -= 1;
     return;
   }
   const double W = (double)d.size;
-  const double cpx = d.p_cmdx[gp], cpy = d.p_cmdy[gp];
+  const double cpx = ph.cpx, cpy = ph.cpy;
   for (int k = kTailRegs; k < n; k++) lst[k] = d.p_list[k * NP + gp];
   PT_MARK(1, 1);
   // (decay, momentum, merge timer and direction already ran per cell: update_cell)
   int n_new = 0;
-  if (d.p_split[gp]) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
+  if (ph.split) {  // Player.split (player.py:46-52): stable sort by mass desc, split the snapshot
     for (int i = 1; i < n; i++) {
       uint8_t key = lst[i];
       double km = cm[(size_t)key * NP + gp];
@@ -533,7 +552,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
     }
   }
   if (n <= kTailRegs) {  // the common case: the rest runs on registers, one load round
-    const int nb = player_tail_regs<kTailRegs>(d, gp, lst, n, d.p_eject[gp] != 0, cpx, cpy, W PT_ARGS);
+    const int nb = player_tail_regs<kTailRegs>(d, gp, lst, n, ph.eject, cpx, cpy, W PT_ARGS);
     PT_MARK(1, 3);
     for (int k = 0; k < n; k++) d.p_list[k * NP + gp] = lst[k];
     d.p_ncells[gp] = n;
@@ -545,7 +564,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, int &nn, int
     for (int k = 0; k < kTailRegs; k++) lst_out[k] = lst[k];
     return;
   }
-  if (d.p_eject[gp])  // Player.eject (player.py:54-58)
+  if (ph.eject)  // Player.eject (player.py:54-58)
     for (int k = 0; k < n; k++) {
       size_t ci = (size_t)lst[k] * NP + gp;
       if (cm[ci] >= 35) cfl[ci] |= F_EJECT;
@@ -812,9 +831,11 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
   // look-back are published before the player chains run, so the look-back after
   // them finds every predecessor's aggregate instead of waiting for the slowest tile
   int pn = 0, pb = 0;
+  PlayerHead ph{};
   if (p < d.B) {
+    ph = player_head(d, gp);  // (update_player's first round, issued with the counts)
     const int heavy = d.p_heavy[gp];
-    if (d.p_alive[gp]) predicted_counts(heavy, d.p_ncells[gp], d.p_split[gp] != 0, d.p_eject[gp] != 0, pn, pb);
+    if (ph.alive) predicted_counts(heavy, ph.n, ph.split, ph.eject, pn, pb);
     if (heavy) d.p_heavy[gp] = 0;  // (the next tick's k_tick_begin adds to it again)
   }
   const int vs = pn + pb, vb = pb;
@@ -859,7 +880,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
   bool fast = false;
   uint8_t flst[kTailRegs];
   if (p < d.B) {
-    update_player(d, gp, nn, nb, fast, flst, fn PT_ARGS);  // (its counts from registers, not re-loaded)
+    update_player(d, gp, ph, nn, nb, fast, flst, fn PT_ARGS);  // (its counts from registers, not re-loaded)
     if (nn != pn || nb != pb) set_err(d, a, ERR_PREDICT);
   }
   PT_MARK(1, 4);
