@@ -228,7 +228,9 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 #else  // 4 waves/SIMD: 4096 bots = 16 waves per CU, one residency round on 256 CUs
 #define OBS_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
-template <typename OutT>
+// WT: the store policy of the row and the history (below), chosen per launch by
+// the number of bots (launch_observe)
+template <typename OutT, bool WT>
 __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch, const uint8_t *mask) {
   FLOOR(9);
   // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
@@ -263,29 +265,23 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   OBS_STAMP(0);
   OutT *row = out + (size_t)gp * L;
   // the output row is written once and read by the host / learner, never by
-  // the next tick, and the history grids are read back one observation later:
-  // both are stored write-through (sc1: the line leaves the XCD's L2 with the
-  // store), so they neither evict the world state (the next tick's working set)
-  // from the L2s nor leave dirty lines for the end-of-launch write-back.
-  // A/B on MI355X (profiles/r03_ab_notes.txt): against non-temporal row stores
-  // and plain history stores, +6.5 % per step (tick 96 -> 92 us, observe -0.6 us).
+  // the next tick, and the history grids are read back one observation later.
+  // WT (one arena, a launch of a few thousand bots beside a latency-bound
+  // tick): both are stored write-through (sc1: the line leaves the XCD's L2 with
+  // the store), so they neither evict the world state (the next tick's working
+  // set) from the L2s nor leave dirty lines for the end-of-launch write-back;
+  // A/B on MI355X (profiles/r03_ab_notes.txt): +6.5 % per C3 step against
+  // non-temporal rows and plain history (tick 96 -> 92 us).  !WT (many arenas:
+  // a streaming launch of hundreds of MB): non-temporal rows, plain history --
+  // write-through stores lost a quarter of the bandwidth there (16 arenas:
+  // 2.66 -> 1.85 TB/s).
   auto hist_st = [](double *p, double v) __attribute__((always_inline)) {
-#if defined(AIGAR_OBS_HIST_NT)
-    __builtin_nontemporal_store(v, p);
-#elif defined(AIGAR_OBS_HIST_PLAIN)
-    *p = v;
-#else
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+    if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
   };
   auto row_st = [&](int i, OutT v) __attribute__((always_inline)) {
-#if defined(AIGAR_OBS_NO_NT)
-    row[i] = v;
-#elif defined(AIGAR_OBS_NT)
-    __builtin_nontemporal_store(v, row + i);
-#else
-    __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+    if constexpr (WT) __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __builtin_nontemporal_store(v, row + i);
   };
   // one round of independent loads: liveness, the FOV cache written at the end
   // of the tick (store_player_fov) and the own cells' slots
@@ -1015,6 +1011,7 @@ void launch_player_fov(const Dev &d, hipStream_t s) {
 
 #include "obs_wide.inc"
 
+constexpr int kObsWtBots = 16384;  // k_observe's store policy switch (bots per launch)
 // the state representation the configuration asks for (bot.py:272-299): the
 // default grid (<= 16 squares per side), the wide grid (CNN grid view), or the
 // simple representation (GRID_VIEW_ENABLED = False)
@@ -1025,10 +1022,17 @@ void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t 
   } else if (d.G > 16) {
     if (dtype == 0) hipLaunchKernelGGL(k_observe_wide<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
     else hipLaunchKernelGGL(k_observe_wide<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
-  } else if (dtype == 0) {
-    hipLaunchKernelGGL(k_observe<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
   } else {
-    hipLaunchKernelGGL(k_observe<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+    // write-through stores up to a few arenas' worth of bots (a latency-bound
+    // launch), non-temporal beyond (a streaming one); see k_observe
+    const bool wt = d.NP <= kObsWtBots;
+    if (dtype == 0) {
+      if (wt) hipLaunchKernelGGL((k_observe<double, true>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
+      else hipLaunchKernelGGL((k_observe<double, false>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
+    } else {
+      if (wt) hipLaunchKernelGGL((k_observe<float, true>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+      else hipLaunchKernelGGL((k_observe<float, false>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+    }
   }
 }
 void launch_policy(const Dev &d, hipStream_t s, double ps, double pe, uint64_t salt) {
