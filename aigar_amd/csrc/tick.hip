@@ -52,8 +52,8 @@ namespace aigar {
 // compiles these to nothing.
 #ifdef AIGAR_PHASE_TIMING
 constexpr int kPtWaves = 8192;
-__device__ unsigned int g_ptw[8][kPtWaves][8];
-__device__ unsigned int g_ptid[8][kPtWaves][2];  // HW_ID, XCC_ID of the wave
+__device__ unsigned int g_ptw[9][kPtWaves][8];
+__device__ unsigned int g_ptid[9][kPtWaves][2];  // HW_ID, XCC_ID of the wave
 __device__ __forceinline__ void pt_ids(unsigned *o) {
   unsigned a, b;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(a));
@@ -3914,9 +3914,18 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
   __shared__ int s_kill[PU_SH];
   __shared__ int64_t s_stg[PU_SH];
   __shared__ int s_n[2];
+  PT_BEGIN(8);
   const int per = nbP + nbB, nup = d.A * per;
-  if ((int)blockIdx.x >= nup + nbF) return spawn_virus(d, (blockIdx.x - nup - nbF) * 256 + threadIdx.x);
-  if ((int)blockIdx.x >= nup) return respawn_fov_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
+  if ((int)blockIdx.x >= nup + nbF) {
+    spawn_virus(d, (blockIdx.x - nup - nbF) * 256 + threadIdx.x);
+    PT_MARK(8, 5);
+    return;
+  }
+  if ((int)blockIdx.x >= nup) {
+    respawn_fov_thread(d, (blockIdx.x - nup) * 256 + threadIdx.x);
+    PT_MARK(8, 4);
+    return;
+  }
   const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
   ArenaCtl &c = d.ctl[a];
   const int mode = c.pu_small, n0 = c.pu_n0, nconv = c.pu_nconv;
@@ -3948,6 +3957,7 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
   }
   const int *kl = d.kill_list + P0;
   const int64_t *sk = d.stg_key + 2 * P0;
+  PT_MARK(8, 1);
   if (small && tid < 64) pellet_lists_wave(d, c, a, n0, nconv, c.n_spawn_p, min(nk, d.Pcap), s_kill, s_stg, s_n);
   const bool kin = small || nk <= PU_SH, sin = small || ns <= PU_SH;
   if (unsorted) return pel_update_blocked(d, a, pel, i, n0, nk, ns, src, dst, dead, x, y, m, sq, col, s0, c0, s_kill,
@@ -3959,6 +3969,7 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
       for (int t = tid; t < ns; t += 256) s_stg[t] = sk[t];
   }
   __syncthreads();
+  PT_MARK(8, 2);
   if (small) {
     ns = s_n[0];
     nk = s_n[1];
@@ -4012,6 +4023,7 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
     d.pstart[(size_t)a * (d.H + 1) + i] = start;
     d.pbc[(size_t)a * d.H + i] = surv + (j1 - j0);
   }
+  PT_MARK(8, 3);
 }
 
 // ------------------------------------------------------------ init helpers
@@ -4303,7 +4315,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
 }
 
 #ifdef AIGAR_PHASE_TIMING
-// out: [8][kPtWaves][8] wave records, ids: [8][kPtWaves][2] (see PT_BEGIN); *khz: the wall clock's rate
+// out: [9][kPtWaves][8] wave records, ids: [9][kPtWaves][2] (see PT_BEGIN); *khz: the wall clock's rate
 extern "C" int aigar_debug_phase_times(unsigned int *out, unsigned int *ids, int *khz, int reset) {
   if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptw), sizeof(g_ptw)) != hipSuccess) return -1;
   if (ids && hipMemcpyFromSymbol(ids, HIP_SYMBOL(g_ptid), sizeof(g_ptid)) != hipSuccess) return -1;

@@ -19,7 +19,8 @@ KERNELS = {0: ("k_food_prep", ["", "player", "cell", "pellet walk", "blob walk",
            2: ("k_tick_begin", ["", "update_cell", "cell loads", "policy", "decay+momentum", "move dir"]),
            3: ("k_pp_active", ["", "player", "cell", "grid test"]),
            4: ("k_food_commit", ["", "round 1", "round 2", "round 3", "round 4", "round 5", "round 6", "round 7+"]),
-           5: ("k_spawn_plan", ["", "pp serial", "compaction", "virus grid", "spawn counts", "pellet close"])}
+           5: ("k_spawn_plan", ["", "pp serial", "compaction", "virus grid", "spawn counts", "pellet close"]),
+           8: ("k_pel_update", ["", "first loads", "kill / join lists", "pellets + buckets", "fov cache", "virus spawns"])}
 
 
 def build():
@@ -46,8 +47,8 @@ def run(steps, policy="random"):
     import numpy as np
     L = C.CDLL(SO)
     W = 8192
-    buf = np.zeros((8, W, 8), dtype=np.uint32)
-    ids = np.zeros((8, W, 2), dtype=np.uint32)
+    buf = np.zeros((9, W, 8), dtype=np.uint32)
+    ids = np.zeros((9, W, 2), dtype=np.uint32)
     khz = C.c_int(0)
     ptr = buf.ctypes.data_as(C.POINTER(C.c_uint))
     iptr = ids.ctypes.data_as(C.POINTER(C.c_uint))
