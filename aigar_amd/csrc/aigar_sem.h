@@ -141,6 +141,10 @@ AIGAR_D double np_sum(const double *a, int n) {
 // to a multiple of 1/1000, returned as the double nearest to k/1000 (what
 // float(repr) of the decimal gives); a zero result keeps the sign of v.
 AIGAR_D double py_round3(double v) {
+  // |1000 v| < 0.4: rounds to k = 0, i.e. a zero with v's sign -- the common
+  // case of the wall channel, whose 1 - freeA / (gs * gs) is a few ulps for a
+  // square inside the field (no floor / fmod / division then)
+  if (fabs(v) < 0.0004) return copysign(0.0, v);
   double p = v * 1000.0;
   double e = fma(v, 1000.0, -p);  // p + e == 1000 * v exactly
   double k0 = floor(p), f, d;
