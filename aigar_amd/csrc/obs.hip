@@ -275,6 +275,11 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // a streaming launch of hundreds of MB): non-temporal rows, plain history --
   // write-through stores lost a quarter of the bandwidth there (16 arenas:
   // 2.66 -> 1.85 TB/s).
+#ifdef AIGAR_OBS_DIAG_NOSTORE  // (cost diagnostics only, results invalid: one store per lane at the end)
+  double diag_sum = 0;
+  auto hist_st = [&](double *p, double v) __attribute__((always_inline)) { diag_sum += v; };
+  auto row_st = [&](int i, OutT v) __attribute__((always_inline)) { diag_sum += (double)v; };
+#else
   auto hist_st = [](double *p, double v) __attribute__((always_inline)) {
     if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
@@ -283,6 +288,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     if constexpr (WT) __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __builtin_nontemporal_store(v, row + i);
   };
+#endif
   // one round of independent loads: liveness, the FOV cache written at the end
   // of the tick (store_player_fov) and the own cells' slots
   const bool alive = d.p_alive[gp];
@@ -606,11 +612,24 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
         fv = true;
       }
     }
+#ifdef AIGAR_OBS_DIAG_NOWALL  // (cost diagnostics only, results invalid)
+    double vw = 0.0;
+#else
     double lb = py_min(py_max(mx - gs / 2, 0.0), fieldSize), tb = py_min(py_max(my - gs / 2, 0.0), fieldSize);
     double rb = py_max(py_min(mx + gs / 2, fieldSize), 0.0), bb = py_max(py_min(my + gs / 2, fieldSize), 0.0);
     double freeA = (rb - lb) * (bb - tb);
-    // a square wholly inside the field: freeA / (gs*gs) is exactly 1 -> round(0, 3) = +0
-    double vw = (freeA == gs * gs) ? 0.0 : py_round3(1 - (freeA / (gs * gs)));
+    // round(1 - freeA / (gs*gs), 3).  A square inside the field has freeA within
+    // a few ulps of gs*gs, and the result is a zero whose sign is that of
+    // 1 - fl(freeA / gs2): negative iff fl(freeA / gs2) > 1, i.e. iff the exact
+    // quotient exceeds 1 + 2^-53 (the midpoint rounds to even, 1), i.e. iff
+    // freeA - gs2 > gs2 * 2^-53 -- exact: the difference of two doubles within a
+    // factor 2 (Sterbenz), a power-of-two scaling.  No division then.
+    const double gs2 = gs * gs, dlt = freeA - gs2;
+    double vw;
+    if (freeA == gs2) vw = 0.0;
+    else if (fabs(dlt) < 0.0003 * gs2) vw = dlt > gs2 * 0x1p-53 ? -0.0 : 0.0;
+    else vw = py_round3(1 - (freeA / gs2));
+#endif
     if (o_pel >= 0) row_st(o_pel + t, held ? (OutT)vp : (OutT)__builtin_nan(""));
     if (o_self >= 0) row_st(o_self + t, (OutT)vs);
     if (o_wall >= 0) row_st(o_wall + t, (OutT)vw);
@@ -698,6 +717,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
         });
   }
   OBS_STAMP(4);
+#ifdef AIGAR_OBS_DIAG_NOSTORE
+  if (diag_sum == -1.2345) row[lane] = (OutT)diag_sum;
+#endif
 #ifdef AIGAR_OBS_TIMING
   if (lane < OBS_TS && gp < 65536) g_obs_ts[(size_t)gp * OBS_TS + lane] = obs_ts_l[lane];
 #endif
