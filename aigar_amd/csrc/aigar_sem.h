@@ -169,19 +169,27 @@ AIGAR_D double py_round3(double v) {
 struct Rect {
   int x0, x1, y0, y1;
 };
+// floor(c / 20) of the exact quotient, c >= 0 (< 2^31): one multiply and two
+// exact corrections (20 q is an exact double) -- what c - py_mod(c, 20) / 20 is
+AIGAR_D int bucket_floor(double c) {
+  int q = (int)(c * 0.05);
+  q += ((double)(q + 1) * kBucket <= c) ? 1 : 0;
+  q -= ((double)q * kBucket > c) ? 1 : 0;
+  return q;
+}
 AIGAR_D Rect footprint(double px, double py, double rad, int size) {
   double cl = py_max(0.0, px - rad), ct = py_max(0.0, py - rad);
-  // (cl, ct >= 0: py_mod by the exact multiply + fma remainder, aigar_math::mod_pos)
+  // bl = cl - cl % 20 = 20 * floor(cl / 20) exactly (Python's float modulo), so
+  // the first bucket is floor(cl / 20); range(bl, lx, 20)'s last value
+  // bl + 20 * floor((lx - 1 - bl) / 20) lies in bucket floor((lx - 1) / 20)
   // (32-bit integers: coordinates are bounded by the field size)
-  int bl = (int)(cl - aigar_math::mod_pos(cl, (double)kBucket, 1.0 / kBucket)),
-      bt = (int)(ct - aigar_math::mod_pos(ct, (double)kBucket, 1.0 / kBucket));
+  const int kx = bucket_floor(cl), ky = bucket_floor(ct);
   int lx = (int)py_min((double)size, px + rad + 1), ly = (int)py_min((double)size, py + rad + 1);
   Rect r;
-  r.x0 = (int)(bl / kBucket);
-  r.y0 = (int)(bt / kBucket);
-  // range(bl, lx, 20): last x = bl + 20*floor((lx - 1 - bl)/20) when lx > bl
-  r.x1 = (lx > bl) ? (int)((bl + kBucket * ((lx - 1 - bl) / kBucket)) / kBucket) : r.x0 - 1;
-  r.y1 = (ly > bt) ? (int)((bt + kBucket * ((ly - 1 - bt) / kBucket)) / kBucket) : r.y0 - 1;
+  r.x0 = kx;
+  r.y0 = ky;
+  r.x1 = (lx > kx * kBucket) ? (lx - 1) / kBucket : kx - 1;
+  r.y1 = (ly > ky * kBucket) ? (ly - 1) / kBucket : ky - 1;
   return r;
 }
 AIGAR_D bool rect_hit(const Rect &a, const Rect &b) {
