@@ -49,21 +49,6 @@ __device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, dou
   return m;
 }
 
-// Pellet radius (cell.py:210-212): spawned pellets weigh 1, 2 or 3
-// (field.py:20-26), whose radii fold to constants (sqrt and division are
-// correctly rounded: the constants are Python's math.sqrt(m / math.pi), checked
-// against the device formula by tests/test_gpu_selftest.py); other masses
-// (converted blobs) take the full formula.
-constexpr double kPelletR1 = 0x1.20dd750429b6dp-1, kPelletR2 = 0x1.9884533d43651p-1,
-                 kPelletR3 = 0x1.f45437857749ap-1;
-__device__ __forceinline__ double pellet_radius(double m) {
-  constexpr double r1 = kPelletR1, r2 = kPelletR2, r3 = kPelletR3;
-  if (m == 1.0) return r1;
-  if (m == 2.0) return r2;
-  if (m == 3.0) return r3;
-  return radius_of(m);
-}
-
 // lane k's value, broadcast to the wave (v_readlane into scalar registers; k is wave-uniform)
 __device__ __forceinline__ double readlane_d(double v, int k) {
   const long long b = __double_as_longlong(v);

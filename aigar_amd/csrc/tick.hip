@@ -1900,7 +1900,7 @@ struct Food {
   __device__ double x(int j) const { return blob(j) ? d.b_x[gb(j)] : (j < n0 ? d.pel[pb][g(j)].x : d.pn[gs(j)].x); }
   __device__ double y(int j) const { return blob(j) ? d.b_y[gb(j)] : (j < n0 ? d.pel[pb][g(j)].y : d.pn[gs(j)].y); }
   __device__ double m(int j) const { return blob(j) ? d.b_m[gb(j)] : (j < n0 ? d.pel[pb][g(j)].m : d.pn[gs(j)].m); }
-  __device__ double r(int j) const { return blob(j) ? d.b_r[gb(j)] : radius_of(m(j)); }
+  __device__ double r(int j) const { return blob(j) ? d.b_r[gb(j)] : pellet_radius(m(j)); }
   __device__ int64_t seq(int j) const {
     return blob(j) ? d.b_seq[gb(j)] : (j < n0 ? d.pel[pb][g(j)].seq : d.pn[gs(j)].seq);
   }
@@ -1920,7 +1920,7 @@ struct Food {
       sq = r.seq;
     }
   }
-  __device__ double rad(int j, double m) const { return blob(j) ? d.b_r[gb(j)] : radius_of(m); }
+  __device__ double rad(int j, double m) const { return blob(j) ? d.b_r[gb(j)] : pellet_radius(m); }
   __device__ bool alive(int j) const { return blob(j) ? (d.b_flags[gb(j)] & F_ALIVE) != 0 : !d.pel_dead[g(j)]; }
   __device__ int64_t ej(int j) const { return blob(j) ? d.b_ej[gb(j)] : -2; }
   // the dead flag alone (food_eat_loop notes its pellet kills in batches)
@@ -2240,7 +2240,7 @@ __device__ double food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, u
         qb = footprint(x, y, r, d.size);
       }
       if (!fb.al[k]) continue;
-      const double fm = fb.m[k], fx = fb.x[k], fy = fb.y[k], fr = Food::blob(j) ? fb.r[k] : radius_of(fm);
+      const double fm = fb.m[k], fx = fb.x[k], fy = fb.y[k], fr = Food::blob(j) ? fb.r[k] : pellet_radius(fm);
       if (blobs && !rect_hit(footprint(fx, fy, fr, d.size), qb)) continue;
       if (!(overlap(x, y, m, r, fx, fy, fm, fr) && can_eat(m, fm))) continue;
       // eatCell (field.py:337-344): the event, the kill, the growth

@@ -46,3 +46,15 @@ def test_trig_is_correctly_rounded(tmp_path):
     assert "mismatches=0 " in out.stdout, out.stdout
     glibc = float(out.stdout.split("(")[1].split("%")[0])
     assert glibc < 0.5, out.stdout
+
+
+def test_pellet_radius_constants():
+    """aigar_sem.h folds the radii of 1-, 2- and 3-mass pellets (cell.py:210-212)
+    to constants: they must be Python's math.sqrt(m / math.pi) exactly."""
+    import math
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "aigar_amd", "csrc", "aigar_sem.h")).read()
+    consts = dict(re.findall(r"kPelletR(\d) = (0x[0-9a-fp.+-]+)", hdr))
+    assert sorted(consts) == ["1", "2", "3"]
+    for m, c in consts.items():
+        assert float.fromhex(c) == math.sqrt(int(m) / math.pi), m
