@@ -45,6 +45,20 @@ AIGAR_D double py_mod(double a, double b) {                            // float 
   return m;
 }
 AIGAR_D double radius_of(double m) { return (m > 0) ? sqrt(m / kPi) : 0.0; }  // cell.py:210-212
+// A pellet's radius: spawned pellets weigh 1, 2 or 3 (field.py:20-26), whose
+// radii fold to constants -- radius_of is correctly rounded (IEEE division and
+// square root), and these are Python's math.sqrt(m / math.pi)
+// (tests/test_pow_host.py::test_pellet_radius_constants); other masses
+// (converted blobs) take the formula.  Saves a division and a square root per
+// pellet candidate.
+constexpr double kPelletR1 = 0x1.20dd750429b6dp-1, kPelletR2 = 0x1.9884533d43651p-1,
+                 kPelletR3 = 0x1.f45437857749ap-1;
+AIGAR_D double pellet_radius(double m) {
+  if (m == 1.0) return kPelletR1;
+  if (m == 2.0) return kPelletR2;
+  if (m == 3.0) return kPelletR3;
+  return radius_of(m);
+}
 AIGAR_D double grow_mass(double m, double food) { return py_min(kMaxMass, m + food); }  // cell.py:119-121
 
 // overlap (cell.py:143-152): bigger = strictly larger mass, else the argument
