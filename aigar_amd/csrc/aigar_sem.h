@@ -106,7 +106,7 @@ AIGAR_D void set_move_direction(double x, double y, double m, double r, double c
                                 double &vy, double &c, double &s) {
   double xd = cpx - x, yd = cpy - y;
   double hyp = xd * xd + yd * yd, r2 = r * r;
-  double mod = py_min(hyp, r2) / r2;
+  double mod = hyp >= r2 ? 1.0 : hyp / r2;  // min(hyp, r2) / r2 (r2 / r2 is exactly 1: no division then)
   double ang = aigar_math::trig_atan2(yd, xd);  // correctly rounded (aigar_trig.h)
   double sp = kMoveSpeed * aigar_math::pow_glibc(m, -0.35);  // glibc pow, bit for bit (aigar_math.h)
   aigar_math::trig_sincos(ang, s, c);
@@ -191,6 +191,13 @@ AIGAR_D int bucket_floor(double c) {
   q -= ((double)q * kBucket > c) ? 1 : 0;
   return q;
 }
+// floor(c / 20) for any sign, = floor of the rounded quotient (see center_bucket_coord)
+AIGAR_D int bucket_floor_s(double c) {
+  int q = (int)floor(c * 0.05);
+  q += ((double)(q + 1) * kBucket <= c) ? 1 : 0;
+  q -= ((double)q * kBucket > c) ? 1 : 0;
+  return q;
+}
 AIGAR_D Rect footprint(double px, double py, double rad, int size) {
   double cl = py_max(0.0, px - rad), ct = py_max(0.0, py - rad);
   // bl = cl - cl % 20 = 20 * floor(cl / 20) exactly (Python's float modulo), so
@@ -210,9 +217,12 @@ AIGAR_D bool rect_hit(const Rect &a, const Rect &b) {
   return a.x0 <= a.x1 && a.y0 <= a.y1 && b.x0 <= b.x1 && b.y0 <= b.y1 && a.x0 <= b.x1 && b.x0 <= a.x1 &&
          a.y0 <= b.y1 && b.y0 <= a.y1;
 }
-AIGAR_D int center_bucket_coord(double v, int cols) {  // storage bucket of a centre coordinate
-  int b = (int)(v / kBucket);
-  if (v < 0) b = 0;
+// storage bucket of a centre coordinate: int(v / 20) of the rounded quotient,
+// which is the exact floor -- the round-up window below an integer k + 1
+// (20 x half the spacing of doubles below k + 1) is narrower than the spacing
+// of doubles near v = 20 (k + 1), so no v rounds up -- hence bucket_floor
+AIGAR_D int center_bucket_coord(double v, int cols) {
+  const int b = v < 0 ? 0 : bucket_floor(v);
   return b < cols ? b : cols - 1;
 }
 

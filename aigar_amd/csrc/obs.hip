@@ -124,8 +124,8 @@ __device__ __forceinline__ int obs_claim(const Dev &d, uint32_t epoch, int n) {
 // the hash expansion adds whenever the FOV edge sits away from a bucket edge.
 __device__ __forceinline__ Span clip_to_fov(Span s, double fx, double fy, double h, double R, int cols, int shift) {
   const double m = h + R + 1.0;
-  const int x0 = max(0, (int)floor((fx - m) / kBucket)) >> shift, x1 = min(cols - 1, (int)floor((fx + m) / kBucket));
-  const int y0 = max(0, (int)floor((fy - m) / kBucket)) >> shift, y1 = min(cols - 1, (int)floor((fy + m) / kBucket));
+  const int x0 = max(0, bucket_floor_s(fx - m)) >> shift, x1 = min(cols - 1, bucket_floor_s(fx + m));
+  const int y0 = max(0, bucket_floor_s(fy - m)) >> shift, y1 = min(cols - 1, bucket_floor_s(fy + m));
   s.bx0 = max(s.bx0, x0);
   s.bx1 = min(s.bx1, x1 < 0 ? -1 : x1 >> shift);
   s.by0 = max(s.by0, y0);
