@@ -2967,7 +2967,10 @@ extern "C" int aigar_debug_ppdiag(unsigned long long *out) {
 constexpr int PPG_SEEDS = 64;  // most pending players for the parallel pass
 constexpr int PPG_PL = 16;     // players per closure
 constexpr int PPG_CELLS = 64;  // cells per closure (also the turn candidate cap)
-constexpr int PPG_WAVES = 8;   // wavefronts running groups
+#ifndef AIGAR_PPG_WAVES
+#define AIGAR_PPG_WAVES 8
+#endif
+constexpr int PPG_WAVES = AIGAR_PPG_WAVES;  // wavefronts running groups
 constexpr int PPG_MIN = 3;     // fewer pending players: the serial pass (closures cost ~10 us)
 __device__ __forceinline__ bool pp_closure(const Dev &d, int a, int P, int *pl, int &npl) {
   const int lane = threadIdx.x & 63, NP = d.NP, B = d.B;
@@ -3070,7 +3073,7 @@ __device__ __forceinline__ bool pp_closure(const Dev &d, int a, int P, int *pl, 
 // group per seed, PPG_WAVES wavefronts each running its seeds' turns (their
 // pending bits together: disjoint groups interleave freely), then the pass's
 // deaths sorted into turn order by their keys.  Called by every thread.
-__device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend, uint32_t *odirty) {
+__device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend, uint32_t *odirty PT_PARAMS) {
   __shared__ int s_nw, s_dead0, s_bad;
   __shared__ int s_pl[PPG_SEEDS][PPG_PL], s_npl[PPG_SEEDS];
   __shared__ double s_rmax[PPG_WAVES];
@@ -3117,6 +3120,7 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
       for (int j = lane; j < s_npl[sd]; j += 64)
         if (__hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sd) s_bad = 1;
   __syncthreads();
+  PT_MARK(5, 6);
   if (tid == 0) PP_DIAG(s_bad ? 5 : 6);
   if (s_bad) {  // a closure overflowed, or two groups may meet: the serial pass
     if (tid < 64) pp_serial_body(d, a, pend, odirty, nw);
@@ -3138,6 +3142,7 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     if (lane == 0) s_rmax[w] = rmax;
   }
   __syncthreads();
+  PT_MARK(5, 7);
   // the pass's deaths (appended by atomics) into turn order: rank by key
   const int nd = __hip_atomic_load(&c.n_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - dead0;
   const int64_t *dk = scr_k + (size_t)a * d.Wcap;
@@ -3452,7 +3457,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
     __syncthreads();
     // (the barrier's workgroup release waits for wave 0's count atomics; the
     // rebuild reads the counts at device scope, from L2)
-    pp_pass(d, a, scr_k, scr_v, pend, defer ? s_odirty : nullptr);
+    pp_pass(d, a, scr_k, scr_v, pend, defer ? s_odirty : nullptr PT_ARGS);
     __syncthreads();
     if (defer) occ_rebuild_dirty(d, a, s_odirty);
     __syncthreads();
