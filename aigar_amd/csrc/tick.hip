@@ -2572,6 +2572,9 @@ __device__ __forceinline__ void occ_remove(const Dev &d, int a, Rect q) {
 // rebuilt from the final counts once the pass is over (occ_rebuild_dirty).
 // Counts are sums, so the order of the updates does not matter.
 constexpr int OCC_DW = 64;  // dirty-word bitmap: up to 2048 occupancy words (C3: 900)
+#ifndef AIGAR_OCC_BATCH
+#define AIGAR_OCC_BATCH 1
+#endif
 __device__ __forceinline__ void occ_mark(uint32_t *dirty, int b) {
   const int wd = b >> 6;
   atomicOr(&dirty[wd >> 5], 1u << (wd & 31));
@@ -2606,6 +2609,26 @@ __device__ __forceinline__ void occ_rebuild_dirty(const Dev &d, int a, const uin
   const uint32_t mine = dirty[lane];
   unsigned long long nz = __ballot(mine != 0);  // (usually none: no pp eat this tick)
   int k = 0;
+#if AIGAR_OCC_BATCH
+  // a wave's words four at a time: their count loads in one round
+  int q0 = -1, q1 = -1, q2 = -1, q3 = -1;
+  auto word = [&](int wd, int c) {
+    const unsigned long long bits = __ballot(c > 0);
+    if (lane == 0) occ[wd] = bits;
+  };
+  auto flush = [&]() {
+    auto ld = [&](int wd) {
+      const int b = wd * 64 + lane;
+      return wd >= 0 && b < d.H ? __hip_atomic_load(&cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    };
+    const int c0 = ld(q0), c1 = ld(q1), c2 = ld(q2), c3 = ld(q3);
+    if (q0 >= 0) word(q0, c0);
+    if (q1 >= 0) word(q1, c1);
+    if (q2 >= 0) word(q2, c2);
+    if (q3 >= 0) word(q3, c3);
+    q0 = q1 = q2 = q3 = -1;
+  };
+#endif
   while (nz) {
     const int i = __ffsll((long long)nz) - 1;
     nz &= nz - 1;
@@ -2614,12 +2637,25 @@ __device__ __forceinline__ void occ_rebuild_dirty(const Dev &d, int a, const uin
       const int wd = i * 32 + __ffs(m) - 1;
       m &= m - 1;
       if (k++ % nw != w) continue;
+#if AIGAR_OCC_BATCH
+      if (q0 < 0) q0 = wd;
+      else if (q1 < 0) q1 = wd;
+      else if (q2 < 0) q2 = wd;
+      else {
+        q3 = wd;
+        flush();
+      }
+#else
       const int b = wd * 64 + lane;
       const int c = b < d.H ? __hip_atomic_load(&cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
       const unsigned long long bits = __ballot(c > 0);
       if (lane == 0) occ[wd] = bits;
+#endif
     }
   }
+#if AIGAR_OCC_BATCH
+  if (q0 >= 0) flush();
+#endif
 }
 
 // one wavefront per player: cells with an overlapping enemy cell at phase start
@@ -2968,17 +3004,19 @@ constexpr int PPG_SEEDS = 64;  // most pending players for the parallel pass
 constexpr int PPG_PL = 16;     // players per closure
 constexpr int PPG_CELLS = 64;  // cells per closure (also the turn candidate cap)
 #ifndef AIGAR_PPG_WAVES
-#define AIGAR_PPG_WAVES 8
+#define AIGAR_PPG_WAVES 16
 #endif
 constexpr int PPG_WAVES = AIGAR_PPG_WAVES;  // wavefronts running groups
+#ifndef AIGAR_PP_MERGE
+#define AIGAR_PP_MERGE 1  // closures sharing a player merge instead of falling back
+#endif
 constexpr int PPG_MIN = 3;     // fewer pending players: the serial pass (closures cost ~10 us)
-__device__ __forceinline__ bool pp_closure(const Dev &d, int a, int P, int *pl, int &npl) {
+// (pl[0..npl): the starting players -- a seed, or merged closures)
+__device__ __forceinline__ bool pp_closure(const Dev &d, int a, int *pl, int &npl) {
   const int lane = threadIdx.x & 63, NP = d.NP, B = d.B;
   const int *st = d.cstart + (size_t)a * (d.H + 1);
   const int *it = d.citems + (size_t)a * kMaxCells * B;
   const double rmax0 = d.ctl[a].rmax_cell;
-  if (lane == 0) pl[0] = P;
-  npl = 1;
   wave_fence();
   for (int iter = 0; iter < 8; iter++) {
     // the group's cells: (player j, slot k) pairs, four per lane, one load round
@@ -3105,8 +3143,9 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   __syncthreads();
   for (int sd = w; sd < nw; sd += nwv) {
     const int P = d.work[(size_t)a * d.Wcap + sd];
-    int npl = 0;
-    const bool ok = pp_closure(d, a, P, s_pl[sd], npl);
+    if (lane == 0) s_pl[sd][0] = P;
+    int npl = 1;
+    const bool ok = pp_closure(d, a, s_pl[sd], npl);
     if (lane == 0) s_npl[sd] = ok ? npl : 0;
     if (!ok) {
       if (lane == 0) s_bad = 1;
@@ -3115,10 +3154,73 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     for (int j = lane; j < npl; j += 64) atomicMin(&pown[s_pl[sd][j]], sd);
   }
   __syncthreads();
+#if AIGAR_PP_MERGE
+  // closures that share a player merge: their seeds' components (label = the
+  // lowest seed, propagated along every shared player to a fixed point), each
+  // component's players united in its root's list and closed again from there;
+  // the groups are then the roots' closures, checked pairwise disjoint as above
+  __shared__ int s_lab[PPG_SEEDS], s_root[PPG_SEEDS];
+  if (!s_bad) {
+    for (int i = tid; i < nw; i += T) s_lab[i] = i;
+    __syncthreads();
+    for (int iter = 0; iter < PPG_SEEDS; iter++) {
+      int chg = 0;
+      for (int sd = w; sd < nw; sd += nwv)
+        for (int j = lane; j < s_npl[sd]; j += 64) {
+          const int o = __hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (o == sd) continue;
+          const int lo = min(s_lab[sd], s_lab[o]);
+          chg |= atomicMin(&s_lab[sd], lo) > lo;
+          chg |= atomicMin(&s_lab[o], lo) > lo;
+        }
+      if (!__syncthreads_or(chg)) break;
+    }
+    for (int i = tid; i < nw; i += T) s_root[i] = s_lab[i];
+    __syncthreads();
+    for (int rt = w; rt < nw; rt += nwv) {
+      if (s_root[rt] != rt) continue;
+      int npl = s_npl[rt];
+      bool more = false;
+      for (int sd = rt + 1; sd < nw && npl <= PPG_PL; sd++) {
+        if (s_root[sd] != rt) continue;
+        more = true;
+        for (int j = 0; j < s_npl[sd] && npl <= PPG_PL; j++) {
+          const int q = s_pl[sd][j];
+          bool dup = false;
+          for (int k = lane; k < npl; k += 64) dup |= s_pl[rt][k] == q;
+          if (__ballot(dup)) continue;
+          if (npl < PPG_PL && lane == 0) s_pl[rt][npl] = q;
+          npl++;
+          wave_fence();
+        }
+      }
+      if (!more) continue;
+      bool ok = npl <= PPG_PL;
+      if (ok) ok = pp_closure(d, a, s_pl[rt], npl);
+      if (lane == 0) s_npl[rt] = ok ? npl : 0;
+      if (!ok && lane == 0) s_bad = 1;
+    }
+    __syncthreads();
+    if (!s_bad) {
+      for (int i = tid; i < d.B; i += T) __hip_atomic_store(&pown[i], INT_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      for (int rt = w; rt < nw; rt += nwv)
+        if (s_root[rt] == rt)
+          for (int j = lane; j < s_npl[rt]; j += 64) atomicMin(&pown[s_pl[rt][j]], rt);
+      __syncthreads();
+    }
+  }
+  if (!s_bad)
+    for (int sd = w; sd < nw; sd += nwv)
+      if (s_root[sd] == sd)
+        for (int j = lane; j < s_npl[sd]; j += 64)
+          if (__hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sd) s_bad = 1;
+#else
   if (!s_bad)
     for (int sd = w; sd < nw; sd += nwv)
       for (int j = lane; j < s_npl[sd]; j += 64)
         if (__hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sd) s_bad = 1;
+#endif
   __syncthreads();
   PT_MARK(5, 6);
   if (tid == 0) PP_DIAG(s_bad ? 5 : 6);
@@ -3131,10 +3233,23 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     uint32_t *mine = pend + (size_t)w * NW;
     for (int i = lane; i < NW; i += 64) mine[i] = 0;
     wave_fence();
+#if AIGAR_PP_MERGE
+    // group g (the g-th root) runs in wave g % PPG_WAVES: every seed of it
+    for (int sd = 0; sd < nw; sd++) {
+      const int rt = s_root[sd];
+      int g = 0;
+      for (int k = lane; k < rt; k += 64) g += s_root[k] == k;
+      for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
+      if (g % PPG_WAVES != w) continue;
+      const int P = d.work[(size_t)a * d.Wcap + sd];
+      if (lane == 0) mine[P >> 5] |= 1u << (P & 31);
+    }
+#else
     for (int sd = w; sd < nw; sd += PPG_WAVES) {
       const int P = d.work[(size_t)a * d.Wcap + sd];
       if (lane == 0) mine[P >> 5] |= 1u << (P & 31);
     }
+#endif
     wave_fence();
     double rmax = c.rmax_cell;
     pp_turns(d, a, mine, PPL{g_key[w], g_val[w], g_srt[w], g_x[w], g_y[w], g_m[w], g_r[w], PPG_CELLS}, odirty,
