@@ -19,6 +19,9 @@
 #include "aigar_sem.h"
 #include "aigar_wave.h"
 
+#ifndef AIGAR_OBS_PAIR
+#define AIGAR_OBS_PAIR 1  // the fast path scans each list once for both of a lane's squares
+#endif
 namespace aigar {
 
 #define GTID ((int)(blockIdx.x * blockDim.x + threadIdx.x))
@@ -536,7 +539,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // The per-square scans read list entry k through accessors: PEL(k) -> (mass,
   // mask) of the k-th pellet in creation order, CEL(k) -> (mass, mask, own),
   // VIR(k) -> (radius, mass, seq, mask).
-  auto squares = [&](auto hist_regs, auto PEL, auto CEL, auto VIR) __attribute__((always_inline)) {
+  // pre (true_type): the scans ran already for both of the lane's squares
+  // (squares t = lane, lane + 64: one pass over each list, vp0 / vp1 ...)
+  double vp0 = 0, vp1 = 0, vs0 = 0, vs1 = 0, ve0 = 0, ve1 = 0, vv0 = 0, vv1 = 0;
+  auto squares = [&](auto hist_regs, auto pre, auto PEL, auto CEL, auto VIR) __attribute__((always_inline)) {
   for (int t = lane; t < GG; t += 64) {
     const int c = idiv(t, G, inv_G), r = t - c * G;
     double mx, my;
@@ -553,7 +559,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     uint32_t need = (1u << ix) | (1u << (16 + iy));
     double vp = 0, ve = 0, vs = 0, vv = 0;
     bool within = !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
-    if (within && ix < 16) {
+    if constexpr (decltype(pre)::value) {
+      vp = t < 64 ? vp0 : vp1;
+      vs = t < 64 ? vs0 : vs1;
+      ve = t < 64 ? ve0 : ve1;
+      vv = t < 64 ? vv0 : vv1;
+    } else if (within && ix < 16) {
       double s = 0;
       bool anyp = false;
       for (int k = 0; k < np; k++) {  // creation order
@@ -661,8 +672,80 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     const double rvr = lane < nv ? v_rad[lane] : 0.0, rvm = lane < nv ? v_mass[lane] : 0.0;
     const int64_t rvs = lane < nv ? v_seqs[lane] : 0;
     const uint32_t rvk = lane < nv ? v_mask[lane] : 0u;
+#if AIGAR_OBS_PAIR
+    if (GG > 64) {  // both squares of a lane in one pass over each list
+      bool ok0, ok1;
+      uint32_t nd0, nd1;
+      {
+        auto sq = [&](int t, bool &ok, uint32_t &need) {
+          const int c = idiv(t, G, inv_G), r = t - c * G;
+          const double mx = __shfl(colx, r), my = __shfl(rowy, c);
+          const int iy = idiv(t, cols, inv_cols), ix = t - iy * cols;
+          need = (1u << ix) | (1u << (16 + iy));
+          ok = t < GG && ix < 16 &&
+               !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
+        };
+        sq(lane, ok0, nd0);
+        sq(lane + 64, ok1, nd1);
+      }
+      double s0 = 0, s1 = 0;
+      bool a0 = false, a1 = false;
+      for (int k = 0; k < np; k++) {  // creation order
+        const double m = readlane_d(rpm, k);
+        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)rpk, k);
+        const bool h0 = ok0 && (mk & nd0) == nd0, h1 = ok1 && (mk & nd1) == nd1;
+        s0 = h0 ? s0 + m : s0;
+        s1 = h1 ? s1 + m : s1;
+        a0 |= h0;
+        a1 |= h1;
+      }
+      vp0 = a0 ? s0 : 0.0;
+      vp1 = a1 ? s1 : 0.0;
+      bool fe0 = false, fo0 = false, fe1 = false, fo1 = false;
+      for (int k = 0; k < nc; k++) {
+        const double m = readlane_d(rcm, k);
+        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)rck, k);
+        const bool own = __builtin_amdgcn_readlane(rco, k) != 0;
+        const bool h0 = ok0 && (mk & nd0) == nd0, h1 = ok1 && (mk & nd1) == nd1;
+        if (own) {
+          if (h0 && (!fo0 || m > vs0)) vs0 = m;
+          if (h1 && (!fo1 || m > vs1)) vs1 = m;
+          fo0 |= h0;
+          fo1 |= h1;
+        } else {
+          if (h0 && (!fe0 || m > ve0)) ve0 = m;
+          if (h1 && (!fe1 || m > ve1)) ve1 = m;
+          fe0 |= h0;
+          fe1 |= h1;
+        }
+      }
+      bool fv0 = false, fv1 = false;
+      double br0 = 0, br1 = 0;
+      int64_t bs0 = 0, bs1 = 0;
+      for (int k = 0; k < nv; k++) {
+        const double rr = readlane_d(rvr, k), vmk = readlane_d(rvm, k);
+        const int64_t sq = readlane_i64(rvs, k);
+        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)rvk, k);
+        const bool h0 = ok0 && (mk & nd0) == nd0, h1 = ok1 && (mk & nd1) == nd1;
+        if (h0 && (!fv0 || rr > br0 || (rr == br0 && sq < bs0))) {
+          br0 = rr;
+          bs0 = sq;
+          vv0 = vmk;
+        }
+        if (h1 && (!fv1 || rr > br1 || (rr == br1 && sq < bs1))) {
+          br1 = rr;
+          bs1 = sq;
+          vv1 = vmk;
+        }
+        fv0 |= h0;
+        fv1 |= h1;
+      }
+      auto none = [](auto...) {};
+      squares(std::true_type{}, std::true_type{}, none, none, none);
+    } else
+#endif
     squares(
-        std::true_type{},
+        std::true_type{}, std::false_type{},
         [&](int k, double &m, uint32_t &mk) {
           m = readlane_d(rpm, k);
           mk = (uint32_t)__builtin_amdgcn_readlane((int)rpk, k);
@@ -683,7 +766,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     const uint32_t *pk = in_lds ? smk : PL.mask;
     const int *pperm = in_lds ? nullptr : PL.perm;
     squares(
-        std::false_type{},
+        std::false_type{}, std::false_type{},
         [&](int k, double &m, uint32_t &mk) {
           const int e = pperm ? pperm[k] : k;
           m = pm[e];
