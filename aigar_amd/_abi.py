@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 RNG_PHILOX = 0
 RNG_MT19937 = 1
@@ -22,6 +22,7 @@ EV_CELL_EAT_PELLET, EV_CELL_EAT_BLOB, EV_CELL_EAT_CELL, EV_PLAYER_DEATH, EV_RESP
 
 FLAG_EVENTS = 0x1
 TILE_OWNED_ONLY = 0x1
+TILE_FORCE = 0x2  # a 1 x 1 tiled handle (the whole field one tile: the one-GPU test of the exchange path)
 
 
 POLICY_NONE, POLICY_RANDOM, POLICY_GREEDY = 0, 1, 2

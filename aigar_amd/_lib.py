@@ -36,6 +36,28 @@ def _preload_single_hip_runtime():
     return None
 
 
+def rccl_path():
+    """The librccl.so this process's torch uses (one HIP runtime for both), else None
+    (the loader's librccl.so)."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is not None and spec.submodule_search_locations:
+        cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "librccl.so")
+        if os.path.exists(cand):
+            return cand
+    return None
+
+
+def rccl_unique_id():
+    """A fresh ncclUniqueId (128 bytes) for aigar_tile_comm_init (rank 0 makes it)."""
+    L = load()
+    buf = C.create_string_buffer(128)
+    path = rccl_path()
+    if L.aigar_rccl_unique_id(path.encode() if path else None, buf) < 0:
+        raise RuntimeError("aigar: " + L.aigar_last_error().decode())
+    return buf.raw
+
+
 def load(build_if_missing=False):
     global _lib
     if _lib is not None:
@@ -63,6 +85,7 @@ def load(build_if_missing=False):
         "aigar_observe": [vp, vp, i32, i32],
         "aigar_observe_pixels": [vp, vp, i32, u64, i32, i32],
         "aigar_set_actions": [vp, vp, vp, i32],
+        "aigar_reset_bots": [vp, vp, i32],
         "aigar_player_stats": [vp, vp, i32],
         "aigar_get_state": [vp, i32, C.POINTER(_abi.State)],
         "aigar_load_state": [vp, i32, C.POINTER(_abi.State)],
@@ -93,6 +116,10 @@ def load(build_if_missing=False):
         "aigar_tile_end": [vp, vp, i32],
         "aigar_tile_exchange_local": [C.POINTER(vp), i32],
         "aigar_tile_observers": [vp, C.POINTER(C.c_int32)],
+        "aigar_rccl_unique_id": [C.c_char_p, vp],
+        "aigar_tile_comm_init": [vp, C.c_char_p, vp, i32, i32],
+        "aigar_tile_run": [vp, i32, C.POINTER(_abi.RunParams), i32, vp, i32],
+        "aigar_tile_run_graphed": [vp],
     }
     for name, args in sig.items():
         f = getattr(L, name, None)
@@ -311,6 +338,14 @@ class Stepper:
         q = None if prev is None else np.ascontiguousarray(prev, np.float64)
         self._chk(self.L.aigar_set_actions(self.h, _ptr(c)[0], _ptr(q)[0], 0))
 
+    def reset_bots(self, mask=None):
+        """Bot.reset's device half (bot.py:125-164) for the players where mask != 0
+        (all if None): history grids zeroed, lastFovSize 0."""
+        if isinstance(mask, np.ndarray):
+            mask = np.ascontiguousarray(mask, np.uint8).reshape(self.NP)
+        p, dev = _ptr(mask)
+        self._chk(self.L.aigar_reset_bots(self.h, p, dev))
+
     def player_stats(self):
         out = np.zeros((self.NP, 5), np.float64)
         self._chk(self.L.aigar_player_stats(self.h, out.ctypes.data_as(C.c_void_p), 0))
@@ -388,6 +423,28 @@ class Stepper:
 
     def tile_resume(self):
         self._chk(self.L.aigar_tile_resume(self.h))
+
+    def tile_comm_init(self, uid, nranks, rank):
+        """This tile's RCCL communicator (ncclCommInitRank): nranks = tiles, rank = tile id."""
+        path = rccl_path()
+        buf = C.create_string_buffer(bytes(uid), 128)
+        self._chk(self.L.aigar_tile_comm_init(self.h, path.encode() if path else None, buf, int(nranks), int(rank)))
+
+    def tile_run(self, n=1, policy="random", out=None, p_split=0.0, p_eject=0.0, seed=0, extra_passes=0):
+        """n tiled steps over RCCL (aigar_tile_run): policy + the tick with its all-gathered
+        eat passes + the observation of this tile's bots into the DEVICE tensor out."""
+        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM}[policy]
+        prm = _abi.RunParams(pol, 0, float(p_split), float(p_eject), int(seed))
+        p, dt = None, 0
+        if out is not None:
+            if not getattr(out, "is_cuda", False) or tuple(out.shape) != (self.NP, self.obs_len):
+                raise ValueError("tile_run writes observations to a device tensor [%d, %d]" % (self.NP, self.obs_len))
+            dt = 0 if str(out.dtype) == "torch.float64" else 1
+            p = C.c_void_p(out.data_ptr())
+        self._chk(self.L.aigar_tile_run(self.h, int(n), C.byref(prm), int(extra_passes), p, dt))
+
+    def tile_run_graphed(self):
+        return bool(self.L.aigar_tile_run_graphed(self.h))
 
     def tile_end(self, out=None):
         p, dt = None, 0

@@ -80,7 +80,8 @@ struct ArenaCtl {
   // tile ate this tick, this pass's outbox fill / pellet kills / undone owned
   // cells, and the undone owned cells of all tiles after the last exchange
   int n_pel_glob, n_eaten_glob, n_out, n_out_pel, n_undone, n_undone_glob;
-  int n_ho;  // observation history hand-off slots in this tile's first-pass message
+  int n_ho;       // observation history hand-off slots in this tile's first-pass message (dead bots first)
+  int n_ho_live;  // live bots whose view centre left this tile: hand-off candidates (t_holive)
   // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
   // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
   int64_t stat[8];
@@ -91,7 +92,8 @@ enum : uint32_t {
   ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256, ERR_TILE_CAP = 512, ERR_TILE_LOOKUP = 1024,
   ERR_TILE_OBS = 2048,    // a tile observed a bot whose view reaches beyond its held pellets
   ERR_TILE_PASSES = 4096,  // a device-bounded tiled tick ended with owned cells undone
-  ERR_PREDICT = 8192       // updatePlayers made other counts than k_tick_begin predicted (head_counts)
+  ERR_PREDICT = 8192,      // updatePlayers made other counts than k_tick_begin predicted (head_counts)
+  ERR_TILE_HANDOFF = 16384  // more dead bots to hand off in one tick than a message has hand-off slots
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
@@ -150,6 +152,7 @@ struct Dev {
   int hcap, hrec, nh;  // hand-off slots per message, records per slot, history grids per bot (0..4)
   int *t_holder;  // [NP] tile holding the bot's current observation history, -1: every tile
   int *t_obsby;   // [NP] tile that observed the bot since the last plan, -1: none
+  int *t_holive;  // [hcap] live bots waiting for a hand-off slot this tick (slots left after the dead ones)
   int own_bx0, own_bx1, own_by0, own_by1;      // owned centre buckets [x0, x1) x [y0, y1)
   int loc_bx0, loc_bx1, loc_by0, loc_by1;      // held pellets: owned range + halo
   TileRec *outbox;       // [1 + tcap] records + bitmap

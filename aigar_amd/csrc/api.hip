@@ -1,4 +1,5 @@
 // api.hip -- host implementation of include/aigar.h (libaigar_hip.so).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -56,6 +57,39 @@ static int fail(const char *fmt, ...) {
     if (e_ != hipSuccess) return fail("%s failed: %s", #x, hipGetErrorString(e_));       \
   } while (0)
 
+// librccl.so, bound at run time (C4 over RCCL, below)
+namespace {
+struct RcclId {
+  char b[128];  // ncclUniqueId (rccl.h: NCCL_UNIQUE_ID_BYTES)
+};
+constexpr int kNcclUint8 = 1;  // ncclDataType_t ncclUint8 (rccl.h)
+struct Rccl {
+  void *so = nullptr;
+  int (*get_unique_id)(RcclId *) = nullptr;
+  int (*comm_init_rank)(void **, int, RcclId, int) = nullptr;
+  int (*all_gather)(const void *, void *, size_t, int, void *, hipStream_t) = nullptr;
+  int (*comm_destroy)(void *) = nullptr;
+  const char *(*error_string)(int) = nullptr;
+};
+Rccl g_rccl;
+int rccl_load(const char *path) {
+  if (g_rccl.so) return 0;
+  void *so = dlopen(path && *path ? path : "librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!so) return fail("RCCL: dlopen(%s) failed: %s", path ? path : "librccl.so", dlerror());
+  Rccl r;
+  r.so = so;
+  r.get_unique_id = (int (*)(RcclId *))dlsym(so, "ncclGetUniqueId");
+  r.comm_init_rank = (int (*)(void **, int, RcclId, int))dlsym(so, "ncclCommInitRank");
+  r.all_gather = (int (*)(const void *, void *, size_t, int, void *, hipStream_t))dlsym(so, "ncclAllGather");
+  r.comm_destroy = (int (*)(void *))dlsym(so, "ncclCommDestroy");
+  r.error_string = (const char *(*)(int))dlsym(so, "ncclGetErrorString");
+  if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy || !r.error_string)
+    return fail("RCCL: %s lacks an nccl* entry point", path ? path : "librccl.so");
+  g_rccl = r;
+  return 0;
+}
+}  // namespace
+
 struct aigar_handle {
   aigar_config cfg;
   Dev d;
@@ -104,6 +138,15 @@ struct aigar_handle {
   // 1-GPU gloo rehearsal, so off by default
   bool tile_graph = false;
   bool graph_failed = false;
+  // C4 over RCCL (aigar_tile_comm_init / aigar_tile_run)
+  void *rccl_comm = nullptr;
+  int rccl_ranks = 0;
+  bool rccl_bad = false;  // an all-gather failed while a graph was captured
+  hipGraphExec_t tr_graph = nullptr;
+  aigar_run_params tr_key{};
+  void *tr_out = nullptr;
+  int tr_dtype = -2, tr_extra = -1;
+  bool tr_failed = false;
   // aigar_run: one whole env step (policy + Field.update + observation) as a graph
   hipGraphExec_t run_graph = nullptr;
   aigar_run_params run_key{};
@@ -180,6 +223,9 @@ static void free_all(aigar_handle *h) {
   if (h->ev_x) (void)hipEventDestroy(h->ev_x);
   if (h->tb_graph) (void)hipGraphExecDestroy(h->tb_graph);
   if (h->te_graph) (void)hipGraphExecDestroy(h->te_graph);
+  if (h->tr_graph) (void)hipGraphExecDestroy(h->tr_graph);
+  if (h->rccl_comm && g_rccl.comm_destroy) (void)g_rccl.comm_destroy(h->rccl_comm);
+  h->rccl_comm = nullptr;
   for (auto &m : h->marks) {
     (void)hipEventDestroy(m.second.first);
     (void)hipEventDestroy(m.second.second);
@@ -266,7 +312,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   // C4 tiles: bucket-aligned tiles, ownership by centre bucket
   const int tx = std::max(1, cfg->tile_x), ty = std::max(1, cfg->tile_y);
   d.ntiles = tx * ty;
-  d.tiled = d.ntiles > 1;
+  d.tiled = d.ntiles > 1 || (cfg->tile_flags & AIGAR_TILE_FORCE);
   d.own_bx0 = d.own_by0 = d.loc_bx0 = d.loc_by0 = 0;
   d.own_bx1 = d.own_by1 = d.loc_bx1 = d.loc_by1 = d.cols;
   if (d.tiled) {
@@ -394,6 +440,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   if (d.tiled) {
     AL(t_holder, int, NP);
     AL(t_obsby, int, NP);
+    AL(t_holive, int, d.hcap);
     AL(outbox, TileRec, h->box_recs);
     TileRec *ib = nullptr;
     ib = dalloc<TileRec>(h, (size_t)h->box_recs * d.ntiles);
@@ -453,7 +500,8 @@ static int check_device_errors(aigar_handle *h) {
       return fail("device error bits 0x%x in arena %d (1 pellet cap, 2 blob cap, 4 virus cap, 8 event cap, "
                   "16 worklist cap, 32 observation cap, 64 candidate cap, 128 slot, 256 pixel-frame object cap, "
                   "512 tile message cap, 1024 tile record lookup, 2048 tile view beyond the held pellets, "
-                  "4096 tiled tick ended with undone cells, 8192 new-cell / blob counts not as predicted)",
+                  "4096 tiled tick ended with undone cells, 8192 new-cell / blob counts not as predicted, "
+                  "16384 more dead bots to hand off than hand-off slots)",
                   ctl[a].err, a);
   return 0;
 }
@@ -610,7 +658,7 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
 // ---------------------------------------------------------------- C4 tiles
 static int need_tiled(aigar_handle *h) {
   if (!h) return fail("null handle");
-  if (!h->d.tiled) return fail("not a tiled handle (tile_x * tile_y must be > 1)");
+  if (!h->d.tiled) return fail("not a tiled handle (tile_x * tile_y must be > 1, or AIGAR_TILE_FORCE)");
   return 0;
 }
 extern "C" int aigar_tile_info(aigar_handle *h, int32_t *info, void **outbox, void **inbox, int64_t *msg_bytes) {
@@ -777,6 +825,133 @@ extern "C" int aigar_tile_exchange_local(aigar_handle **hs, int n) {
   }
   return 0;
 }
+
+// ---------------------------------------------------------------- C4 over RCCL
+// The exchange is ncclAllGather over the tiles' communicator (xGMI between the
+// GPUs of a node).  librccl.so is bound at run time (dlopen of the file the
+// caller names -- torch's, so one HIP runtime serves both -- and dlsym of the
+// five entry points used); the library itself does not link RCCL.
+
+extern "C" int aigar_rccl_unique_id(const char *path, void *id) {
+  if (!id) return fail("null argument");
+  if (rccl_load(path)) return -1;
+  RcclId u;
+  const int r = g_rccl.get_unique_id(&u);
+  if (r) return fail("ncclGetUniqueId: %s", g_rccl.error_string(r));
+  memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+extern "C" int aigar_tile_comm_init(aigar_handle *h, const char *path, const void *id, int nranks, int rank) {
+  if (need_tiled(h)) return -1;
+  if (!id) return fail("null argument");
+  if (nranks != h->d.ntiles || rank != h->d.tile_id)
+    return fail("tile_comm_init: %d ranks / rank %d for %d tiles / tile %d (one rank per tile, rank = tile id)",
+                nranks, rank, h->d.ntiles, h->d.tile_id);
+  if (rccl_load(path)) return -1;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->rccl_comm) {
+    (void)g_rccl.comm_destroy(h->rccl_comm);
+    h->rccl_comm = nullptr;
+  }
+  RcclId u;
+  memcpy(&u, id, sizeof u);
+  const int r = g_rccl.comm_init_rank(&h->rccl_comm, nranks, u, rank);
+  if (r) {
+    h->rccl_comm = nullptr;
+    return fail("ncclCommInitRank(%d ranks, rank %d): %s", nranks, rank, g_rccl.error_string(r));
+  }
+  h->rccl_ranks = nranks;
+  return 0;
+}
+
+// every tile's current-pass message into every tile's inbox (tile k at k * bytes)
+static int tile_allgather(aigar_handle *h, hipStream_t s, int recs) {
+  const int r = g_rccl.all_gather(h->d.outbox, (void *)h->d.inbox, (size_t)recs * sizeof(TileRec), kNcclUint8,
+                                  h->rccl_comm, s);
+  if (r) {
+    h->rccl_bad = true;
+    return fail("ncclAllGather: %s", g_rccl.error_string(r));
+  }
+  return 0;
+}
+
+// One tiled step (the rank-side sequence of include/aigar.h's aigar_tile_* calls)
+static int issue_tile_step(aigar_handle *h, hipStream_t s, const aigar_run_params &p, int extra, void *obs,
+                           int dtype) {
+  const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
+  const int first_recs = 1 + h->d.tcap + h->d.hcap * h->d.hrec, later_recs = 1 + h->d.tcap + h->d.bm_words / 4;
+  {
+    Mark m(h, "tile_begin");
+    launch_tick_pre(h->d, s, h->scr_k, h->scr_v, &rp);
+    launch_tile_pass(h->d, s, h->rounds, h->scr_k, h->scr_v, 1);
+  }
+  for (int k = 0; k <= extra; k++) {
+    {
+      Mark m(h, "exchange");
+      if (tile_allgather(h, s, k == 0 ? first_recs : later_recs)) return -1;
+    }
+    {
+      Mark m(h, "tile_apply");
+      launch_tile_apply(h->d, s, k == 0 ? first_recs : later_recs, k == 0 ? 1 : 0);
+    }
+    if (k < extra) {
+      Mark m(h, "tile_resume");
+      launch_tile_pass(h->d, s, h->rounds, h->scr_k, h->scr_v, 0);
+    }
+  }
+  {
+    Mark m(h, "tile_end");
+    launch_tick_post(h->d, s, h->scr_k, h->scr_v);
+  }
+  if (obs) {
+    Mark m(h, "observe");
+    launch_observe(h->d, s, obs, dtype, 0);
+  }
+  return 0;
+}
+
+extern "C" int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_params *p, int extra_passes,
+                              void *obs_out, int dtype) {
+  if (need_tiled(h) || !p) return p ? -1 : fail("null argument");
+  if (!h->rccl_comm) return fail("tile_run: no RCCL communicator (aigar_tile_comm_init)");
+  if (n_steps < 0 || extra_passes < 0 || extra_passes > 64) return fail("tile_run: bad n_steps / extra_passes");
+  if (p->policy != AIGAR_POLICY_NONE && p->policy != AIGAR_POLICY_RANDOM)
+    return fail("tile_run: policy must be NONE or RANDOM (the greedy policy reads pellets other tiles hold)");
+  if (obs_out && dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every call (all n_steps accumulate)
+    hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, h->stream, h->d);
+  h->pass_recs = 0;  // (the aigar_tile_* call sequence restarts at a tile_begin)
+  const bool same = h->tr_graph && memcmp(&h->tr_key, p, sizeof *p) == 0 && h->tr_out == obs_out &&
+                    h->tr_dtype == (obs_out ? dtype : -1) && h->tr_extra == extra_passes;
+  if (h->use_graph && !h->profile && !same && !h->tr_failed && n_steps > 0) {
+    if (h->tr_graph) (void)hipGraphExecDestroy(h->tr_graph);
+    h->rccl_bad = false;
+    h->tr_graph = capture_graph(h, [&](hipStream_t cs) { (void)issue_tile_step(h, cs, *p, extra_passes, obs_out, dtype); });
+    if (h->rccl_bad && h->tr_graph) {  // an all-gather refused the capture: direct launches from now on
+      (void)hipGraphExecDestroy(h->tr_graph);
+      h->tr_graph = nullptr;
+    }
+    if (!h->tr_graph) h->tr_failed = true;
+    h->tr_key = *p;
+    h->tr_out = obs_out;
+    h->tr_dtype = obs_out ? dtype : -1;
+    h->tr_extra = extra_passes;
+  }
+  for (int t = 0; t < n_steps; t++) {
+    if (h->tr_graph && !h->profile) {
+      Mark m(h, "tile_step");
+      HIPCHK(hipGraphLaunch(h->tr_graph, h->stream));
+    } else if (issue_tile_step(h, h->stream, *p, extra_passes, obs_out, dtype)) {
+      return -1;
+    }
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int aigar_tile_run_graphed(aigar_handle *h) { return h && h->tr_graph ? 1 : 0; }
 
 // the tile that computed each bot's row at the last observation (-1: dead /
 // not observed); every tile computes the same assignment
@@ -971,6 +1146,38 @@ extern "C" int aigar_set_actions(aigar_handle *h, const double *cur, const doubl
     if (prev) HIPCHK(hipMemcpyAsync(h->d.o_act_prev, prev, n * 8, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
   }
+  return 0;
+}
+
+// Bot.reset (bot.py:125-164) for the masked players: an NN bot's last /
+// second-last self and enemy grids restart at zero and fovSize / lastFovSize at
+// 0 (the collector calls model.resetBots() every FRAME_SKIP_RATE + 2 updates,
+// aigar.py:845-852).  C4: every tile's copy is then current (all zero).
+__global__ void k_reset_bots(Dev d, const uint8_t *mask) {
+  const int GG = d.G * d.G;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= (size_t)d.NP * GG) return;
+  const int gp = (int)(i / GG);
+  if (mask && !mask[gp]) return;
+  d.o_self_lf[i] = d.o_self_slf[i] = d.o_en_lf[i] = d.o_en_slf[i] = 0.0;
+  if (i % GG == 0) {
+    d.o_lastfov[gp] = 0.0;
+    if (d.tiled) d.t_holder[gp] = -1;
+  }
+}
+
+extern "C" int aigar_reset_bots(aigar_handle *h, const uint8_t *mask, int on_device) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const uint8_t *m = mask;
+  if (mask && !on_device) {
+    HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)h->d.NP, hipMemcpyHostToDevice, h->stream));
+    m = h->d_mask;
+  }
+  const size_t n = (size_t)h->d.NP * h->d.G * h->d.G;
+  hipLaunchKernelGGL(k_reset_bots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->d, m);
+  HIPCHK(hipGetLastError());
+  if (mask && !on_device) HIPCHK(hipStreamSynchronize(h->stream));  // caller may reuse its buffer
   return 0;
 }
 

@@ -661,13 +661,30 @@ __device__ void tick_zero(const Dev &d, int gi) {
 // threads of k_tick_begin, one per player.  A bot's history is current on
 // t_holder (-1: on every tile), or on the tile that observed it since the last
 // plan (t_obsby) -- that update is replicated, every tile makes it.  The holder
-// hands the history off when the bot is dead (it respawns anywhere) or its
-// view centre (the FOV cache, end of the last tick) lies in another tile: it
-// takes a slot of its first-pass message (at most hcap per tick, in any order;
-// the rest wait a tick) and drops the bot (t_holder := -1); every other tile
-// does the same for the slots it receives (k_tile_apply), so the holders stay
-// identical on every tile.  Otherwise the holder observes the bot again: its
-// centre moved at most one tick's distance from the tile, which the halo covers.
+// hands the history off when the bot is dead (it respawns anywhere at the end of
+// this tick) or its view centre (the FOV cache, end of the last tick) lies in
+// another tile, in a slot of its first-pass message; every other tile drops the
+// holder for the slots it receives (k_tile_apply), so the holders stay identical
+// on every tile.  Dead bots come first: they take slots here (more than hcap in
+// one tick is ERR_TILE_HANDOFF, never a silent deferral -- the stale holder could
+// not observe a bot respawned outside its pellets).  Live bots only queue here
+// (t_holive); tile_plan_live, in the message's last block, gives them the slots
+// the dead left, and the rest keep their holder a tick longer: their centre moved
+// at most one tick's distance from the tile, which the halo covers.
+__device__ void tile_hist_slot(const Dev &d, int gp, int sl) {
+  const int GG = d.G * d.G;
+  TileRec *slot = d.outbox + 1 + d.tcap + (size_t)sl * d.hrec;
+  slot->kind = TR_HIST;
+  slot->idx = gp;
+  slot->seq = 0;
+  slot->x = d.o_lastfov[gp];
+  slot->y = 0;
+  double *dst = (double *)(slot + 1);
+  for (int g = 0; g < d.nh; g++) {
+    const double *src = hist_grid(d, g) + (size_t)gp * GG;
+    for (int t = 0; t < GG; t++) dst[g * GG + t] = src[t];
+  }
+}
 __device__ void tile_plan_thread(const Dev &d, int gp) {
   ArenaCtl &c = d.ctl[0];
   if (gp == 0) {  // the first pass's counters
@@ -683,22 +700,39 @@ __device__ void tile_plan_thread(const Dev &d, int gp) {
     d.t_holder[gp] = h;
   }
   if (h != d.tile_id) return;
-  if (d.p_alive[gp] && tile_of(d, d.p_fx[gp], d.p_fy[gp]) == h) return;
-  const int sl = atomicAdd(&c.n_ho, 1);
-  if (sl >= d.hcap) return;  // (the header clamps the slot count)
-  d.t_holder[gp] = -1;
-  const int GG = d.G * d.G;
-  TileRec *slot = d.outbox + 1 + d.tcap + (size_t)sl * d.hrec;
-  slot->kind = TR_HIST;
-  slot->idx = gp;
-  slot->seq = 0;
-  slot->x = d.o_lastfov[gp];
-  slot->y = 0;
-  double *dst = (double *)(slot + 1);
-  for (int g = 0; g < d.nh; g++) {
-    const double *src = hist_grid(d, g) + (size_t)gp * GG;
-    for (int t = 0; t < GG; t++) dst[g * GG + t] = src[t];
+  if (d.p_alive[gp]) {
+    if (tile_of(d, d.p_fx[gp], d.p_fy[gp]) == h) return;
+    const int q = atomicAdd(&c.n_ho_live, 1);
+    if (q < d.hcap) d.t_holive[q] = gp;
+    return;
   }
+  const int sl = atomicAdd(&c.n_ho, 1);
+  if (sl >= d.hcap) {
+    set_err(d, 0, ERR_TILE_HANDOFF);
+    return;
+  }
+  d.t_holder[gp] = -1;
+  tile_hist_slot(d, gp, sl);
+}
+// the live bots' hand-offs, in the slots the dead left (one block, first pass;
+// lowest player index first, so the choice does not depend on atomic order)
+__device__ void tile_plan_live(const Dev &d) {
+  ArenaCtl &c = d.ctl[0];
+  __shared__ int s_q[kHcapMax];
+  const int nd = min(c.n_ho, d.hcap), nq = min(c.n_ho_live, d.hcap), room = d.hcap - nd;
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) s_q[i] = d.t_holive[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {  // rank by player index
+    const int gp = s_q[i];
+    int r = 0;
+    for (int j = 0; j < nq; j++) r += s_q[j] < gp;
+    if (r < room) {
+      d.t_holder[gp] = -1;
+      tile_hist_slot(d, gp, nd + r);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) c.n_ho = nd + min(nq, room);
 }
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   FLOOR(0);
@@ -4175,6 +4209,7 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
   c.n_pel_glob = c.n_eaten_glob = c.n_out = c.n_out_pel = c.n_undone = c.n_undone_glob = 0;
+  c.n_ho = c.n_ho_live = 0;
   for (int k = 0; k < 8; k++) c.stat[k] = 0;
 }
 
@@ -4267,7 +4302,15 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
 __global__ void k_tile_pass_begin(Dev d) {  // a later pass
   ArenaCtl &c = d.ctl[0];
   c.n_out = c.n_out_pel = c.n_undone = 0;
-  c.n_ho = 0;
+  c.n_ho = c.n_ho_live = 0;
+  // a fresh, empty header: when the pass is gated (no undone cell anywhere) the
+  // collect kernel returns before writing one, and the previous pass's header
+  // (its pellet kills) must not be exchanged and summed a second time
+  TileRec &hd = d.outbox[0];
+  hd.kind = TR_HDR;
+  hd.idx = 0;
+  hd.seq = 0;
+  hd.x = hd.y = 0.0;
 }
 __device__ void tile_header(const Dev &d);
 __global__ void __launch_bounds__(256) k_tile_collect(Dev d, int with_bitmap) {
@@ -4285,8 +4328,12 @@ __global__ void __launch_bounds__(256) k_tile_collect(Dev d, int with_bitmap) {
     }
     if (und) atomicAdd(&d.ctl[0].n_undone, und);
   }
-  // the message header, once every owned cell is counted (the last block)
-  if (last_block(d.ticket + 3, gridDim.x) && threadIdx.x == 0) tile_header(d);
+  // the message header, once every owned cell is counted (the last block); on
+  // the first pass, first the live bots' history hand-offs
+  if (last_block(d.ticket + 3, gridDim.x)) {
+    if (!with_bitmap) tile_plan_live(d);
+    if (threadIdx.x == 0) tile_header(d);
+  }
 }
 __device__ void tile_header(const Dev &d) {
   const ArenaCtl &c = d.ctl[0];
@@ -4332,7 +4379,7 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int fir
       }
       c.n_eaten_glob += kills;
       c.n_undone_glob = und;
-      if (first) c.n_ho = 0;  // (the header holds this tick's hand-off count; the next plan counts afresh)
+      if (first) c.n_ho = c.n_ho_live = 0;  // (the header holds this tick's hand-offs; the next plan counts afresh)
     }
     return;
   }

@@ -492,10 +492,10 @@ class Field:
         mask[idx] = 1
         if "obs_buf" not in self._cache:
             self._cache["obs_buf"] = np.zeros((len(self.players), self.stepper.obs_len))
-            self._cache["obs_rows"] = {}
         buf = self.stepper.observe(self._cache["obs_buf"], mask=mask)
+        rows = self._cache.setdefault("obs_rows", {})
         for i in idx:
-            self._cache["obs_rows"][i] = buf[i].copy()
+            rows[i] = buf[i].copy()
 
     def _state_row(self, index):
         self._prefetch_states([index])
@@ -568,7 +568,7 @@ class Bot:
     def _param(self, name, default):
         return getattr(self.parameters, name, default) if self.parameters is not None else default
 
-    def reset(self):  # bot.py:125-164 (the NN bot's history grids are the device's, cleared by the world reset)
+    def reset(self, _device=True):  # bot.py:125-164
         if self.learningAlg is not None and hasattr(self.learningAlg, "reset"):
             self.learningAlg.reset()
         self.lastMass = None
@@ -587,6 +587,13 @@ class Bot:
                 self.memories[-1][-1] = True
             self.fovSize = 0
             self.lastFovSize = 0
+            # the history grids and lastFovSize live on the device (Model.resetBots batches this)
+            st = self.field.stepper if self.field is not None else None
+            if _device and st is not None:
+                mask = np.zeros(len(self.field.players), np.uint8)
+                mask[self.player.index] = 1
+                st.reset_bots(mask)
+                self.field._cache.pop("obs_rows", None)
         else:
             self.currentAction = [0, 0, 0, 0]
         self.experiences = []
@@ -734,17 +741,71 @@ class Bot:
         row = self.field._state_row(self.player.index)  # grid view + extras, flattened (bot.py:286-295)
         return row.reshape(1, -1).copy()
 
+    # the parts of getStateRepresentation by their public names (bot.py:302-323,
+    # 326-497, 511-547).  All read the one device observation this bot computes in
+    # a tick (its history grids and last fov size advance once per tick, as they do
+    # when the reference's getStateRepresentation calls them in sequence).
+    def _grid_len(self):
+        g = self.field.grid_squares
+        return bin(int(self.field.stepper.cfg.obs_channels) & 0x3FF).count("1") * g * g
+
+    def getGridStateRepresentation(self):  # bot.py:326-497: gridView [NUM_OF_GRIDS, G, G]
+        if not self._param("GRID_VIEW_ENABLED", True):
+            raise RuntimeError("getGridStateRepresentation: the field was built for the simple "
+                               "representation (GRID_VIEW_ENABLED = False)")
+        if not self.player.getIsAlive():
+            raise RuntimeError("getGridStateRepresentation: the player is dead (the reference reads a "
+                               "dead player's FOV and fails)")
+        g = self.field.grid_squares
+        row = self.field._state_row(self.player.index)
+        return row[:self._grid_len()].reshape(-1, g, g).copy()
+
+    def getAdditionalFeatures(self):  # bot.py:302-323: [lastFovSize, fovSize, mass, action(4), action(4)]
+        if not self._param("GRID_VIEW_ENABLED", True) or not self.player.getIsAlive():
+            raise RuntimeError("getAdditionalFeatures: no grid observation for this bot")
+        row = self.field._state_row(self.player.index)
+        return [float(v) for v in row[self._grid_len():]]
+
+    def getSimpleStateRepresentation(self):  # bot.py:511-547: 12 values
+        if self._param("GRID_VIEW_ENABLED", True):
+            raise NotImplementedError("getSimpleStateRepresentation: the device computes it when the field is "
+                                      "built with GRID_VIEW_ENABLED = False (one observation layout per field)")
+        return [float(v) for v in self.field._state_row(self.player.index)]
+
+    def getCoorConvGrids(self):  # bot.py:500-508
+        g = self.field.grid_squares
+        row, col = np.meshgrid(np.arange(g, dtype=np.float64), np.arange(g, dtype=np.float64), indexing="ij")
+        return row, col
+
+    # bookkeeping (bot.py:115-123, 235-241)
+    def saveInitialModels(self, path):
+        if self.learningAlg is not None:
+            self.learningAlg.save(path, "init_")
+
+    def saveModel(self, path):
+        self.learningAlg.save(path)
+
+    def resetMassList(self): self.totalMasses = []
+    def setMassesOverTime(self, array): self.totalMasses = array
+    def setExploring(self, val): self.player.setExploring(val)
+
     def getPlayer(self): return self.player
     def getType(self): return self.type
     def getLearningAlg(self): return self.learningAlg
     def getCurrentAction(self): return self.currentAction
+    def getCurrentActionIdx(self): return self.currentActionIdx
     def getMassOverTime(self): return self.totalMasses
+    def getAvgReward(self): return self.rewardAvgOfEpisode
     def getLastReward(self): return self.lastReward
     def getCumulativeReward(self): return self.cumulativeReward
     def getLastState(self): return self.oldState
     def getLastMemory(self): return self.lastMemory
     def getExperiences(self): return self.experiences
     def getFrameSkipRate(self): return self._param("FRAME_SKIP_RATE", 0)
+    def getTrainMode(self): return getattr(self, "trainMode", None)
+    def getExpRepEnabled(self): return self._param("EXP_REPLAY_ENABLED", False)
+    # (the reference's getGridSquaresPerFov calls itself and never returns, bot.py:702-703)
+    def getGridSquaresPerFov(self): return self.field.grid_squares
 
 
 class RGBGenerator:
@@ -803,6 +864,11 @@ class Model:
         self.virusEnabled = bool(getattr(parameters, "VIRUS_SPAWN", False)) if parameters is not None else False
         self.resetLimit = getattr(parameters, "RESET_LIMIT", 20000) if parameters is not None else 20000
         self.players, self.bots, self.humans = [], [], []
+        self.listeners = []
+        self.playerSpectator = None
+        self.spectatedPlayer = None
+        self.path = None
+        self.screenWidth = self.screenHeight = None
         self.field = Field(self.virusEnabled, parameters, seed=seed, device=device, **field_kw)
         self.counter = 0
         # model.py:67-71: the pixel generator exists when the CNN reads pixels
@@ -861,9 +927,15 @@ class Model:
             if bot.type != "Greedy":
                 bot.makeMove(_prepared=True)
 
-    def resetBots(self):
+    def resetBots(self):  # model.py:117-119 (the NN bots' device history in one call)
         for bot in self.bots:
-            bot.reset()
+            bot.reset(_device=False)
+        nn = [b.player.index for b in self.bots if b.type == "NN"]
+        if nn and self.field.stepper is not None:
+            mask = np.zeros(len(self.players), np.uint8)
+            mask[nn] = 1
+            self.field.stepper.reset_bots(mask)
+            self.field._cache.pop("obs_rows", None)
 
     def update(self):  # model.py:98-111
         self.counter += 1
@@ -873,9 +945,99 @@ class Model:
             self.field._set_actions(nn)
         self.takeBotActions()
         self.field.update()
+        if self.guiEnabled and self.viewEnabled:  # model.py:107-108
+            self.notify()
 
-    # getters
+    def initParameters(self, parameters):  # model.py:79-84 (before initialize: the world is sized then)
+        if self.field.stepper is not None:
+            raise RuntimeError("initParameters after initialize(): the device world is already built")
+        self.parameters = parameters
+        self.virusEnabled = bool(getattr(parameters, "VIRUS_SPAWN", False))
+        self.resetLimit = getattr(parameters, "RESET_LIMIT", self.resetLimit)
+        self.field = Field(self.virusEnabled, parameters, seed=self.field.seed, device=self.field.device)
+        for p in self.players:
+            p.field = None
+            self.field.addPlayer(p)
+        for b in self.bots:
+            b.field = self.field
+
+    def modifySettings(self, reset_time):  # model.py:87-88
+        self.resetLimit = reset_time
+
+    def printBotMasses(self):  # model.py:139-142
+        for bot in self.bots:
+            mass = bot.getPlayer().getTotalMass()
+            print("Mass of ", bot.getPlayer(), ": ", round(mass, 1) if mass is not None else "Dead")
+
+    def createHuman(self, name):  # model.py:165-167
+        self.addHuman(self.createPlayer(name))
+
+    def addHuman(self, human): self.humans.append(human)
+
+    def addPlayerSpectator(self):  # model.py:181-183
+        self.playerSpectator = True
+        self.setSpectatedPlayer(self.players[0])
+
+    def setPath(self, path): self.path = path
+    def setSpectatedPlayer(self, player): self.spectatedPlayer = player
+    def setViewEnabled(self, boolean): self.viewEnabled = boolean
+
+    def setScreenSize(self, width, height):
+        self.screenWidth, self.screenHeight = width, height
+
+    # checks (model.py:201-205)
+    def hasHuman(self): return bool(self.humans)
+    def hasPlayerSpectator(self): return self.playerSpectator is not None
+
+    # getters (model.py:208-270)
+    def getNNBot(self):
+        for bot in self.bots:
+            if bot.getType() == "NN":
+                return bot
+        return None
+
+    def getNNBots(self): return [bot for bot in self.bots if bot.getType() == "NN"]
+
+    def getTopTenPlayers(self):  # stable sort by total mass, descending (list.sort is stable)
+        players = self.getPlayers()[:]
+        players.sort(key=lambda p: p.getTotalMass(), reverse=True)
+        return players[0:10]
+
+    def getFovPos(self, humanNr):
+        if self.hasHuman():
+            return np.array(self.humans[humanNr].getFovPos())
+        if self.hasPlayerSpectator():
+            return np.array(self.spectatedPlayer.getFovPos())
+        return np.array([self.field.getWidth() / 2, self.field.getHeight() / 2])
+
+    def getFovSize(self, humanNr):
+        if self.hasHuman():
+            return self.humans[humanNr].getFovSize()
+        if self.hasPlayerSpectator():
+            return self.spectatedPlayer.getFovSize()
+        return self.field.getWidth()
+
+    def getSpectatedPlayer(self):
+        if self.hasHuman():
+            return self.humans
+        if self.hasPlayerSpectator():
+            return self.spectatedPlayer
+        return None
+
     def getField(self): return self.field
+    def getPellets(self): return self.field.getPellets()
+    def getViruses(self): return self.field.getViruses()
+    def getPlayerCells(self): return self.field.getPlayerCells()
     def getPlayers(self): return self.players
     def getBots(self): return self.bots
     def getHumans(self): return self.humans
+    def getParameters(self): return self.parameters
+    def getVirusEnabled(self): return self.virusEnabled
+
+    # MVC (model.py:273-281)
+    def set_GUI(self, value): self.guiEnabled = value
+    def register_listener(self, listener): self.listeners.append(listener)
+
+    def notify(self):
+        for listener in self.listeners:
+            listener()

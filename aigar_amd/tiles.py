@@ -21,6 +21,9 @@ history handed off in the next tick's first message.  Every tile computes the
 same assignment (`aigar_tile_observers`).
 
 Transports:
+  - RCCL inside the library (`rccl_comm` + `Stepper.tile_run`): one tile per rank,
+    the exchange an ncclAllGather on the tile's stream, the whole tiled step one
+    hipGraph replay -- the production path (bench.py on the nccl backend).
   - `LocalTransport`: all tiles in this process (one GPU): device copies.
   - `TorchTransport`: one tile per rank; `torch.distributed.all_gather_into_tensor`
     over the process group (RCCL over xGMI on the `nccl` backend; gloo on CPU
@@ -115,6 +118,21 @@ def tiled_tick(tiles, transport, policy="none", p_split=0.0, p_eject=0.0, seed=0
     for k, t in enumerate(tiles):
         t.tile_end(None if obs is None else obs[k])
     return passes
+
+
+def rccl_comm(stepper, dist=None, group=None):
+    """Give this rank's tile handle an RCCL communicator over all the tiles (rank =
+    tile id): rank 0 makes the ncclUniqueId, the process group broadcasts it.
+    Then `stepper.tile_run` steps the tile with the exchange as an RCCL all-gather
+    inside the step's hipGraph (no Python, no host round trip per tick)."""
+    info = stepper.tile_info()
+    n, k = info["ntiles"], info["tile_id"]
+    uid = _lib.rccl_unique_id() if k == 0 else None
+    if n > 1:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = box[0]
+    stepper.tile_comm_init(uid, n, k)
 
 
 class LocalTransport:

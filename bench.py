@@ -84,7 +84,7 @@ def obs_bytes_per_bot(L, p_fov, c_fov, v_fov, n_cells=1.2):
 def pmc_traffic(kernel_prefix, workload):
     """HBM-side bytes per launch of the kernel (kernel_prefix "_step": per env
     step, all the step's kernels) from the newest committed PMC summary
-    (profiles/r*_pmc_<workload>.json, written by tools/pmc.sh +
+    (profiles/r*_pmc_<workload>.json, written by tools/gpu.sh TAG pmc +
     tools/pmc_summary.py on the same bench command).  None if absent."""
     import glob
     import re
@@ -281,39 +281,55 @@ def tick_bytes(st, alive, field, n_eaten):
 
 def c4_leg(args, name, rank, world, local, seed, dist, backend):
     """BASELINE configs[3]: ONE C3 arena tiled over the N ranks (aigar_amd/tiles.py),
-    each rank one tile; the eat-phase messages (and the observation-history
-    hand-offs) all-gathered over RCCL (xGMI).  Strong scaling: the same 4096 bots
-    whatever N.  One step = the random policy + Field.update + the observation of
-    every bot (each by one tile).  The passes are device-decided (no host round
-    trip): first with no extra pass; if a tick needed one (device error bit), the
-    world is reloaded and timed again with one extra pass per tick."""
+    each rank one tile.  On the nccl backend (the production path) every step is
+    aigar_tile_run: policy + Field.update with the eat-phase messages (and the
+    observation-history hand-offs) all-gathered by RCCL over xGMI + the observation
+    of this tile's bots, captured as ONE hipGraph per step (no Python, no host round
+    trip per tick).  On gloo (the 1-GPU rehearsal: N ranks sharing one card, which
+    RCCL cannot do) the exchange goes through TorchTransport, staged through host
+    memory.  Strong scaling: the same 4096 bots whatever N.  The passes are
+    device-decided: first with no extra pass; if a tick needed one (device error
+    bit), the world is reloaded and timed again with one extra gated pass per tick.
+    world == 1 (AIGAR_C4_SELFTEST): the whole field as one forced tile over a
+    1-rank communicator -- the same code path on the one GPU of a test box."""
     import torch
     from aigar_amd import _lib, tiles
     tx, ty = tiles.tile_grid(world)
     # 512 records per message (the random population's owned outcomes per tick and tile are
     # a few dozen; an overflow is a device error, not a silent loss) and 16 hand-off slots:
     # a 48 KB first-pass message per tile
-    cfg = tiles.tile_config(make_cfg(name, device=local, arenas=1), tx, ty, rank, cap=512)
+    cfg = tiles.tile_config(make_cfg(name, device=local, arenas=1), tx, ty, rank, cap=512 if world > 1 else 4096,
+                            flags=_abi.TILE_FORCE if world == 1 else 0)
     stp = _lib.Stepper(cfg)
-    tr = tiles.TorchTransport.for_stepper(stp, staged=(backend != "nccl"))
+    rccl = backend == "nccl"
+    if rccl:
+        stp.set_stream(torch.cuda.current_stream().cuda_stream)
+        tiles.rccl_comm(stp, dist)
+        tr = None
+    else:
+        tr = tiles.TorchTransport.for_stepper(stp, staged=True)
     bots, field, pellets, virus, ps, pe, ch, ex, _ = WORKLOADS[name]
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
     steps, warm = args.steps, args.warmup
+
+    def run(n, extra):
+        if rccl:
+            stp.tile_run(n, "random", obs, p_split=ps, p_eject=pe, seed=args.seed, extra_passes=extra)
+        else:
+            for _ in range(n):
+                tiles.tiled_tick([stp], tr, "random", ps, pe, args.seed, [obs], extra_passes=extra)
+
     dev = "cuda" if backend == "nccl" else None
     for extra in (0, 1):
         start = start_world(stp, name, seed, 1)  # every tile loads the same world and keeps its held pellets
-        tick = lambda: tiles.tiled_tick([stp], tr, "random", ps, pe, args.seed, [obs], extra_passes=extra)
         try:
-            for _ in range(warm):
-                tick()
+            run(warm, extra)
             torch.cuda.synchronize()
             stp.sync()
             replicas.barrier(dist)
             torch.cuda.synchronize()
-            tr.reset_timing()
             t0 = time.perf_counter()
-            for _ in range(steps):
-                tick()
+            run(steps, extra)
             torch.cuda.synchronize()
             replicas.barrier(dist)
             el = time.perf_counter() - t0
@@ -323,26 +339,28 @@ def c4_leg(args, name, rank, world, local, seed, dist, backend):
             if extra == 1 or "device error bits" not in str(e):
                 raise
     el = replicas.max_over_ranks(dist, el, device=dev)
-    ex_ms = tr.avg_exchange_ms()
-    # per-tile breakdown: the next steps as separate calls, HIP events on the tile's stream
+    graphed = stp.tile_run_graphed() if rccl else False
+    # per-tile breakdown: the next steps as separate launches, HIP events on the tile's stream
     nb = min(steps, 30)
     stp.profile(True)
-    tr.reset_timing()
-    for _ in range(nb):
-        tick()
+    if tr is not None:
+        tr.reset_timing()
+    run(nb, extra)
     torch.cuda.synchronize()
-    br = {k: stp.kernel_time(k) for k in ("tile_begin", "tile_apply", "tile_resume", "tile_end", "observe")}
+    names = ("tile_begin", "exchange", "tile_apply", "tile_resume", "tile_end", "observe")
+    br = {k: stp.kernel_time(k) for k in names}
     stp.profile(False)
-    ex_ms_b = tr.avg_exchange_ms()
+    ex_ms = br["exchange"][0] / max(1, br["exchange"][1]) if rccl else tr.avg_exchange_ms()
     stp.sync()
     observed = int(np.sum(stp.tile_observers() == rank))
     info = stp.tile_info()
     stp.close()
     per_tile = {"tile": rank, "bots_observed": observed,
                 "ms_per_step": {k: v[0] / nb for k, v in br.items() if v[1]},
-                "exchange_ms_per_pass": ex_ms_b,
-                "note": "tile_begin = policy + updateViruses .. playerVirusOverlap + the first eat pass and the "
-                        "hand-off plan; tile_end = playerPlayerOverlap .. spawnStuff; observe = this tile's bots"}
+                "exchange_ms_per_pass": ex_ms,
+                "note": "separate launches with HIP events (the timed steps replay one graph): tile_begin = "
+                        "policy + updateViruses .. playerVirusOverlap + the first eat pass and the hand-off plan; "
+                        "tile_end = playerPlayerOverlap .. spawnStuff; observe = this tile's bots"}
     tiles_all = [per_tile]
     if dist is not None:
         tiles_all = [None] * world
@@ -351,7 +369,9 @@ def c4_leg(args, name, rank, world, local, seed, dist, backend):
                 bots, int(pellets), tx, ty, world, start),
             "value": bots * steps / el, "unit": "env-steps/s", "scaling": "strong", "steps": steps,
             "ms_per_step": el / steps * 1e3, "eat_passes_per_tick": 1 + extra, "extra_passes": extra,
-            "exchange": {"collective": "all_gather_into_tensor (%s)" % backend,
+            "step_graph": graphed,
+            "exchange": {"collective": "ncclAllGather inside the step graph (RCCL, xGMI)" if rccl else
+                         "all_gather_into_tensor (%s, staged through host memory)" % backend,
                          "bytes_per_rank_first_pass": (1 + info["tcap"]) * 32 + info.get("handoff_bytes", 0),
                          "avg_ms": ex_ms},
             "per_tile": tiles_all}
@@ -515,6 +535,9 @@ def main():
             out["batched"] = batched(name, args.batched_arenas, args.policy, ps, pe, args.seed, local)
         if args.policy == "random" and name == "c3":  # the same start with the reference's Greedy bots
             out["greedy"] = greedy_side(name, args.seed, local)
+    if world == 1 and name == "c3" and os.environ.get("AIGAR_C4_SELFTEST") and not args.profile_run:
+        # the C4 code path on one GPU: the whole field as one forced tile over a 1-rank RCCL communicator
+        out["c4_selftest"] = c4_leg(args, name, rank, world, local, args.seed, dist, "nccl")
     if not args.no_c4 and world > 1 and name == "c3":
         # the metric's world at N GPUs: one 4096-bot arena tiled over them (value);
         # the replicas measured above become the side line

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AIGAR_ABI_VERSION 4
+#define AIGAR_ABI_VERSION 5
 
 /* random number stream of the world (spawns, explosion angles) */
 #define AIGAR_RNG_PHILOX 0   /* Philox4x64-10 keyed by (seed, site, index): device + oracle */
@@ -74,6 +74,10 @@ extern "C" {
 /* tile_flags: decide only the cells this tile owns (the others wait for their
  * owners' messages) -- the strictest exchange pattern, used by the tests */
 #define AIGAR_TILE_OWNED_ONLY 0x1
+/* a 1 x 1 "tiled" handle: the whole field is one tile that still runs the tile
+ * passes and the exchange (a 1-rank RCCL communicator: the one-GPU test of the
+ * C4 exchange path) */
+#define AIGAR_TILE_FORCE 0x2
 
 typedef struct aigar_handle aigar_handle;
 
@@ -285,6 +289,11 @@ int aigar_policy_random_bots(aigar_handle *h);
 int aigar_observe_pixels(aigar_handle *h, void *out, int side, uint64_t color_seed, int dtype, int on_device);
 /* bot.currentAction / bot.lastAction used by the action extras: [A*B][4] each (may be NULL). */
 int aigar_set_actions(aigar_handle *h, const double *cur, const double *prev, int on_device);
+/* Bot.reset (bot.py:125-164) for the players with mask[i] != 0 (NULL: all): the
+ * NN bot's last / second-last self and enemy grids restart at zero and its
+ * lastFovSize at 0, as model.resetBots() does between the collector's windows
+ * (aigar.py:845-852, 833-838).  mask: NP bytes, host or (on_device) device. */
+int aigar_reset_bots(aigar_handle *h, const uint8_t *mask, int on_device);
 
 /* per-player summary [A*B][5]: alive, total mass (player.py:129), fov x, fov y, fov size
  * (player.py:156-167). */
@@ -356,6 +365,29 @@ int aigar_tile_resume(aigar_handle *h);
 int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype);
 int aigar_tile_exchange_local(aigar_handle **hs, int n);
 int aigar_tile_observers(aigar_handle *h, int32_t *out);
+
+/* C4 over RCCL (xGMI): the tile's exchange as ncclAllGather(outbox -> inbox) on
+ * the handle's stream, so a whole tiled step -- policy, the tick with its eat
+ * passes and exchanges, the observation of this tile's bots -- is one hipGraph
+ * replay with no host round trip (the rank-side loop of the aigar_tile_* calls
+ * above, with the caller's transport replaced by RCCL).
+ *   aigar_rccl_unique_id(path, id)   rank 0: a fresh ncclUniqueId (128 bytes),
+ *                                    which the caller broadcasts to every rank
+ *   aigar_tile_comm_init(h, path, id, nranks, rank)  ncclCommInitRank; nranks
+ *                                    must be the tile count and rank the tile id
+ *   aigar_tile_run(h, n, p, extra_passes, obs, dtype)  n tiled steps: per step
+ *       aigar_tile_begin, all-gather, aigar_tile_apply, extra_passes gated
+ *       (resume, all-gather, apply) rounds, aigar_tile_end (obs: DEVICE buffer
+ *       or NULL) -- captured once as a hipGraph (RCCL is captured with it),
+ *       direct launches if the capture fails or while profiling
+ * path: the librccl.so to bind (the one the process's torch loaded, so that one
+ * HIP runtime serves both), or NULL for "librccl.so" on the loader path. */
+int aigar_rccl_unique_id(const char *path, void *id);
+int aigar_tile_comm_init(aigar_handle *h, const char *path, const void *id, int nranks, int rank);
+int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_params *p, int extra_passes, void *obs_out,
+                   int dtype);
+/* 1 if aigar_tile_run replays a captured graph, 0 if it launches directly */
+int aigar_tile_run_graphed(aigar_handle *h);
 
 /* The event log as raw rows (key_hi = tick << 8 | phase, key_lo = order within the
  * phase, code, a, b), unsorted: tiled arenas merge their tiles' logs by key. */

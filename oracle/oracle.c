@@ -1673,6 +1673,25 @@ int oracle_reset_obs_state(void *h) {
   for (int a = 0; a < O->A; a++) arena_reset_obs_state(O, &O->ar[a]);
   return 0;
 }
+/* Bot.reset (bot.py:125-164, NN branch) for the players with mask[p] != 0 of
+ * every arena (player index a * B + p): the history grids restart at zero and
+ * fovSize / lastFovSize at 0.  NULL mask: every player. */
+int oracle_reset_bots(void *h, const uint8_t *mask) {
+  Oracle *O = (Oracle *)h;
+  for (int a = 0; a < O->A; a++) {
+    Arena *A = &O->ar[a];
+    const size_t GG = (size_t)A->G * A->G;
+    for (int p = 0; p < A->B; p++) {
+      if (mask && !mask[(size_t)a * A->B + p]) continue;
+      A->obs_fov[p] = 0;
+      memset(A->self_lf + p * GG, 0, sizeof(double) * GG);
+      memset(A->self_slf + p * GG, 0, sizeof(double) * GG);
+      memset(A->enemy_lf + p * GG, 0, sizeof(double) * GG);
+      memset(A->enemy_slf + p * GG, 0, sizeof(double) * GG);
+    }
+  }
+  return 0;
+}
 
 static void mark_hashed(const Hash *h) {
   for (int i = 0; i < h->rows * h->cols; i++)

@@ -47,6 +47,7 @@ def lib():
         L.oracle_player_stats.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_get_events.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.c_int]
         L.oracle_reset_obs_state.argtypes = [vp]
+        L.oracle_reset_bots.argtypes = [vp, C.POINTER(C.c_uint8)]
         L.oracle_set_mt.argtypes = [vp, C.c_int, C.POINTER(C.c_uint32), C.c_int]
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_np_sum.restype = C.c_double
@@ -144,6 +145,11 @@ class Oracle:
         out = np.zeros(self.obs_len, np.float64)
         self._chk(self.L.oracle_observe_one(self.h, arena, player, _dp(out)))
         return out
+
+    def reset_bots(self, mask=None):
+        """Bot.reset's history half (bot.py:125-164) for the players where mask != 0."""
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self._chk(self.L.oracle_reset_bots(self.h, None if m is None else m.ctypes.data_as(C.POINTER(C.c_uint8))))
 
     def pixels(self, side=42, color_seed=0):
         """RGB frames of RGBGenerator.get_cnn_inputRGB (surfarray order [x][y][rgb]),

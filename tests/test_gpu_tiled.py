@@ -208,3 +208,99 @@ def test_tiled_load_state_continues_like_the_oracle():
     assert not dif, dif
     ta.close()
     o.close()
+
+
+def test_c3_4x2_gated_extra_pass_matches_oracle():
+    """extra_passes=1 (the bench's fallback): the second pass is issued blindly
+    and gated on the device.  With the default halo every cell is final after
+    the first pass, so the second is gated on every tick; its message must be an
+    empty header (k_tile_pass_begin), not the first pass's header again -- a
+    stale one would add every tile's pellet kills twice and over-spawn pellets
+    (n_pellets and ctr_pellet drift from the oracle within a tick)."""
+    st = run(c3_config(), 4, 2, 40, 35, synthetic(4096, 4800, 2.5e-3, 1e-2, 35), obs_every=5, check_every=1,
+             start=parity.load_snapshot("c3_t600"), extra_passes=1)
+    assert set(st["passes"]) == {2}
+    assert _abi.EV_CELL_EAT_PELLET in st["kinds"] and _abi.EV_RESPAWN in st["kinds"]
+
+
+def _crossing_world(n_move=64, seed=11):
+    """A 256-bot reset world (field 1200, 2 x 1 tiles: tile 0 holds x < 600) with
+    bots 0..n_move-1 moved to x = 595 in a column, one cell each."""
+    cfg = make_config(bots=256, channels=C3_CH, extras=0x1F)
+    o = Oracle(cfg)
+    o.reset(seed)
+    snap = o.get_state()
+    o.close()
+    cf = np.array(snap["cells_f"], copy=True)
+    owner = np.asarray(snap["cells_i"])[:, 0]
+    for p in range(n_move):
+        k = int(np.nonzero(owner == p)[0][0])
+        cf[k, 0], cf[k, 1] = 595.0, 80.0 + 16.0 * p
+        cf[k, 4:8] = 0.0
+    snap["cells_f"] = cf
+    return cfg, snap, owner
+
+
+def test_many_bots_crossing_a_border_in_one_tick():
+    """64 bots observed by tile 0 cross into tile 1 in the same tick: more than
+    the hand-off slots of one message (16 at tile_cap 512).  The lowest player
+    indices are handed off first, the rest stay with tile 0 a tick longer (their
+    view is inside its halo) and follow in the next messages; every bot's
+    observation, history channels included, equals the oracle's every tick."""
+    cfg, snap, _ = _crossing_world()
+    ta, o = TiledArena(cfg, 2, 1, cap=512), Oracle(cfg)
+    assert ta.tiles[0].tile_info()["hcap"] == 16
+    ta.load_state(snap)
+    o.load_state(snap)
+    rng = np.random.default_rng(3)
+    moves = []
+    prev = None
+    for t in range(14):
+        cmd = parity.synthetic_commands(rng, None, 256, 1200)
+        cmd[:64, 0], cmd[:64, 1] = 1190.0, 80.0 + 16.0 * np.arange(64)  # straight across the border
+        ta.set_commands(cmd)
+        o.set_commands(cmd)
+        ta.tick(extra_passes=0)
+        o.step(1)
+        assert np.array_equal(ta.events(), o.events()), "tick %d" % t
+        og, oo = ta.observe(), o.observe()
+        assert parity.obs_close(og, oo), "tick %d: observations differ" % t
+        by = ta.last_observers[:64].copy()
+        if prev is not None:
+            moves.append(int(np.sum((prev == 0) & (by == 1))))
+        prev = by
+    dif = parity.diff_states(ta.get_state(), o.get_state())
+    assert not dif, dif
+    assert np.all(prev == 1), prev
+    # the crossing happened in one tick but the hand-offs were spread over several
+    assert max(moves) == 16 and sum(moves) == 64, moves
+    ta.close()
+    o.close()
+
+
+def test_dead_bots_beyond_the_hand_off_slots_raise():
+    """More bots held by one tile die in one tick than its message has hand-off
+    slots: a dead bot respawns anywhere, so its history may not wait for a later
+    message -- the tick must fail with its own error bit (16384), not defer."""
+    cfg, snap, owner = _crossing_world(n_move=0)
+    cf = np.array(snap["cells_f"], copy=True)
+    big = int(np.nonzero(owner == 100)[0][0])
+    cf[big, 0], cf[big, 1], cf[big, 2] = 400.0, 600.0, 20000.0
+    cf[big, 3] = np.sqrt(20000.0 / np.pi)
+    ang = np.arange(64) * 2 * np.pi / 64
+    for p in range(64):  # a ring around the big cell, just out of its reach
+        k = int(np.nonzero(owner == p)[0][0])
+        cf[k, 0], cf[k, 1] = 400.0 + 84.0 * np.cos(ang[p]), 600.0 + 84.0 * np.sin(ang[p])
+        cf[k, 4:8] = 0.0
+    snap["cells_f"] = cf
+    ta = TiledArena(cfg, 2, 1, cap=512)
+    ta.load_state(snap)
+    ta.observe()  # tile 0 becomes the ring bots' history holder
+    cmd = np.zeros((256, 4))
+    cmd[:, 0], cmd[:, 1] = 400.0, 600.0
+    with pytest.raises(RuntimeError, match=r"device error bits 0x4[0-9a-f]{3} "):
+        for _ in range(12):
+            ta.set_commands(cmd)
+            ta.tick(extra_passes=0)
+            ta.observe()
+    ta.close()

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch and per-step HBM-side bytes of every kernel from tools/pmc.sh output.
+"""Per-launch and per-step HBM-side bytes of every kernel from `tools/gpu.sh TAG pmc` output.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 128-B read requests as 64 B (MI355X_MICROARCH.md, HBM section), so the read
