@@ -7,9 +7,14 @@
 //           owned by a player; the player's cell *list* (order matters:
 //           player.py:22,48-61) is p_list[k*NP + gp] = slot of the k-th cell.
 //           Slot-major layout makes per-player loops coalesce across lanes.
-//   pellet  a*Pcap + i  (two buffers: P0 at tick boundaries, P1 during the
-//           eat phases; each rebuild counting-sorts records by centre bucket,
-//           so bucket b's pellets are contiguous: [pstart[b], pstart[b+1]) )
+//   pellet  a*PS + slot: bucket rows with two homes each (slot = home * cols * PR
+//           + row * PR + k); a row's live records are contiguous in its current
+//           home, sorted by centre bucket, so bucket (bx, by) is the range
+//           [pstart[a*PH1 + by*(cols+1) + bx], the next entry) and a grid row's
+//           buckets bx0..bx1 are ONE range (entry cols of a row = the row's end).
+//           The closing update rewrites only the rows whose pellets changed, each
+//           into its other home (field.py:303-313, 327-344 change a few per tick).
+//           Dead flags / reservation keys: a*PD + slot, staged records a*PD + PS + j.
 //   blob    a*Ecap + i,   virus a*Vcap + i   (list order == creation order)
 //   grids   a*(H+1) + bucket   (H = cols*cols, 20-unit buckets)
 #pragma once
@@ -43,7 +48,7 @@ struct ArenaCtl {
   int64_t seq_base_upd;  // seq_next before updatePlayers' creations (this tick)
   int64_t seq_base_spawn;
   uint64_t ctr_pellet_base, ctr_virus_base;
-  int n_pel;          // pellets in the current primary buffer
+  int n_pel;          // pellets in the store (a tile: those it holds)
   int n_pnew;         // staged pellets (blob conversions, spawns)
   int n_pel_eaten;    // eaten in this tick's eat phase
   int n_blob;         // blob slots in use
@@ -64,14 +69,10 @@ struct ArenaCtl {
   uint32_t food_round;   // reservation epoch (grows every eat phase)
   uint32_t scan_epoch[2];  // decoupled look-back epoch per scan slot (grows every launch)
   int scan_ticket[2];      // slot 0: pellet rebuilds, slot 1: cell grid (may run concurrently)
-  int src_n_pel, src_n_stage;
-  int src_n_conv;  // blob conversions among the staged records (eaten ones are dropped)
+  int src_n_stage;  // reset: the staged records the row build places
   int n_kill;      // buffer pellets killed this tick (kill_list; sorted + unique after k_spawn_plan)
-  int n_stg;       // staged records joining the buffer at the closing update (stg_key)
-  int pu_src, pu_n0, pu_nconv;  // the closing update's source buffer, its count, blob conversions
-  int pu_small;  // a usual tick: k_pel_update builds the short lists (n_kill raw) and closes the counts
-  int pcur;           // pellet buffer holding the current (end-of-tick) pellets
-  int peat;           // pellet buffer of this tick's eat phase (pcur when nothing was converted)
+  int pu_nconv;   // the closing update: this tick's blob conversions (staged records 0 .. pu_nconv - 1)
+  int pu_nsp, pu_spec;  // the closing update: this tick's pellet spawns, drawn ahead (spec_*) or staged (pn)
   uint32_t dirty;     // DIRTY_*: a virus / blob died this tick (k_spawn_plan compacts)
   int food_undone[3];  // cells that failed reservation round r (index r % 3)
   uint32_t pl_epoch;  // k_players look-back epoch / finished-tile ticket
@@ -97,8 +98,6 @@ enum : uint32_t {
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };
-// pellet rebuild modes (also the scan's epilogue selector)
-enum : int { PR_NONE = 0, PR_RESET = 1, PR_CLOSE = 2 };
 
 // event phases (sort key high word), in reference order within a tick
 enum : uint32_t { PH_MERGE = 0, PH_VB = 1, PH_PV = 2, PH_PELLET = 3, PH_BLOB = 4, PH_PP = 5, PH_SPAWN = 6 };
@@ -153,22 +152,24 @@ struct Dev {
   int *t_holder;  // [NP] tile holding the bot's current observation history, -1: every tile
   int *t_obsby;   // [NP] tile that observed the bot since the last plan, -1: none
   int *t_holive;  // [hcap] live bots waiting for a hand-off slot this tick (slots left after the dead ones)
+  int *t_hoslot;  // [hcap] the player of each hand-off slot of this tick's first message
   int own_bx0, own_bx1, own_by0, own_by1;      // owned centre buckets [x0, x1) x [y0, y1)
   int loc_bx0, loc_bx1, loc_by0, loc_by1;      // held pellets: owned range + halo
   TileRec *outbox;       // [1 + tcap] records + bitmap
   const TileRec *inbox;  // [ntiles] outboxes (the transport fills it)
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
-  // closing pellet update (k_pel_update): killed buffer indices, staged (bucket << 32 | index)
-  // keys -- both sorted by k_spawn_plan -- and the per-bucket counts that go with pstart
+  // closing pellet update (k_pel_update): the store slots killed this tick (their rows
+  // are rewritten), and this tick's first pellet spawns, drawn ahead by k_tick_begin
   int *kill_list;     // [A][Pcap]
-  double *spec_x, *spec_y, *spec_m;  // [A][64] this tick's first pellet spawns, drawn ahead (k_tick_begin)
-  int64_t *stg_key;   // [A][2 Pcap] (second half: padding of a global-memory sort)
-  int64_t *pu_tmp;    // [A][2 Pcap] (kills sorted in global memory when LDS is too small)
-  int *pbc;           // [A][H] pellets per bucket of the current buffer
+  double *spec_x, *spec_y, *spec_m;  // [A][64]
   double pow_n032[17];  // pow_glibc(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
   int cshift;  // blob/virus grids: 2^cshift x 2^cshift fine buckets per cell (grid_span)
   int cshift_c;  // player-cell grid: smallest shift with <= 4096 cells (k_cgrid_count / k_cgrid_scatter)
   int Pcap, Ecap, Vcap, Wcap, EVcap;
+  int PR;   // pellet slots per row home
+  int PS;   // pellet store slots per arena: 2 homes x cols rows x PR
+  int PD;   // dead-flag / reservation index space per arena: PS + Pcap (staged records j at PS + j)
+  int PH1;  // pstart entries per arena: cols * (cols + 1) + 1
   int virus_enabled;
   double max_pellets, max_viruses;
   int G, L;
@@ -201,16 +202,16 @@ struct Dev {
   // per-player blob staging [16][NP]
   double *sb_x, *sb_y, *sb_svx, *sb_svy;
   uint8_t *sb_slot;
-  // pellets: two record buffers + staging
-  PelRec *pel[2];  // one 32-byte record per pellet: a bucket row's gather touches whole lines
-  int *pel_col[2];  // colour owner: the player whose colour a blob-made pellet carries, -1: its own
-  PelRec *pn;
+  // pellets: the row store + staging
+  PelRec *pel;      // [A*PS] one 32-byte record per pellet: a bucket row's gather touches whole lines
+  int *pel_col;     // [A*PS] colour owner: the player whose colour a blob-made pellet carries, -1: its own
+  PelRec *pn;       // [A*Pcap] staging: this tick's blob conversions, then (closing update) spawns
   int *pn_col;
-  uint8_t *pel_dead;  // [A*Pcap] for the eat-phase buffer
-  int *pel_rank;      // scratch [A*(Pcap)]
-  int *pcnt, *pstart; // [A*(H+1)] survivor counts / bucket starts (pellets)
-  int *pncnt;         // [A*(H+1)] staged-record counts (pellets)
-  uint64_t *pel_owner;  // reservation keys [A*Pcap]
+  uint8_t *pel_dead;  // [A*PD] eaten this tick (store slots, then staged records)
+  int *pel_rank;      // [A*Pcap] reset: a staged record's rank in its bucket
+  int *pstart;        // [A*PH1] bucket starts in the store, rows of cols + 1 entries
+  int *pncnt;         // [A*PH1] reset: staged records per bucket
+  uint64_t *pel_owner;  // reservation keys [A*PD]
   // blobs [A*Ecap]
   double *b_x, *b_y, *b_m, *b_r, *b_vx, *b_vy, *b_svx, *b_svy;
   int *b_svc;

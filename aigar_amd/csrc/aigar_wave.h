@@ -124,11 +124,13 @@ __device__ __forceinline__ Span grid_span(Rect q, int E, int cols, int shift) {
 // xlo/xlen: one extra range of item indices [xlo, xlo + xlen) walked in the same
 // steps (valid only without an items array: f receives xlo + k)
 template <class F>
+// stride: entries per grid row of st (0: the grid's own width; the pellet rows keep
+// one more, the row's end)
 __device__ __forceinline__ void wave_grid_for(const int *st, const int *items, int cols, Rect q, int E, F f,
-                                              int shift = 0, int xlo = 0, int xlen = 0) {
+                                              int shift = 0, int xlo = 0, int xlen = 0, int stride = 0) {
   if (q.x1 < q.x0 || q.y1 < q.y0) return;
   const Span g = grid_span(q, E, cols, shift);
-  const int bx0 = g.bx0, bx1 = g.bx1, by0 = g.by0, cols_ = g.stride;
+  const int bx0 = g.bx0, bx1 = g.bx1, by0 = g.by0, cols_ = stride ? stride : g.stride;
   const int lane = threadIdx.x & 63, ngrid = g.by1 - by0 + 1, nrows = ngrid + (xlen > 0 ? 1 : 0);
   for (int r0 = 0; r0 < nrows; r0 += 64) {
     const int r = r0 + lane, nr = min(64, nrows - r0);

@@ -299,6 +299,17 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.Ecap = r64(cfg->blob_cap > 0 ? cfg->blob_cap : 4 * d.B + 256);
   d.Pcap = r64(cfg->pellet_cap > 0 ? cfg->pellet_cap : (int)std::ceil(d.max_pellets) + d.Ecap + 64);
   d.Vcap = r64(cfg->virus_cap > 0 ? cfg->virus_cap : 2 * (int)std::ceil(d.max_viruses) + 64);
+  // the pellet row store (aigar_dev.h): per bucket row a home of PR slots, twice;
+  // PR leaves a quarter of headroom over the row's share of Pcap (uniform spawns
+  // put ~Pcap / cols pellets in a row) plus 64
+  if (d.cols > 1024) {
+    delete h;
+    return fail("aigar_create: field size %d: more than 1024 bucket rows", d.size);
+  }
+  d.PR = r64((int)std::ceil(1.25 * d.Pcap / d.cols) + 64);
+  d.PS = 2 * d.cols * d.PR;
+  d.PD = d.PS + d.Pcap;
+  d.PH1 = d.cols * (d.cols + 1) + 1;
   d.Wcap = std::max(kMaxCells * d.B, std::max(d.Ecap, 4096));
   d.EVcap = cfg->event_cap > 0 ? cfg->event_cap : 65536;
   d.G = G;
@@ -399,14 +410,11 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(c_flags, uint32_t, C); AL(c_seq, int64_t, C); AL(c_active, uint8_t, C);
   AL(sp_r, double, C); AL(sp_svx, double, C); AL(sp_svy, double, C);
   AL(sb_x, double, C); AL(sb_y, double, C); AL(sb_svx, double, C); AL(sb_svy, double, C); AL(sb_slot, uint8_t, C);
-  const size_t P = A * d.Pcap;
-  for (int b = 0; b < 2; b++) {
-    AL(pel[b], PelRec, P);
-    AL(pel_col[b], int, P);
-  }
+  const size_t P = A * d.Pcap, PSA = A * d.PS, PDA = A * d.PD, PHA = A * d.PH1;
+  AL(pel, PelRec, PSA); AL(pel_col, int, PSA);
   AL(pn, PelRec, P); AL(pn_col, int, P);
-  AL(pel_dead, uint8_t, P); AL(pel_rank, int, 2 * P); AL(pcnt, int, A * H1); AL(pncnt, int, A * H1); AL(pstart, int, A * H1);
-  AL(pel_owner, uint64_t, P);
+  AL(pel_dead, uint8_t, PDA); AL(pel_rank, int, P); AL(pncnt, int, PHA); AL(pstart, int, PHA);
+  AL(pel_owner, uint64_t, PDA);
   const size_t E = A * d.Ecap, V = A * d.Vcap;
   AL(b_x, double, E); AL(b_y, double, E); AL(b_m, double, E); AL(b_r, double, E); AL(b_vx, double, E);
   AL(b_vy, double, E); AL(b_svx, double, E); AL(b_svy, double, E); AL(b_svc, int, E); AL(b_seq, int64_t, E);
@@ -430,7 +438,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(scan_state, unsigned long long, 2 * A * d.scan_tiles);
   AL(pl_state, unsigned long long, A * d.pl_tiles);
   AL(ticket, int, 16);
-  AL(kill_list, int, P); AL(spec_x, double, A * 64); AL(spec_y, double, A * 64); AL(spec_m, double, A * 64); AL(stg_key, int64_t, 2 * P); AL(pu_tmp, int64_t, 2 * P); AL(pbc, int, A * d.H);
+  AL(kill_list, int, P); AL(spec_x, double, A * 64); AL(spec_y, double, A * 64); AL(spec_m, double, A * 64); 
   AL(ob_used, unsigned long long, 1);
   AL(ob_epoch, uint32_t, 1);
   AL(p_split_lh, int, NP);
@@ -441,6 +449,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
     AL(t_holder, int, NP);
     AL(t_obsby, int, NP);
     AL(t_holive, int, d.hcap);
+    AL(t_hoslot, int, d.hcap);
     AL(outbox, TileRec, h->box_recs);
     TileRec *ib = nullptr;
     ib = dalloc<TileRec>(h, (size_t)h->box_recs * d.ntiles);
@@ -1283,20 +1292,28 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
     HIPCHK(hipMemcpyAsync(cfl.data() + ho, d.c_flags + o, 4 * B, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipMemcpyAsync(cseq.data() + ho, d.c_seq + o, 8 * B, hipMemcpyDeviceToHost, h->stream));
   }
-  const size_t po = (size_t)arena * d.Pcap, bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;
+  const size_t po = (size_t)arena * d.PS, bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;
   std::vector<double> px, py, pm, bf[8], vf[8];
   std::vector<int64_t> ps, bseq, bej, vseq;
   std::vector<int> bsvc, vsvc, pcol, bcol;
   std::vector<uint32_t> bfl, vfl;
-  const int pb = c.pcur;
-  {
-    std::vector<PelRec> pr;
-    if (d2h(h, pr, d.pel[pb] + po, c.n_pel) || d2h(h, pcol, d.pel_col[pb] + po, c.n_pel)) return -1;
+  int n_pel = 0;
+  {  // the row store: each row's live records [entry 0, entry cols) of its current home
+    std::vector<int> pst;
+    std::vector<PelRec> store;
+    std::vector<int> scol;
+    if (d2h(h, pst, d.pstart + (size_t)arena * d.PH1, d.PH1) || d2h(h, store, d.pel + po, d.PS) ||
+        d2h(h, scol, d.pel_col + po, d.PS))
+      return -1;
     HIPCHK(hipStreamSynchronize(h->stream));  // (unpacked below)
-    px.resize(pr.size()); py.resize(pr.size()); pm.resize(pr.size()); ps.resize(pr.size());
-    for (size_t i = 0; i < pr.size(); i++) {
-      px[i] = pr[i].x; py[i] = pr[i].y; pm[i] = pr[i].m; ps[i] = pr[i].seq;
+    for (int r = 0; r < d.cols; r++) {
+      const int lo = pst[(size_t)r * (d.cols + 1)], hi = pst[(size_t)r * (d.cols + 1) + d.cols];
+      for (int i = lo; i < hi; i++) {
+        px.push_back(store[i].x); py.push_back(store[i].y); pm.push_back(store[i].m); ps.push_back(store[i].seq);
+        pcol.push_back(scol[i]);
+      }
     }
+    n_pel = (int)px.size();
   }
   double *bfs[8] = {d.b_x, d.b_y, d.b_m, d.b_r, d.b_vx, d.b_vy, d.b_svx, d.b_svy};
   double *vfs[8] = {d.v_x, d.v_y, d.v_m, d.v_r, d.v_vx, d.v_vy, d.v_svx, d.v_svy};
@@ -1319,7 +1336,7 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
   std::sort(bl.begin(), bl.end(), [&](int x, int y) { return bseq[x] < bseq[y]; });
   std::sort(vl.begin(), vl.end(), [&](int x, int y) { return vseq[x] < vseq[y]; });
   std::vector<int> pord;
-  for (int i = 0; i < c.n_pel; i++) {
+  for (int i = 0; i < n_pel; i++) {
     const int bx = std::min(d.cols - 1, std::max(0, (int)(px[i] / kBucket)));
     const int by = std::min(d.cols - 1, std::max(0, (int)(py[i] / kBucket)));
     if (bx >= d.own_bx0 && bx < d.own_bx1 && by >= d.own_by0 && by < d.own_by1) pord.push_back(i);  // (tiles: owned)
@@ -1498,20 +1515,24 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
     pc.push_back(st->pellets_col ? (int)st->pellets_col[i] : -1);
   }
   host_grid(d.cols, px, py, start, order);
-  {
-    std::vector<PelRec> sr(order.size());
-    std::vector<int> sc(order.size());
-    for (size_t i = 0; i < order.size(); i++) {
-      sr[i] = PelRec{px[order[i]], py[order[i]], pm[order[i]], ps[order[i]]};
-      sc[i] = pc[order[i]];
+  {  // the row store, every row in home 0 (aigar_dev.h)
+    const int C = d.cols;
+    std::vector<PelRec> sr(d.PS);
+    std::vector<int> sc(d.PS, -1), pst(d.PH1, 0);
+    for (int r = 0; r < C; r++) {
+      const int b0 = start[(size_t)r * C], n = start[(size_t)(r + 1) * C] - b0, base = r * d.PR;
+      if (n > d.PR) return fail("load_state: %d pellets in bucket row %d, more than its %d slots", n, r, d.PR);
+      for (int bx = 0; bx <= C; bx++) pst[(size_t)r * (C + 1) + bx] = base + (start[(size_t)r * C + bx] - b0);
+      for (int k = 0; k < n; k++) {
+        const int i = order[b0 + k];
+        sr[base + k] = PelRec{px[i], py[i], pm[i], ps[i]};
+        sc[base + k] = pc[i];
+      }
     }
-    const size_t po = (size_t)arena * d.Pcap;
-    if (h2d(h, d.pel[0] + po, sr) || h2d(h, d.pel_col[0] + po, sc)) return -1;
+    const size_t po = (size_t)arena * d.PS;
+    if (h2d(h, d.pel + po, sr) || h2d(h, d.pel_col + po, sc) || h2d(h, d.pstart + (size_t)arena * d.PH1, pst))
+      return -1;
     HIPCHK(hipStreamSynchronize(h->stream));  // (the host records go out of scope)
-    HIPCHK(hipMemcpyAsync(d.pstart + arena * H1, start.data(), 4 * H1, hipMemcpyHostToDevice, h->stream));
-    std::vector<int> cnt(d.H);  // per-bucket counts (the closing update keeps them with pstart)
-    for (int b = 0; b < d.H; b++) cnt[b] = start[b + 1] - start[b];
-    if (h2d(h, d.pbc + (size_t)arena * d.H, cnt)) return -1;
   }
   // blobs and viruses in list order; blob grid for completeness, virus grid for observations
   const size_t bo = (size_t)arena * d.Ecap, vo = (size_t)arena * d.Vcap;
@@ -1565,11 +1586,11 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   c.rmax_cell = std::max(rmax_c, std::sqrt(10.0 / 3.141592653589793));
   c.rmax_virus = std::max(rmax_v, std::sqrt(100.0 / 3.141592653589793));
   c.food_round = 1;  // reservation epochs restart: clear this arena's keys
-  HIPCHK(hipMemsetAsync(d.pel_owner + (size_t)arena * d.Pcap, 0, 8 * (size_t)d.Pcap, h->stream));
+  HIPCHK(hipMemsetAsync(d.pel_owner + (size_t)arena * d.PD, 0, 8 * (size_t)d.PD, h->stream));
   HIPCHK(hipMemsetAsync(d.b_owner + (size_t)arena * d.Ecap, 0, 8 * (size_t)d.Ecap, h->stream));
   // look-back epochs restart too: clear this arena's tile states
   HIPCHK(hipMemsetAsync(d.pl_state + (size_t)arena * d.pl_tiles, 0, 8 * (size_t)d.pl_tiles, h->stream));
-  HIPCHK(hipMemsetAsync(d.pel_dead + (size_t)arena * d.Pcap, 0, (size_t)d.Pcap, h->stream));  // buffer 0 is current
+  HIPCHK(hipMemsetAsync(d.pel_dead + (size_t)arena * d.PD, 0, (size_t)d.PD, h->stream));
   HIPCHK(hipMemsetAsync(d.cgcnt + (size_t)arena * 2 * 4100, 0, sizeof(int) * 2 * 4100, h->stream));
   for (int sl = 0; sl < 2; sl++)
     HIPCHK(hipMemsetAsync(d.scan_state + ((size_t)sl * d.A + arena) * d.scan_tiles, 0, 8 * (size_t)d.scan_tiles,

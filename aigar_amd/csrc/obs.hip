@@ -150,7 +150,8 @@ __device__ __forceinline__ void wave_fov_walk_k(const Dev &d, int a, Rect Q, dou
   const int Ev = (int)ceil((rv + 1.0) / kBucket) + 1;
   const double h = fs / 2;
   // pellets weigh 1-3, or 14.4 when converted from a blob: radius < 2.2
-  const Span sp = clip_to_fov(grid_span(Q, 1, d.cols, 0), fx, fy, h, 2.2, d.cols, 0);
+  Span sp = clip_to_fov(grid_span(Q, 1, d.cols, 0), fx, fy, h, 2.2, d.cols, 0);
+  sp.stride = d.cols + 1;  // (pellet rows keep one more entry: the row's end)
 #ifdef AIGAR_OBS_CLIP_ALL
   const Span sc = clip_to_fov(grid_span(Q, Ec, d.cols, d.cshift_c), fx, fy, h, rc, d.cols, d.cshift_c);
   const Span sv = clip_to_fov(grid_span(Q, Ev, d.cols, d.cshift), fx, fy, h, rv, d.cols, d.cshift);
@@ -162,7 +163,7 @@ __device__ __forceinline__ void wave_fov_walk_k(const Dev &d, int a, Rect Q, dou
   const int nv_rows = (qok && want_v) ? span_rows(sv) : 0;
   const int nrows = np_rows + nc_rows + nv_rows;
   const size_t H1 = (size_t)a * (d.H + 1);
-  const int *pst = d.pstart + H1, *cst = d.cstart + H1, *vst = d.vstart + H1;
+  const int *pst = d.pstart + (size_t)a * d.PH1, *cst = d.cstart + H1, *vst = d.vstart + H1;
   const int *cit = d.citems + (size_t)a * kMaxCells * d.B, *vit = d.vitems + (size_t)a * d.Vcap;
   if (nrows <= 0) pre();
   for (int r0 = 0; r0 < nrows; r0 += 64) {
@@ -198,7 +199,7 @@ __device__ __forceinline__ void wave_fov_walk_k(const Dev &d, int a, Rect Q, dou
       const int kd = __shfl(kind, rw);
       const bool valid = t < total;
       size_t g = 0;
-      if (valid) g = kd == 0 ? (size_t)a * d.Pcap + idx : (kd == 1 ? (size_t)cit[idx] : (size_t)a * d.Vcap + vit[idx]);
+      if (valid) g = kd == 0 ? (size_t)a * d.PS + idx : (kd == 1 ? (size_t)cit[idx] : (size_t)a * d.Vcap + vit[idx]);
       f(valid, kd, g);
     }
   }
@@ -285,7 +286,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const int oslot = lane < kMaxCells ? (int)d.p_list[lane * NP + gp] : 0;
   const ArenaCtl &ctl = d.ctl[a];
   const double rmax_c = ctl.rmax_cell, rmax_v = ctl.rmax_virus;  // (the walk's grid expansions)
-  const int pcur = ctl.pcur;                                      // current pellet buffer
   if (!alive) {  // getStateRepresentation returns None for dead players
     for (int i = lane; i < L; i += 64) row_st(i, (OutT)__builtin_nan(""));
     return;
@@ -365,7 +365,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
                   [&](bool valid, int kd, size_t g) {
       // per-lane base and stride: a pellet is one 32-byte record (x, y, m, seq), the
       // other kinds structure-of-arrays -- one load instruction per field either way
-      const PelRec *PR = d.pel[pcur];
+      const PelRec *PR = d.pel;
       const double *X = kd == 0 ? &PR->x : (kd == 1 ? d.c_x : d.v_x);
       const double *Y = kd == 0 ? &PR->y : (kd == 1 ? d.c_y : d.v_y);
       const double *M = kd == 0 ? &PR->m : (kd == 1 ? d.c_m : d.v_m);
@@ -864,14 +864,13 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   bx = __shfl(bx, bl);
   by = __shfl(by, bl);
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
-  const int pcur = ctl.pcur;
   double best = -1;
   uint64_t bord = ~0ull;
   double tx = 0, ty = 0;
   wave_fov_walk(d, a, Q, fx, fy, fs, ctl.rmax_cell, ctl.rmax_virus, true, d.virus_enabled, [] {},
                 [&](bool valid, int kd, size_t g) {
     if (!valid) return;
-    const PelRec *PR = d.pel[pcur];
+    const PelRec *PR = d.pel;
     const double *X = kd == 0 ? &PR->x : (kd == 1 ? d.c_x : d.v_x);
     const double *Y = kd == 0 ? &PR->y : (kd == 1 ? d.c_y : d.v_y);
     const double *M = kd == 0 ? &PR->m : (kd == 1 ? d.c_m : d.v_m);

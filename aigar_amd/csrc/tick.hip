@@ -25,7 +25,8 @@
 //                             incl. skip-after-removal, re-activating neighbours on growth)
 //                             opens k_spawn_plan
 //   k_spawn_plan/all          spawnStuff               field.py:256-313
-//   k_scan_lb, k_pgrid_scatter closing pellet rebuild; extra blocks refresh the FOV cache
+//   k_pel_update              closing pellet update: the bucket rows whose pellets changed are
+//                             rewritten; extra blocks respawn players (FOV cache) and spawn viruses
 // "last block" = the block that draws the last ticket (last_block): an idle
 // serial pass then costs a ticket, not a dependent launch.
 #include <hip/hip_runtime.h>
@@ -241,7 +242,7 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
   if (i >= d.ctl[a].n_blob || !(d.b_flags[gi] & F_ALIVE)) return;
   if (d.b_svc[gi] == 0) {  // stopped blob becomes a pellet (addPellet)
     int j = atomicAdd(&d.ctl[a].n_pnew, 1);
-    if (d.ctl[a].n_pel + j >= d.Pcap) {  // (eat-phase index n_pel + j must fit, see Food)
+    if (j >= d.Pcap) {  // (the staging list; eat-phase index PS + j, see Food)
       set_err(d, a, ERR_PELLET_CAP);
       return;
     }
@@ -654,7 +655,7 @@ __device__ void tick_zero(const Dev &d, int gi) {
   for (long t = gi; t < (long)d.A * d.Ecap; t += kTickZero) {
     const int a = (int)(t / d.Ecap), j = (int)(t - (long)a * d.Ecap);
     const ArenaCtl &c = d.ctl[a];
-    if (j < c.pu_nconv && c.pu_n0 + j < d.Pcap) d.pel_dead[(size_t)a * d.Pcap + c.pu_n0 + j] = 0;
+    if (j < c.pu_nconv) d.pel_dead[(size_t)a * d.PD + d.PS + j] = 0;
   }
 }
 // C4: the tick's first pass opens with the observation hand-off plan: extra
@@ -671,20 +672,6 @@ __device__ void tick_zero(const Dev &d, int gi) {
 // (t_holive); tile_plan_live, in the message's last block, gives them the slots
 // the dead left, and the rest keep their holder a tick longer: their centre moved
 // at most one tick's distance from the tile, which the halo covers.
-__device__ void tile_hist_slot(const Dev &d, int gp, int sl) {
-  const int GG = d.G * d.G;
-  TileRec *slot = d.outbox + 1 + d.tcap + (size_t)sl * d.hrec;
-  slot->kind = TR_HIST;
-  slot->idx = gp;
-  slot->seq = 0;
-  slot->x = d.o_lastfov[gp];
-  slot->y = 0;
-  double *dst = (double *)(slot + 1);
-  for (int g = 0; g < d.nh; g++) {
-    const double *src = hist_grid(d, g) + (size_t)gp * GG;
-    for (int t = 0; t < GG; t++) dst[g * GG + t] = src[t];
-  }
-}
 __device__ void tile_plan_thread(const Dev &d, int gp) {
   ArenaCtl &c = d.ctl[0];
   if (gp == 0) {  // the first pass's counters
@@ -712,10 +699,13 @@ __device__ void tile_plan_thread(const Dev &d, int gp) {
     return;
   }
   d.t_holder[gp] = -1;
-  tile_hist_slot(d, gp, sl);
+  d.t_hoslot[sl] = gp;  // (its history is copied into the slot by tile_plan_live, block-parallel)
 }
-// the live bots' hand-offs, in the slots the dead left (one block, first pass;
-// lowest player index first, so the choice does not depend on atomic order)
+// The first pass's hand-off slots, in the message's last block: the live bots
+// take the slots the dead left (lowest player index first, so the choice does
+// not depend on atomic order), then the whole block copies every slot's
+// history -- [TR_HIST record: player, lastFovSize][nh grids] -- element by
+// element (a thread per bot copying its ~250 doubles serially took ~4 us)
 __device__ void tile_plan_live(const Dev &d) {
   ArenaCtl &c = d.ctl[0];
   __shared__ int s_q[kHcapMax];
@@ -728,11 +718,26 @@ __device__ void tile_plan_live(const Dev &d) {
     for (int j = 0; j < nq; j++) r += s_q[j] < gp;
     if (r < room) {
       d.t_holder[gp] = -1;
-      tile_hist_slot(d, gp, nd + r);
+      d.t_hoslot[nd + r] = gp;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) c.n_ho = nd + min(nq, room);
+  const int ns = nd + min(nq, room), GG = d.G * d.G, per = 1 + d.nh * GG;
+  for (int e = threadIdx.x; e < ns * per; e += blockDim.x) {
+    const int sl = e / per, j = e - sl * per, gp = d.t_hoslot[sl];
+    TileRec *slot = d.outbox + 1 + d.tcap + (size_t)sl * d.hrec;
+    if (j == 0) {
+      slot->kind = TR_HIST;
+      slot->idx = gp;
+      slot->seq = 0;
+      slot->x = d.o_lastfov[gp];
+      slot->y = 0;
+    } else {
+      const int q = j - 1, g = q / GG, t = q - g * GG;
+      ((double *)(slot + 1))[q] = hist_grid(d, g)[(size_t)gp * GG + t];
+    }
+  }
+  if (threadIdx.x == 0) c.n_ho = ns;
 }
 __global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
   FLOOR(0);
@@ -1221,259 +1226,97 @@ __device__ void cgrid_scatter_block(const Dev &d, int a, int bx) {
 
 // blocks [0, A): blob grids; [A, 2A): virus grids (when enabled)
 
-// Single-pass multi-block exclusive scan with decoupled look-back.  Grid
-// (tiles, arenas), 256 threads, LB_TILE counts per block.  Each tile publishes
-// one self-contained 64-bit word {status:2 | epoch:30 | value:32} with an
-// agent-scope store; successors read it with agent-scope loads (L1 bypass), so
-// no other data needs ordering.  The epoch (ArenaCtl::scan_epoch, bumped by the
-// last block of every launch) makes stale words of earlier launches invisible,
-// so the state array is never cleared -- graph replays stay valid.
-constexpr int LB_TILE = 2048, LB_PER = LB_TILE / 256;
-constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
-__device__ __forceinline__ unsigned long long lb_word(unsigned long long st, uint32_t ep, uint32_t v) {
-  return st | ((unsigned long long)(ep & 0x3FFFFFFFu) << 32) | v;
+// ------------------------------------------------------------ pellet rows
+// The pellet store (aigar_dev.h): bucket rows with two homes each.  Reset
+// (Field.initialize's spawnPellets, field.py:57-67, 303-313) places the staged
+// spawns by a counting sort -- atomic ranks per bucket, one block per row for
+// the row's bucket starts, then the records -- into home 0.  A tick changes a
+// few pellets (eaten: field.py:327-344; blob conversions: :99-110; spawns): the
+// closing update (k_pel_update) rewrites only the rows they touch.
+__device__ __forceinline__ int prow_entry(const Dev &d, int bx, int by) { return by * (d.cols + 1) + bx; }
+// staged record j: its rank in its bucket (tiles: -1 outside the held range)
+__global__ void k_prow_count(Dev d) {
+  const int gi = GTID;
+  if (gi >= d.A * d.Pcap) return;
+  const int a = gi / d.Pcap, j = gi - a * d.Pcap;
+  ArenaCtl &c = d.ctl[a];
+  if (j == 0) c.n_pel = 0;  // (k_prow_scan adds the rows' counts)
+  if (j >= c.n_pnew) return;
+  const PelRec r = d.pn[gi];
+  const int bx = center_bucket_coord(r.x, d.cols), by = center_bucket_coord(r.y, d.cols);
+  d.pel_rank[gi] = tile_holds_bucket(d, bx, by) ? atomicAdd(&d.pncnt[(size_t)a * d.PH1 + prow_entry(d, bx, by)], 1) : -1;
 }
-// pfix (pellet rebuilds): the block of the last tile, which knows the total,
-// closes the rebuild -- snapshot the source counts for the scatter, set the
-// new pellet count, empty the staging list; pfix 2 also closes the tick.
-// extra: this tick's spawns sit in the staging list uncommitted.
-__global__ void __launch_bounds__(256) k_scan_lb(Dev d, int *cnt, int *start, int *cnt2, int pfix, int extra,
-                                                 int slot) {
-  __shared__ int wsum[4];
-  __shared__ int s_total, s_prefix;
-  __shared__ uint32_t s_epoch;
-  const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = d.H, ntiles = gridDim.x;
-  int *c = cnt + (size_t)a * (d.H + 1);
-  int *c2 = cnt2 ? cnt2 + (size_t)a * (d.H + 1) : nullptr;  // optional second count array (summed, re-zeroed)
-  int *o = start + (size_t)a * (d.H + 1);
-  unsigned long long *st = d.scan_state + ((size_t)slot * d.A + a) * d.scan_tiles;
-  ArenaCtl &ctl = d.ctl[a];
-  if (tid == 0) s_epoch = __hip_atomic_load(&ctl.scan_epoch[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int base = tile * LB_TILE + tid * LB_PER;
-  int v[LB_PER], sum = 0;
-#pragma unroll
-  for (int j = 0; j < LB_PER; j++) {
-    int i = base + j;
-    v[j] = i < n ? c[i] + (c2 ? c2[i] : 0) : 0;
-    if (pfix && i < n) d.pbc[(size_t)a * d.H + i] = v[j];  // pellets: the bucket counts kept with pstart
-    sum += v[j];
-  }
-#pragma unroll
-  for (int j = 0; j < LB_PER; j++)
-    if (base + j < n) {
-      if (c2) c2[base + j] = 0;  // pellets: survivor counts are rewritten whole, staged counts re-zeroed
-      else c[base + j] = 0;      // counts re-zeroed for the next counting pass
-    }
-  // block exclusive scan of per-thread sums (4 waves)
-  int inc = sum;
+// block-wide exclusive scan of up to 4 values per thread (256 threads); returns the total
+__device__ __forceinline__ int block_scan4(int *v, int *wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int sum = v[0] + v[1] + v[2] + v[3], inc = sum;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    int y = __shfl_up(inc, off);
+    const int y = __shfl_up(inc, off);
     if (lane >= off) inc += y;
   }
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
+  int before = 0, total = 0;
+  for (int k = 0; k < 4; k++) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  __syncthreads();
+  int run = before + inc - sum;
+  for (int k = 0; k < 4; k++) {
+    const int x = v[k];
+    v[k] = run;
+    run += x;
+  }
+  return total;
+}
+// one block per (row, arena): the row's bucket starts in home 0 (cols <= 1024)
+__global__ void __launch_bounds__(256) k_prow_scan(Dev d) {
+  __shared__ int wsum[4];
+  const int r = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, C = d.cols;
+  ArenaCtl &c = d.ctl[a];
+  int *cnt = d.pncnt + (size_t)a * d.PH1 + (size_t)r * (C + 1);
+  int *st = d.pstart + (size_t)a * d.PH1 + (size_t)r * (C + 1);
+  int v[4];
+  for (int k = 0; k < 4; k++) {
+    const int bx = tid * 4 + k;
+    v[k] = bx < C ? cnt[bx] : 0;
+  }
+  const int total = block_scan4(v, wsum), base = r * d.PR;
+  for (int k = 0; k < 4; k++) {
+    const int bx = tid * 4 + k;
+    if (bx < C) {
+      st[bx] = base + min(v[k], d.PR);
+      cnt[bx] = 0;  // (re-zeroed for the next reset)
+    }
+  }
   if (tid == 0) {
-    int t0 = wsum[0], t1 = wsum[1], t2 = wsum[2], t3 = wsum[3];
-    wsum[0] = 0;
-    wsum[1] = t0;
-    wsum[2] = t0 + t1;
-    wsum[3] = t0 + t1 + t2;
-    s_total = t0 + t1 + t2 + t3;
-  }
-  __syncthreads();
-  const uint32_t ep = s_epoch;
-  const int total = s_total;
-  if (w == 0) {
-    if (tile == 0) {
-      if (lane == 0) {
-        __hip_atomic_store(&st[0], lb_word(LB_INC, ep, (uint32_t)total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_prefix = 0;
-      }
-    } else {
-      if (lane == 0)
-        __hip_atomic_store(&st[tile], lb_word(LB_AGG, ep, (uint32_t)total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      // parallel look-back over a window of up to 64 predecessors
-      int run = 0, hi = tile - 1;
-      for (;;) {
-        int t = hi - lane;
-        unsigned long long word = 0;
-        bool ready = true;
-        if (t >= 0) {
-          word = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ready = (word >> 62) != 0 && (uint32_t)((word >> 32) & 0x3FFFFFFFu) == (ep & 0x3FFFFFFFu);
-        }
-        if (!__all(ready)) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        bool is_inc = t >= 0 && (word >> 62) == 2;
-        unsigned long long incmask = __ballot(is_inc);
-        int stop = incmask ? __ffsll((long long)incmask) - 1 : 64;  // nearest inclusive predecessor
-        int val = (t >= 0 && lane <= stop) ? (int)(uint32_t)word : 0;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off);
-        run += val;
-        if (incmask || hi - 63 < 0) break;
-        hi -= 64;
-      }
-      if (lane == 0) {
-        __hip_atomic_store(&st[tile], lb_word(LB_INC, ep, (uint32_t)(run + total)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        s_prefix = run;
-      }
-    }
-  }
-  __syncthreads();
-  int run = s_prefix + (inc - sum) + wsum[w];
-#pragma unroll
-  for (int j = 0; j < LB_PER; j++) {
-    int i = base + j;
-    if (i < n) o[i] = run;
-    run += v[j];
-  }
-  if (tile == ntiles - 1 && tid == 0) {
-    o[n] = s_prefix + total;
-    if (pfix) {
-      ctl.src_n_pel = ctl.n_pel;
-      ctl.src_n_stage = ctl.n_pnew + (extra ? ctl.n_spawn_p : 0);
-      ctl.src_n_conv = extra ? ctl.n_pnew : 0;
-      ctl.n_pel = min(s_prefix + total, d.Pcap);
-      ctl.n_pnew = 0;
-      ctl.n_pel_eaten = 0;
-      if (pfix == PR_CLOSE) {
-        ctl.tick += 1;
-        ctl.pcur = ctl.peat ^ 1;
-        ctl.peat = ctl.pcur;  // the next eat phase reads the buffer built here
-      }
-    }
-  }
-  if (tid == 0) {  // last block of this launch bumps the epoch
-    int tk = atomicAdd(&ctl.scan_ticket[slot], 1);
-    if (tk == ntiles - 1) {
-      ctl.scan_ticket[slot] = 0;
-      __hip_atomic_fetch_add(&ctl.scan_epoch[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st[C] = base + min(total, d.PR);
+    if (total > d.PR) set_err(d, a, ERR_PELLET_CAP);
+    atomicAdd(&c.n_pel, min(total, d.PR));
+    if (r == 0) {
+      c.src_n_stage = c.n_pnew;  // (k_prow_scatter's bound; nothing here reads n_pnew)
+      c.n_pnew = 0;
+      c.n_pel_eaten = 0;
     }
   }
 }
-
-// Pellet records: (src buffer [- dead]) U staging -> dst buffer, sorted by
-// centre bucket.  The source is itself bucket-sorted (it is the output of the
-// previous rebuild, or of load_state's host sort) and pstart still describes
-// it, so survivors need no atomics: one thread per bucket ranks the live
-// records of its (short) range and writes the bucket's survivor count.  Staged
-// records (blob conversions, spawns) take atomic ranks in pncnt and fill their
-// bucket from the end.  Order inside a bucket carries no meaning: every
-// consumer ranks candidates by creation sequence.
-// survivors of source bucket i: ranks and count (no atomics)
-__device__ __forceinline__ void pgrid_count_bucket(const Dev &d, int a, int i, int use_dead) {
-  const ArenaCtl &c = d.ctl[a];
-  const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
-  const int lo = min(d.pstart[H1 + i], c.n_pel), hi = min(d.pstart[H1 + i + 1], c.n_pel);  // (empty source at reset)
-  int k = 0;
-  for (int t = lo; t < hi; t++) {
-    if (use_dead && d.pel_dead[(size_t)a * d.Pcap + t]) continue;
-    d.pel_rank[R0 + t] = k++;
-  }
-  d.pcnt[H1 + i] = k;
-}
-// staged record j (index into the staging list): atomic rank in its bucket
-// (tiles: a record outside the held range is dropped, rank -1)
-__device__ __forceinline__ void pgrid_rank_staged(const Dev &d, int a, int j) {
-  const size_t g = (size_t)a * d.Pcap + j, H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
-  const int bx = center_bucket_coord(d.pn[g].x, d.cols), by = center_bucket_coord(d.pn[g].y, d.cols);
-  if (!tile_holds_bucket(d, bx, by)) {
-    d.pel_rank[R0 + d.Pcap + j] = -1;
-    return;
-  }
-  d.pel_rank[R0 + d.Pcap + j] = atomicAdd(&d.pncnt[H1 + by * d.cols + bx], 1);
-}
-// mode PR_RESET: staging -> buffer 0 (Field.initialize; a tick closes through
-// k_spawn_plan + k_pel_update instead)
-__global__ void k_pgrid_count(Dev d, int mode) {
+__global__ void k_prow_scatter(Dev d) {
   const int gi = GTID;
-  const int per = d.H + d.Pcap;
-  if (gi >= d.A * per) return;
-  const int a = gi / per, i = gi - a * per;
-  if (i < d.H) {  // bucket i of the source layout
-    pgrid_count_bucket(d, a, i, 0);
-    return;
-  }
-  const int j = i - d.H;
-  if (j < d.ctl[a].n_pnew) pgrid_rank_staged(d, a, j);
-}
-// the source counts were snapshotted by the scan's epilogue (src_n_pel, src_n_stage)
-__device__ __forceinline__ void pgrid_scatter_one(const Dev &d, int gi, int mode) {
-  const int per = 2 * d.Pcap;
-  if (gi >= d.A * per) return;
-  const int a = gi / per, i = gi - a * per;
-  const ArenaCtl &c = d.ctl[a];
-  const bool use_dead = mode == PR_CLOSE;
-  // (PR_CLOSE: the scan's epilogue already made the destination current)
-  const int src = mode == PR_RESET ? 1 : c.pcur ^ 1, dst = src ^ 1;
-  const size_t H1 = (size_t)a * (d.H + 1), R0 = (size_t)a * 2 * d.Pcap;
-  double x, y, m;
-  int64_t s;
-  int pos, col;
-  if (i < d.Pcap) {
-    if (i >= c.src_n_pel) return;
-    size_t g = (size_t)a * d.Pcap + i;
-    if (use_dead && d.pel_dead[g]) {  // eaten: drop it, and leave the flags clean for the next eat phase
-      d.pel_dead[g] = 0;
-      return;
-    }
-    {
-      const PelRec r_ = d.pel[src][g];
-      x = r_.x;
-      y = r_.y;
-      m = r_.m;
-      s = r_.seq;
-    }
-    col = d.pel_col[src][g];
-    int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-    pos = d.pstart[H1 + b] + d.pel_rank[R0 + i];
-  } else {
-    int j = i - d.Pcap;
-    if (j >= c.src_n_stage) return;
-    size_t g = (size_t)a * d.Pcap + j;
-    if (use_dead && j < c.src_n_conv) {  // blob conversion: eat-phase index src_n_pel + j
-      const size_t ge = (size_t)a * d.Pcap + c.src_n_pel + j;
-      if (d.pel_dead[ge]) {
-        d.pel_dead[ge] = 0;
-        return;
-      }
-    }
-    const int rk = d.pel_rank[R0 + d.Pcap + j];
-    if (rk < 0) return;  // (tiles: not held here)
-    {
-      const PelRec r_ = d.pn[g];
-      x = r_.x;
-      y = r_.y;
-      m = r_.m;
-      s = r_.seq;
-    }
-    col = d.pn_col[g];
-    int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-    pos = d.pstart[H1 + b + 1] - 1 - rk;
-  }
-  if (pos >= d.Pcap) {
-    set_err(d, a, ERR_PELLET_CAP);
-    return;
-  }
-  size_t o = (size_t)a * d.Pcap + pos;
-  d.pel[dst][o] = PelRec{x, y, m, s};
-  d.pel_col[dst][o] = col;
-  if (!use_dead) d.pel_dead[o] = 0;  // (dead flags of the source are being read when use_dead)
-}
-// fov_blocks > 0 (the tick's closing rebuild): the last fov_blocks blocks
-// refresh the FOV cache instead -- the player state is final by then, and the
-// pellet records the scatter moves are not part of it
-__global__ void __launch_bounds__(256) k_pgrid_scatter(Dev d, int mode, int fov_blocks) {
-  const int nsc = gridDim.x - fov_blocks;
-  if ((int)blockIdx.x >= nsc) return fov_cache_thread(d, (blockIdx.x - nsc) * 256 + threadIdx.x);
-  pgrid_scatter_one(d, GTID, mode);
+  if (gi >= d.A * d.Pcap) return;
+  const int a = gi / d.Pcap, j = gi - a * d.Pcap;
+  if (j >= d.ctl[a].src_n_stage) return;
+  const int rk = d.pel_rank[gi];
+  if (rk < 0) return;  // (tiles: not held here)
+  const PelRec r = d.pn[gi];
+  const int bx = center_bucket_coord(r.x, d.cols), by = center_bucket_coord(r.y, d.cols);
+  const int e = (int)((size_t)a * d.PH1) + prow_entry(d, bx, by);
+  const int pos = d.pstart[e] + rk;
+  if (pos >= d.pstart[e + 1]) return;  // (row overflow: ERR_PELLET_CAP is set)
+  const size_t o = (size_t)a * d.PS + pos;
+  d.pel[o] = r;
+  d.pel_col[o] = d.pn_col[gi];
 }
 // ------------------------------------------------------------ T10 merge
 __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
@@ -1911,9 +1754,9 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 // and [n0, n0 + nst) (this tick's blob conversions, addPellet in updateBlobs,
 // still in the staging list -- they join the sorted buffer at the closing
 // rebuild, so no rebuild runs before the eat phase); blobs kBlobBit | slot.
-// Pellet dead flags and reservation words are indexed by a * Pcap + j.
+// Pellet dead flags and reservation words are indexed by a * PD + j.
 constexpr int kBlobBit = 1 << 30;
-// a buffer pellet killed this tick, for the closing update (each once: a tile
+// a store pellet killed this tick, for the closing update (each once: a tile
 // applying another tile's kill notes it only if its own eat phase did not)
 __device__ __forceinline__ void note_kill(const Dev &d, int a, int j) {
   const int k = atomicAdd(&d.ctl[a].n_kill, 1);
@@ -1922,21 +1765,21 @@ __device__ __forceinline__ void note_kill(const Dev &d, int a, int j) {
 }
 struct Food {
   const Dev &d;
-  int a, pb;  // pb: the eat-phase pellet buffer (ArenaCtl::peat)
-  int n0, nst;
+  int a;
+  int n0, nst;  // n0: the store's slots (PS); staged records (this tick's blob conversions) follow
   int nblob;  // (the blob list's length is fixed during the eat phase: loaded with the rest, no round of its own)
-  __device__ Food(const Dev &dd, int aa)
-      : d(dd), a(aa), pb(dd.ctl[aa].peat), n0(dd.ctl[aa].n_pel), nst(dd.ctl[aa].n_pnew), nblob(dd.ctl[aa].n_blob) {}
+  __device__ Food(const Dev &dd, int aa) : d(dd), a(aa), n0(dd.PS), nst(dd.ctl[aa].n_pnew), nblob(dd.ctl[aa].n_blob) {}
   __device__ static bool blob(int j) { return (j & kBlobBit) != 0; }
-  __device__ size_t g(int j) const { return (size_t)a * d.Pcap + j; }               // pellet j
+  __device__ size_t g(int j) const { return (size_t)a * d.PD + j; }                 // pellet j's flag / key
+  __device__ size_t gp(int j) const { return (size_t)a * d.PS + j; }                // store pellet j's record
   __device__ size_t gs(int j) const { return (size_t)a * d.Pcap + (j - n0); }       // staged pellet j
   __device__ size_t gb(int j) const { return (size_t)a * d.Ecap + (j & ~kBlobBit); }  // blob
-  __device__ double x(int j) const { return blob(j) ? d.b_x[gb(j)] : (j < n0 ? d.pel[pb][g(j)].x : d.pn[gs(j)].x); }
-  __device__ double y(int j) const { return blob(j) ? d.b_y[gb(j)] : (j < n0 ? d.pel[pb][g(j)].y : d.pn[gs(j)].y); }
-  __device__ double m(int j) const { return blob(j) ? d.b_m[gb(j)] : (j < n0 ? d.pel[pb][g(j)].m : d.pn[gs(j)].m); }
+  __device__ double x(int j) const { return blob(j) ? d.b_x[gb(j)] : (j < n0 ? d.pel[gp(j)].x : d.pn[gs(j)].x); }
+  __device__ double y(int j) const { return blob(j) ? d.b_y[gb(j)] : (j < n0 ? d.pel[gp(j)].y : d.pn[gs(j)].y); }
+  __device__ double m(int j) const { return blob(j) ? d.b_m[gb(j)] : (j < n0 ? d.pel[gp(j)].m : d.pn[gs(j)].m); }
   __device__ double r(int j) const { return blob(j) ? d.b_r[gb(j)] : pellet_radius(m(j)); }
   __device__ int64_t seq(int j) const {
-    return blob(j) ? d.b_seq[gb(j)] : (j < n0 ? d.pel[pb][g(j)].seq : d.pn[gs(j)].seq);
+    return blob(j) ? d.b_seq[gb(j)] : (j < n0 ? d.pel[gp(j)].seq : d.pn[gs(j)].seq);
   }
   // the whole food record in one round of loads (a pellet: its 32-byte record)
   __device__ void load(int j, double &x, double &y, double &m, int64_t &sq) const {
@@ -1947,7 +1790,7 @@ struct Food {
       m = d.b_m[b];
       sq = d.b_seq[b];
     } else {
-      const PelRec r = j < n0 ? d.pel[pb][g(j)] : d.pn[gs(j)];
+      const PelRec r = j < n0 ? d.pel[gp(j)] : d.pn[gs(j)];
       x = r.x;
       y = r.y;
       m = r.m;
@@ -1980,7 +1823,7 @@ struct Food {
   // every pellet / blob whose footprint may touch q: f(valid, j) on all lanes (wave-uniform calls)
   template <class Fn>
   __device__ void walk_pellets(Rect q, Fn f) const {
-    wave_grid_for(d.pstart + (size_t)a * (d.H + 1), nullptr, d.cols, q, 1, f, 0, n0, nst);  // (+ staged)
+    wave_grid_for(d.pstart + (size_t)a * d.PH1, nullptr, d.cols, q, 1, f, 0, n0, nst, d.cols + 1);  // (+ staged)
   }
   template <class Fn>
   __device__ void walk_blobs(Rect q, Fn f) const {
@@ -3359,234 +3202,27 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
 __device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait);
 // ---------------------------------------------------- closing pellet update
 // Pellets never move and only a few change per tick (eaten, spawned, converted
-// from blobs), so the end-of-tick pellet layout (bucket-sorted, double buffered)
-// is an update, not a re-sort: with K = the killed buffer indices and S = the
-// joining staged records' (bucket, index) keys, both sorted,
-//   survivor i of bucket b:  i - |K < i| + |S in buckets < b|
-//   bucket b's new start:    start(b) - |K < start(b)| + |S in buckets < b|
-// and bucket b's staged records follow its survivors.  k_spawn_plan builds and
-// sorts K and S; k_pel_update moves every record and rewrites every bucket's
-// start and count in one launch (no scan).
+// from blobs): the closing update (k_pel_update) rewrites only the bucket rows
+// those touch, each into its other home.  Step 1, by the arena's block of
+// k_spawn_plan after the spawn counts: this tick's pellet spawns are staged
+// (spawnPellets, field.py:303-313) -- the first kSpawnAhead were drawn by
+// k_tick_begin already (spec_*) -- and the tick's pellet bookkeeping closes.
 __device__ void spawn_pellet_at(const Dev &d, int a, int j, double *px, double *py);
-// bitonic sort of v[0..n) ascending by the whole block (v: LDS or global, with
-// room for n rounded up to a power of two)
-__device__ void block_bitonic_i64(int64_t *v, int n) {
-  const int T = blockDim.x, tid = threadIdx.x;
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int i = n + tid; i < np2; i += T) v[i] = INT64_MAX;
-  __syncthreads();
-  for (int k = 2; k <= np2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = tid; t < np2 / 2; t += T) {
-        const int i = 2 * j * (t / j) + (t % j), l = i + j;
-        const int64_t x = v[i], y = v[l];
-        if ((x > y) == ((i & k) == 0)) {
-          v[i] = y;
-          v[l] = x;
-        }
-      }
-      __syncthreads();
-    }
-}
-__device__ __forceinline__ int pow2_at_least(int n) {
-  int p = 1;
-  while (p < n) p <<= 1;
-  return p;
-}
-// ascending bitonic sort of one value per lane across the wavefront (64 lanes)
-__device__ __forceinline__ int64_t wave_sort_i64(int64_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1)
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int64_t o = __shfl_xor(v, j);
-      const bool lower = (lane & j) == 0, up = (lane & k) == 0;
-      v = (lower == up) ? (v < o ? v : o) : (v < o ? o : v);
-    }
-  return v;
-}
-// step 1, one block per arena after the spawn counts: this tick's pellet spawns
-// into the staging list (spawnPellets, field.py:258-265); the staged records that
-// join the buffer -- blob conversions nobody ate, spawns (tiles: those in the
-// held range) -- as sorted (bucket << 32 | staging index) keys; the killed
-// buffer indices sorted and made unique.  Then the tick's pellet bookkeeping
-// closes here (the update reads pu_*): new count, staging emptied, the buffer
-// the update builds made current.  A usual tick (<= 64 staged, <= 64 kills)
-// only hands over pu_*: k_pel_update's blocks sort the short lists themselves.  The tick counter advances in k_pel_update
-// (its respawn threads key on tick_sp).  lds: 4096 free int64.
-constexpr int PU_LDS = 4096;
-constexpr int PU_SH = 2048;  // k_pel_update: kill / staged lists up to this length sit in LDS
-__device__ __forceinline__ void pellet_close_prep(const Dev &d, int a, int64_t *lds, int *sh) {
+__device__ __forceinline__ void pellet_close_prep(const Dev &d, int a) {
   ArenaCtl &c = d.ctl[a];
-  const int T = blockDim.x, tid = threadIdx.x;
-  const int n0 = c.n_pel, nconv = c.n_pnew, nsp = c.n_spawn_p, nst = nconv + nsp;
-  const int nk_raw = min(c.n_kill, d.Pcap);
-  int *kl = d.kill_list + (size_t)a * d.Pcap;
-  int64_t *key = d.stg_key + (size_t)a * 2 * d.Pcap;
-  __shared__ int s_n[2];
-  if (nst <= 64 && nsp <= kSpawnAhead && nk_raw <= 64) {
-    // the usual tick (a few dozen changes): every k_pel_update block builds the
-    // short lists itself (pellet_lists_wave), which also closes the bookkeeping
-    if (tid == 0) {
-      c.pu_src = c.peat;
-      c.pu_n0 = n0;
-      c.pu_nconv = nconv;
-      c.pu_small = 1;
-    }
-    return;
-  }
-  if (nst <= PU_SH && nk_raw <= PU_SH) {
-    // a busy tick (greedy crowds: hundreds of kills and spawns): the lists stay
-    // unsorted (the staged keys in staging order; kills are unique) and every
-    // k_pel_update block counts ranks over them in LDS -- no sorting network here
-    int ns = 0;
-    for (int j0 = 0; j0 < nst; j0 += T) {
-      const int j = j0 + tid;
-      bool live = false;
-      int64_t k = 0;
-      if (j < nst) {
-        double x, y;
-        if (j < nconv) {
-          const size_t g = (size_t)a * d.Pcap + j;
-          x = d.pn[g].x;
-          y = d.pn[g].y;
-          live = !d.pel_dead[(size_t)a * d.Pcap + n0 + j];
-        } else {
-          spawn_pellet_at(d, a, j - nconv, &x, &y);
-          live = true;
-        }
-        const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
-        live = live && tile_holds_bucket(d, bx, by);
-        k = ((int64_t)(by * d.cols + bx) << 32) | j;
-      }
-      int chunk;
-      const int pos = ns + block_rank(live, sh, &chunk);
-      if (live) key[pos] = k;
-      ns += chunk;
-    }
-    if (tid == 0) {
-      const int nn = n0 - nk_raw + ns;
-      c.n_stg = ns;
-      c.n_kill = nk_raw;
-      c.pu_src = c.peat;
-      c.pu_n0 = n0;
-      c.pu_nconv = nconv;
-      c.pu_small = 2;
-      if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
-      c.n_pel = min(nn, d.Pcap);
-      d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
-      c.n_pnew = 0;
-      c.n_pel_eaten = 0;
-      c.pcur = c.peat ^ 1;
-      c.peat = c.pcur;
-    }
-    return;
-  }
-  if (nst <= T && nk_raw <= T && nk_raw <= PU_LDS / 2) {
-    // one round of loads: the thread's staged record (a spawn is made here, in
-    // registers) and killed index; keys into LDS, both lists sorted there
-    int64_t *ks = lds, *kk = lds + PU_LDS / 2;
-    bool live = false;
-    int64_t k = 0, kv = INT64_MAX;
-    if (tid < nst) {
-      double x, y;
-      if (tid < nconv) {
-        const size_t g = (size_t)a * d.Pcap + tid;
-        x = d.pn[g].x;
-        y = d.pn[g].y;
-        live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
-      } else {
-        spawn_pellet_at(d, a, tid - nconv, &x, &y);
-        live = true;
-      }
-      const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
-      live = live && tile_holds_bucket(d, bx, by);
-      k = ((int64_t)(by * d.cols + bx) << 32) | tid;
-    }
-    if (tid < nk_raw) kv = kl[tid];
-    int chunk;
-    const int pos = block_rank(live, sh, &chunk);
-    if (live) ks[pos] = k;
-    if (tid < nk_raw) kk[tid] = kv;
-    const int ns = chunk;
-    block_bitonic_i64(ks, ns);
-    block_bitonic_i64(kk, nk_raw);
-    const bool keep = tid < nk_raw && (tid == 0 || kk[tid] != kk[tid - 1]);
-    int nu;
-    const int upos = block_rank(keep, sh, &nu);
-    if (keep) kl[upos] = (int)kk[tid];
-    if (tid < ns) key[tid] = ks[tid];
-    if (tid == 0) {
-      s_n[0] = ns;
-      s_n[1] = nu;
-    }
-  } else {  // many changes this tick: the same in passes, sorts in global memory when large
-    for (int j = tid; j < nsp; j += T) spawn_pellet_at(d, a, j, nullptr, nullptr);
-    __syncthreads();
-    int ns = 0;
-    for (int j0 = 0; j0 < nst; j0 += T) {
-      const int j = j0 + tid;
-      bool live = false;
-      int64_t k = 0;
-      if (j < nst) {
-        const size_t g = (size_t)a * d.Pcap + j;
-        const int bx = center_bucket_coord(d.pn[g].x, d.cols), by = center_bucket_coord(d.pn[g].y, d.cols);
-        live = !(j < nconv && d.pel_dead[(size_t)a * d.Pcap + n0 + j]) && tile_holds_bucket(d, bx, by);
-        k = ((int64_t)(by * d.cols + bx) << 32) | j;
-      }
-      int chunk;
-      const int pos = ns + block_rank(live, sh, &chunk);
-      if (live) key[pos] = k;
-      ns += chunk;
-    }
-    __syncthreads();
-    if (pow2_at_least(ns) <= PU_LDS) {
-      for (int i = tid; i < ns; i += T) lds[i] = key[i];
-      block_bitonic_i64(lds, ns);
-      for (int i = tid; i < ns; i += T) key[i] = lds[i];
-    } else {
-      block_bitonic_i64(key, ns);
-    }
-    __syncthreads();
-    int64_t *kb = pow2_at_least(nk_raw) <= PU_LDS ? lds : d.pu_tmp + (size_t)a * 2 * d.Pcap;
-    for (int i = tid; i < nk_raw; i += T) kb[i] = kl[i];
-    block_bitonic_i64(kb, nk_raw);
-    int nu = 0;
-    for (int i0 = 0; i0 < nk_raw; i0 += T) {
-      const int i = i0 + tid;
-      const bool keep = i < nk_raw && (i == 0 || kb[i] != kb[i - 1]);
-      int chunk;
-      const int pos = nu + block_rank(keep, sh, &chunk);
-      if (keep) kl[pos] = (int)kb[i];
-      nu += chunk;
-    }
-    if (tid == 0) {
-      s_n[0] = ns;
-      s_n[1] = nu;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const int ns = s_n[0], nu = s_n[1], nn = n0 - nu + ns;
-    c.n_stg = ns;
-    c.n_kill = nu;
-    c.pu_src = c.peat;
-    c.pu_n0 = n0;
+  const int nconv = c.n_pnew, nsp = c.n_spawn_p;
+  const bool spec = nsp <= kSpawnAhead;
+  if (!spec)  // into the staging list after the conversions (pn[nconv + j])
+    for (int j = threadIdx.x; j < nsp; j += blockDim.x) spawn_pellet_at(d, a, j, nullptr, nullptr);
+  __syncthreads();  // (spawn_pellet_at reads n_pnew)
+  if (threadIdx.x == 0) {
     c.pu_nconv = nconv;
-    c.pu_small = 0;
-    if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
-    c.n_pel = min(nn, d.Pcap);
-    d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
+    c.pu_nsp = nsp;
+    c.pu_spec = spec ? 1 : 0;
     c.n_pnew = 0;
-    c.n_pel_eaten = 0;
-    c.pcur = c.peat ^ 1;
-    c.peat = c.pcur;  // the next eat phase reads the buffer built by the update
+    c.n_pel_eaten = 0;  // (n_pel: the rewritten rows add their change)
   }
-  __syncthreads();
 }
-
 // pp (tick only): playerPlayerOverlap's serial pass first, by wave 0 of the
 // arena's block (its pending bitmap in the dynamic LDS)
 // close (tick only): then the closing pellet update's step 1 (pellet_close_prep)
@@ -3595,7 +3231,6 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   FLOOR(7);
   __shared__ int sflag[1024];
   __shared__ int gcnt[SG_CAP + 1];
-  __shared__ int64_t s_sort[PU_LDS];
   PT_BEGIN(5);
   int a = blockIdx.x;
   if (pp) {
@@ -3708,7 +3343,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   PT_MARK(5, 4);
   if (close) {
     __syncthreads();
-    pellet_close_prep(d, a, s_sort, sflag);
+    pellet_close_prep(d, a);
   }
   PT_MARK(5, 5);
 }
@@ -3792,7 +3427,7 @@ __device__ void spawn_pellet_at(const Dev &d, int a, int j, double *px, double *
     *py = y;
   }
 }
-__device__ __forceinline__ void spawn_pellet(const Dev &d, int gi, bool rank_staged) {
+__device__ __forceinline__ void spawn_pellet(const Dev &d, int gi) {
   if (gi >= d.A * d.Pcap) return;
   int a = gi / d.Pcap, j = gi - a * d.Pcap;
   ArenaCtl &c = d.ctl[a];
@@ -3805,9 +3440,8 @@ __device__ __forceinline__ void spawn_pellet(const Dev &d, int gi, bool rank_sta
   size_t o = (size_t)a * d.Pcap + c.n_pnew + j;
   d.pn[o] = PelRec{(double)x, (double)y, m, c.seq_base_spawn + j};
   d.pn_col[o] = -1;  // Cell(..., None): a colour of its own
-  if (rank_staged) pgrid_rank_staged(d, a, c.n_pnew + j);  // rebuild ranks taken at spawn time
 }
-__global__ void k_spawn_pellets(Dev d) { spawn_pellet(d, GTID, false); }
+__global__ void k_spawn_pellets(Dev d) { spawn_pellet(d, GTID); }
 __device__ __forceinline__ void spawn_virus(const Dev &d, int gi) {
   if (gi >= d.A * d.Vcap) return;
   int a = gi / d.Vcap, j = gi - a * d.Vcap;
@@ -3884,192 +3518,180 @@ __device__ __forceinline__ void respawn_fov_thread(const Dev &d, int gp) {
   fov_cache_thread(d, gp);
 }
 
-// step 2 of the closing pellet update (see pellet_close_prep): blocks
-// [arena][pellet blocks | bucket blocks] + extra blocks for the rest of
-// spawnStuff, which reads nothing this launch writes: the player respawns with
-// the FOV cache (respawn_fov_thread), then the virus spawns.  A
-// pellet thread moves one buffer record (or drops an eaten one and clears its
-// flag); a bucket thread rewrites its bucket's start and count and moves its
-// staged records behind the survivors.  Every thread issues its own loads
-// before the block fetches K and S into LDS (short lists; long ones are
-// searched in global memory), so the launch is one round of loads.  No
-// epilogue: k_spawn_plan already closed the counts; block 0 advances the tick.
-// A usual tick (pu_small): wave 0 of every block builds K and S itself from the
-// raw kill list, the blob conversions and this tick's spawns (drawn ahead by
-// k_tick_begin) -- a few dozen keys ranked in registers, the same in every
-// block -- and block 0 closes the bookkeeping.
-// the short lists of a usual tick, by one wavefront: the staged keys (bucket <<
-// 32 | staging index) of the records that join, sorted, to S; the killed
-// indices sorted and unique to K; their counts to n[0], n[1]
-__device__ __forceinline__ void pellet_lists_wave(const Dev &d, const ArenaCtl &c, int a, int n0, int nconv, int nsp,
-                                                  int nk_raw, int *K, int64_t *S, int *n) {
-  const int tid = threadIdx.x;
-  const int nst = nconv + nsp;
-  const int *kl = d.kill_list + (size_t)a * d.Pcap;
-  const int kv = tid < nk_raw ? kl[tid] : INT_MAX;
-  bool live = false;
-  int bk = 0;
-  if (tid < nst) {
+// Step 2 of the closing pellet update (see pellet_close_prep): one block per
+// bucket row of every arena, + extra blocks for the rest of spawnStuff, which
+// reads nothing this launch writes: the player respawns with the FOV cache
+// (respawn_fov_thread), then the virus spawns.  A row block finds whether a
+// killed slot (kill_list) lies in its row or a joining staged record (a blob
+// conversion nobody ate, a spawn; tiles: in the held range) has its centre in
+// it; if so it writes the row anew into its other home -- survivors by bucket
+// in their old order, each bucket's new records behind them (consumers rank
+// candidates by creation sequence, so order inside a bucket carries no meaning)
+// -- and the row's bucket starts.  Rows nothing touched are left alone: a
+// usual tick rewrites a few dozen of the 240 rows instead of the whole store.
+constexpr int PU_ROW_STG = 512;  // joining records per row and tick (more: ERR_PELLET_CAP)
+constexpr int kPelRowCols = 1024;  // buckets per row the update handles (aigar_create checks)
+__device__ __forceinline__ int block_excl1(int v, int *wsum, int &total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int before = 0;
+  total = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  __syncthreads();
+  return before + inc - v;
+}
+__device__ void pel_row_update(const Dev &d, int a, int r) {
+  __shared__ int s_flag[2];
+  __shared__ int s_sj[PU_ROW_STG];
+  __shared__ short s_sbx[PU_ROW_STG];
+  __shared__ int s_ost[kPelRowCols + 1];  // the row's old bucket starts (absolute slots)
+  __shared__ int s_live[kPelRowCols], s_stc[kPelRowCols];  // per bucket: survivors, joining records
+  __shared__ int s_lpre[kPelRowCols], s_nofs[kPelRowCols];  // survivors before the bucket; its new start - row base
+  __shared__ int wsum[4];
+  const int tid = threadIdx.x, C = d.cols;
+  ArenaCtl &c = d.ctl[a];
+  const int nconv = c.pu_nconv, nst = nconv + c.pu_nsp, spec = c.pu_spec;
+  const int nk = min(c.n_kill, d.Pcap);
+  int *e0 = d.pstart + (size_t)a * d.PH1 + (size_t)r * (C + 1);
+  const size_t S0 = (size_t)a * d.PS, D0 = (size_t)a * d.PD, Q0 = (size_t)a * d.Pcap;
+  if (tid == 0) s_flag[0] = s_flag[1] = 0;
+  for (int bx = tid; bx <= C; bx += blockDim.x) s_ost[bx] = e0[bx];
+  __syncthreads();
+  const int lo = s_ost[0], hi = s_ost[C];
+  const int *kl = d.kill_list + Q0;
+  for (int t = tid; t < nk; t += blockDim.x) {
+    const int k = kl[t];
+    if (k >= lo && k < hi) s_flag[0] = 1;
+  }
+  for (int j = tid; j < nst; j += blockDim.x) {
     double x, y;
-    if (tid < nconv) {
-      const size_t g = (size_t)a * d.Pcap + tid;
-      x = d.pn[g].x;
-      y = d.pn[g].y;
-      live = !d.pel_dead[(size_t)a * d.Pcap + n0 + tid];
-    } else {  // (nsp <= kSpawnAhead)
-      const size_t o = (size_t)a * kSpawnAhead + tid - nconv;
+    bool live = true;
+    if (j < nconv) {
+      x = d.pn[Q0 + j].x;
+      y = d.pn[Q0 + j].y;
+      live = !d.pel_dead[D0 + d.PS + j];  // (a conversion eaten this tick does not join)
+    } else if (spec) {
+      const size_t o = (size_t)a * kSpawnAhead + (j - nconv);
       x = d.spec_x[o];
       y = d.spec_y[o];
-      live = true;
+    } else {
+      x = d.pn[Q0 + j].x;
+      y = d.pn[Q0 + j].y;
     }
-    const int bx = center_bucket_coord(x, d.cols), by = center_bucket_coord(y, d.cols);
-    live = live && tile_holds_bucket(d, bx, by);
-    bk = by * d.cols + bx;
-  }
-  // ranks by counting over the few live lanes (wave-uniform loops of lane reads:
-  // far shorter than a 64-wide sorting network of cross-lane permutes)
-  const unsigned long long lm = __ballot(live);
-  int rs = 0;
-  for (unsigned long long w = lm; w; w &= w - 1) {  // key order (bucket, staging index)
-    const int j = __ffsll((long long)w) - 1;
-    const int bj = __builtin_amdgcn_readlane(bk, j);
-    rs += bj < bk || (bj == bk && j < tid);
-  }
-  if (live) S[rs] = ((int64_t)bk << 32) | tid;
-  bool first = tid < nk_raw;
-  for (int j = 0; j < nk_raw; j++) first = first && !(j < tid && __builtin_amdgcn_readlane(kv, j) == kv);
-  const unsigned long long fm = __ballot(first);
-  int rk = 0;
-  for (unsigned long long w = fm; w; w &= w - 1) rk += __builtin_amdgcn_readlane(kv, __ffsll((long long)w) - 1) < kv;
-  if (first) K[rk] = kv;
-  if (tid == 0) {
-    n[0] = __popcll(lm);
-    n[1] = __popcll(fm);
-  }
-}
-__device__ __forceinline__ int count_below_i32(const int *v, int n, int x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int m = (lo + hi) >> 1;
-    if (v[m] < x) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
-}
-__device__ __forceinline__ int count_below_i64(const int64_t *v, int n, int64_t x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int m = (lo + hi) >> 1;
-    if (v[m] < x) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
-}
-// A busy tick's unsorted lists (pu_small == 2): a block's 256 queries are
-// monotone (pellet indices; buffer starts; buckets -- the buffer is sorted by
-// bucket), so each list entry is either below the block's query range (counted
-// once, block-wide) or inside it (a short LDS list every thread scans).
-__device__ __forceinline__ int block_sum(int v, int *red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  int s = 0;
-  for (int w = 0; w < (int)(blockDim.x >> 6); w++) s += red[w];
-  return s;
-}
-__device__ __forceinline__ void pel_update_blocked(const Dev &d, int a, bool pel, int i, int n0, int nk, int ns,
-                                                   int src, int dst, bool dead, double x, double y, double m,
-                                                   int64_t sq, int col, int s0, int c0, int *lk, int64_t *ls,
-                                                   bool tick_block) {
-  __shared__ int s_lo[4], s_red[4], s_n[2];
-  const int tid = threadIdx.x;
-  const size_t P0 = (size_t)a * d.Pcap;
-  const int *kl = d.kill_list + P0;
-  const int64_t *sk = d.stg_key + 2 * P0;
-  const int i0 = i - tid;  // the block's first query
-  // the block's query range: pellets [i0, i0 + 256) of buckets [b_lo, b_hi];
-  // buckets [i0, i0 + 256) with buffer starts [s_lo, s_hi)
-  const int b = pel && i < n0 ? center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols) : 0;
-  const int last = pel ? min(i0 + 255, n0 - 1) : min(i0 + 255, d.H - 1);
-  if (tid == 0) {
-    s_lo[0] = pel ? b : s0;
-    s_n[0] = s_n[1] = 0;
-    if (last < i0) s_lo[1] = s_lo[0];  // (a pellet block past the buffer: no queries)
-  }
-  if (i == last) s_lo[1] = pel ? b : s0 + c0;
-  __syncthreads();
-  const int klo = pel ? i0 : s_lo[0], khi = pel ? i0 + 256 : s_lo[1];         // kills: [klo, khi)
-  const int blo = pel ? s_lo[0] : i0, bhi = pel ? s_lo[1] + 1 : i0 + 256;  // staged buckets: [blo, bhi)
-  int below_k = 0, below_s = 0;
-  for (int t = tid; t < nk; t += 256) {
-    const int v = kl[t];
-    below_k += v < klo;
-    if (v >= klo && v < khi) lk[atomicAdd(&s_n[0], 1)] = v;
-  }
-  for (int t = tid; t < ns; t += 256) {
-    const int64_t k = sk[t];
-    const int bk = (int)(k >> 32);
-    below_s += bk < blo;
-    if (bk >= blo && bk < bhi) ls[atomicAdd(&s_n[1], 1)] = k;
-  }
-  below_k = block_sum(below_k, s_red);  // (its barrier also publishes the short lists)
-  __syncthreads();
-  below_s = block_sum(below_s, s_red);
-  const int nlk = s_n[0], nls = s_n[1];
-  ArenaCtl &c = d.ctl[a];
-  if (tick_block && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
-  if (pel) {
-    if (i < n0) {
-      const size_t g = P0 + i;
-      if (dead) {
-        d.pel_dead[g] = 0;
-      } else {
-        int kb = below_k, sb = below_s;
-        for (int t = 0; t < nlk; t++) kb += lk[t] < i;
-        for (int t = 0; t < nls; t++) sb += (int)(ls[t] >> 32) < b;
-        const int pos = i - kb + sb;
-        if (pos < d.Pcap) {
-          const size_t o = P0 + pos;
-          pel_store(&d.pel[dst][o], PelRec{x, y, m, sq});
-          d.pel_col[dst][o] = col;
+    const int by = center_bucket_coord(y, C);
+    if (live && by == r) {
+      const int bx = center_bucket_coord(x, C);
+      if (tile_holds_bucket(d, bx, by)) {
+        const int k = atomicAdd(&s_flag[1], 1);
+        if (k < PU_ROW_STG) {
+          s_sj[k] = j;
+          s_sbx[k] = (short)bx;
         }
       }
     }
-    return;
   }
-  if (i >= d.H) return;
-  int k0 = below_k, k1 = below_k, j0 = below_s, nb = 0;
-  for (int t = 0; t < nlk; t++) {
-    k0 += lk[t] < s0;
-    k1 += lk[t] < s0 + c0;
+  __syncthreads();
+  const int ns_all = s_flag[1];
+  if (!s_flag[0] && ns_all == 0) return;  // (uniform) untouched row
+  const int ns = min(ns_all, PU_ROW_STG);
+  const int home = C * d.PR, nb = lo >= home ? lo - home : lo + home;  // the other home of the row
+  for (int bx = tid; bx < C; bx += blockDim.x) s_live[bx] = s_stc[bx] = 0;
+  __syncthreads();
+  auto bucket_of = [&](int i) {  // old bucket of slot i: s_ost[bx] <= i < s_ost[bx + 1]
+    int l = 0, h = C;  // invariant: s_ost[l] <= i < s_ost[h]
+    while (h - l > 1) {
+      const int m = (l + h) >> 1;
+      if (s_ost[m] <= i) l = m;
+      else h = m;
+    }
+    return l;
+  };
+  for (int i = lo + tid; i < hi; i += blockDim.x)
+    if (!d.pel_dead[D0 + i]) atomicAdd(&s_live[bucket_of(i)], 1);
+  for (int k = tid; k < ns; k += blockDim.x) atomicAdd(&s_stc[s_sbx[k]], 1);
+  __syncthreads();
+  int total;
+  {
+    int v[4], w[4];
+    for (int k = 0; k < 4; k++) {
+      const int bx = tid * 4 + k;
+      v[k] = bx < C ? s_live[bx] + s_stc[bx] : 0;
+      w[k] = bx < C ? s_live[bx] : 0;
+    }
+    total = block_scan4(v, wsum);
+    (void)block_scan4(w, wsum);
+    for (int k = 0; k < 4; k++) {
+      const int bx = tid * 4 + k;
+      if (bx < C) {
+        s_nofs[bx] = v[k];
+        s_lpre[bx] = w[k];
+      }
+    }
   }
-  for (int t = 0; t < nls; t++) {
-    const int bt = (int)(ls[t] >> 32);
-    j0 += bt < i;
-    nb += bt == i;
+  if (total > d.PR && tid == 0) set_err(d, a, ERR_PELLET_CAP);
+  __syncthreads();
+  const int lim = nb + d.PR;
+  // survivors: slot i of bucket bx -> nb + new start + (survivors of bx before i)
+  int carry = 0;
+  for (int c0 = lo; c0 < hi; c0 += blockDim.x) {
+    const int i = c0 + tid;
+    bool live = false;
+    if (i < hi) live = !d.pel_dead[D0 + i];
+    int tot;
+    const int ex = carry + block_excl1(live ? 1 : 0, wsum, tot);
+    carry += tot;
+    if (i < hi) {
+      if (live) {
+        const int bx = bucket_of(i);
+        const int pos = nb + s_nofs[bx] + (ex - s_lpre[bx]);
+        if (pos < lim) {
+          d.pel[S0 + pos] = d.pel[S0 + i];
+          d.pel_col[S0 + pos] = d.pel_col[S0 + i];
+        }
+      } else {
+        d.pel_dead[D0 + i] = 0;  // eaten: dropped, and its flag clean for the next time this home is used
+      }
+    }
   }
-  const int start = s0 - k0 + j0, surv = c0 - (k1 - k0);
-  // this bucket's staged records in staging order (the short list is unordered)
-  for (int t = 0; t < nls; t++) {
-    if ((int)(ls[t] >> 32) != i) continue;
-    int r = 0;
-    for (int u = 0; u < nls; u++) r += (int)(ls[u] >> 32) == i && ls[u] < ls[t];
-    const int pos = start + surv + r;
-    if (pos >= d.Pcap) continue;
-    const size_t o = P0 + pos, gs = P0 + (int)(ls[t] & 0xFFFFFFFFll);
-    pel_store(&d.pel[dst][o], d.pn[gs]);
-    d.pel_col[dst][o] = d.pn_col[gs];
+  // joining records: behind the bucket's survivors, in staging order
+  for (int k = tid; k < ns; k += blockDim.x) {
+    const int j = s_sj[k], bx = s_sbx[k];
+    int rk = 0;
+    for (int q = 0; q < ns; q++) rk += s_sbx[q] == bx && s_sj[q] < j;
+    const int pos = nb + s_nofs[bx] + s_live[bx] + rk;
+    if (pos >= lim) continue;
+    PelRec rec;
+    int col = -1;
+    if (j >= nconv && spec) {  // a spawn drawn ahead by k_tick_begin
+      const size_t o = (size_t)a * kSpawnAhead + (j - nconv);
+      rec = PelRec{d.spec_x[o], d.spec_y[o], d.spec_m[o], c.seq_base_spawn + (j - nconv)};
+    } else {
+      rec = d.pn[Q0 + j];
+      col = d.pn_col[Q0 + j];
+    }
+    d.pel[S0 + pos] = rec;
+    d.pel_col[S0 + pos] = col;
   }
-  d.pstart[(size_t)a * (d.H + 1) + i] = start;
-  d.pbc[(size_t)a * d.H + i] = surv + nb;
+  for (int bx = tid; bx < C; bx += blockDim.x) e0[bx] = nb + min(s_nofs[bx], d.PR);
+  if (tid == 0) {
+    e0[C] = nb + min(total, d.PR);
+    atomicAdd(&c.n_pel, min(total, d.PR) - (hi - lo));
+  }
 }
-__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int nbF) {
+__global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbF) {
   FLOOR(8);
-  __shared__ int s_kill[PU_SH];
-  __shared__ int64_t s_stg[PU_SH];
-  __shared__ int s_n[2];
   PT_BEGIN(8);
-  const int per = nbP + nbB, nup = d.A * per;
+  const int nup = d.A * d.cols;
   if ((int)blockIdx.x >= nup + nbF) {
     spawn_virus(d, (blockIdx.x - nup - nbF) * 256 + threadIdx.x);
     PT_MARK(8, 5);
@@ -4080,103 +3702,9 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbP, int nbB, int
     PT_MARK(8, 4);
     return;
   }
-  const int a = blockIdx.x / per, blk = blockIdx.x - a * per, tid = threadIdx.x;
-  ArenaCtl &c = d.ctl[a];
-  const int mode = c.pu_small, n0 = c.pu_n0, nconv = c.pu_nconv;
-  const bool small = mode == 1, unsorted = mode == 2;  // (else: sorted lists from k_spawn_plan)
-  int nk = c.n_kill, ns = c.n_stg;
-  const int src = c.pu_src, dst = src ^ 1;
-  const size_t P0 = (size_t)a * d.Pcap;
-  // this thread's record (pellet blocks) or bucket (bucket blocks), loaded first
-  const bool pel = blk < nbP;
-  const int i = pel ? blk * 256 + tid : (blk - nbP) * 256 + tid;
-  const size_t g = P0 + i;
-  bool dead = false;
-  double x = 0, y = 0, m = 0;
-  int64_t sq = 0;
-  int col = -1, s0 = 0, c0 = 0;
-  if (pel && i < n0) {
-    dead = d.pel_dead[g];
-    {
-      const PelRec r_ = d.pel[src][g];
-      x = r_.x;
-      y = r_.y;
-      m = r_.m;
-      sq = r_.seq;
-    }
-    col = d.pel_col[src][g];
-  } else if (!pel && i < d.H) {
-    s0 = d.pstart[(size_t)a * (d.H + 1) + i];
-    c0 = d.pbc[(size_t)a * d.H + i];
-  }
-  const int *kl = d.kill_list + P0;
-  const int64_t *sk = d.stg_key + 2 * P0;
-  PT_MARK(8, 1);
-  if (small && tid < 64) pellet_lists_wave(d, c, a, n0, nconv, c.n_spawn_p, min(nk, d.Pcap), s_kill, s_stg, s_n);
-  const bool kin = small || nk <= PU_SH, sin = small || ns <= PU_SH;
-  if (unsorted) return pel_update_blocked(d, a, pel, i, n0, nk, ns, src, dst, dead, x, y, m, sq, col, s0, c0, s_kill,
-                                         s_stg, blk == 0 && pel);
-  if (!small) {
-    if (kin)
-      for (int t = tid; t < nk; t += 256) s_kill[t] = kl[t];
-    if (sin)
-      for (int t = tid; t < ns; t += 256) s_stg[t] = sk[t];
-  }
-  __syncthreads();
-  PT_MARK(8, 2);
-  if (small) {
-    ns = s_n[0];
-    nk = s_n[1];
-    if (blk == 0 && tid == 0) {  // the tick's pellet bookkeeping (nothing in this launch reads it)
-      const int nn = n0 - nk + ns;
-      if (nn > d.Pcap) c.err |= ERR_PELLET_CAP;
-      c.n_pel = min(nn, d.Pcap);
-      d.pstart[(size_t)a * (d.H + 1) + d.H] = c.n_pel;
-      c.n_pnew = 0;
-      c.n_pel_eaten = 0;
-      c.pcur = dst;
-      c.peat = dst;  // the next eat phase reads the buffer built here
-    }
-  }
-  const int *K = kin ? s_kill : kl;
-  const int64_t *S = sin ? s_stg : sk;
-  if (pel) {
-    if (i < n0) {
-      if (dead) {
-        d.pel_dead[g] = 0;  // eaten: dropped (the flags stay clean for the next eat phase)
-      } else {
-        const int b = center_bucket_coord(y, d.cols) * d.cols + center_bucket_coord(x, d.cols);
-        const int pos = i - count_below_i32(K, nk, i) + count_below_i64(S, ns, (int64_t)b << 32);
-        if (pos < d.Pcap) {
-          const size_t o = P0 + pos;
-          pel_store(&d.pel[dst][o], PelRec{x, y, m, sq});
-          d.pel_col[dst][o] = col;
-        }
-      }
-    }
-    if (blk == 0 && tid == 0) c.tick += 1;  // (nothing in this launch reads it)
-  } else if (i < d.H) {
-    const int k0 = count_below_i32(K, nk, s0), k1 = count_below_i32(K, nk, s0 + c0);
-    const int j0 = count_below_i64(S, ns, (int64_t)i << 32), j1 = count_below_i64(S, ns, (int64_t)(i + 1) << 32);
-    const int start = s0 - k0 + j0, surv = c0 - (k1 - k0);
-    for (int r = j0; r < j1; r++) {
-      const int js = (int)(S[r] & 0xFFFFFFFFll);
-      const int pos = start + surv + (r - j0);
-      if (pos >= d.Pcap) continue;
-      const size_t o = P0 + pos;
-      if (small && js >= nconv) {  // a spawn, drawn by k_tick_begin (k_spawn_plan did not stage it)
-        const size_t so = (size_t)a * kSpawnAhead + js - nconv;
-        pel_store(&d.pel[dst][o], PelRec{d.spec_x[so], d.spec_y[so], d.spec_m[so], c.seq_base_spawn + (js - nconv)});
-        d.pel_col[dst][o] = -1;
-        continue;
-      }
-      const size_t gs = P0 + js;
-      pel_store(&d.pel[dst][o], d.pn[gs]);
-      d.pel_col[dst][o] = d.pn_col[gs];
-    }
-    d.pstart[(size_t)a * (d.H + 1) + i] = start;
-    d.pbc[(size_t)a * d.H + i] = surv + (j1 - j0);
-  }
+  const int a = blockIdx.x / d.cols, r = blockIdx.x - a * d.cols;
+  if (r == 0 && threadIdx.x == 0) d.ctl[a].tick += 1;  // (nothing in this launch reads it)
+  pel_row_update(d, a, r);
   PT_MARK(8, 3);
 }
 
@@ -4196,8 +3724,8 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.n_dead = 0;
   c.n_ev = 0;
   c.n_pend = c.n_pend2 = 0;
-  c.n_kill = c.n_stg = 0;
-  c.pu_n0 = c.pu_nconv = c.pu_small = 0;
+  c.n_kill = 0;
+  c.pu_nconv = c.pu_nsp = c.pu_spec = 0;
   c.err = c.warn = 0;
   c.rmax_cell = radius_of(kStartMass);
   c.rmax_virus = radius_of(kVirusBase);
@@ -4205,7 +3733,6 @@ __global__ void k_init_ctl(Dev d, uint64_t seed) {
   c.scan_epoch[0] = c.scan_epoch[1] = 0;
   c.pl_epoch = 0;
   c.dirty = 0;
-  c.pcur = c.peat = 0;
   c.pl_ticket = 0;
   c.scan_ticket[0] = c.scan_ticket[1] = 0;
   c.n_pel_glob = c.n_eaten_glob = c.n_out = c.n_out_pel = c.n_undone = c.n_undone_glob = 0;
@@ -4221,14 +3748,12 @@ struct Scratch {
   int *v;
 };
 
-// counts -> scan (+ epilogue) -> scatter
-void launch_pellet_rebuild(const Dev &d, hipStream_t s, int mode) {
-  long nc = (long)d.A * (d.H + d.Pcap), ns = (long)d.A * 2 * d.Pcap;
-  if (mode != PR_CLOSE) hipLaunchKernelGGL(k_pgrid_count, dim3(nblk(nc, 256)), dim3(256), 0, s, d, mode);
-  hipLaunchKernelGGL(k_scan_lb, dim3(d.scan_tiles, d.A), dim3(256), 0, s, d, d.pcnt, d.pstart, d.pncnt, mode,
-                     mode == PR_CLOSE ? 1 : 0, 0);
-  const int fovb = mode == PR_CLOSE ? nblk(d.NP, 256) : 0;  // closing rebuild: + the FOV cache
-  hipLaunchKernelGGL(k_pgrid_scatter, dim3(nblk(ns, 256) + fovb), dim3(256), 0, s, d, mode, fovb);
+// Field.initialize's pellets: the staging list -> home 0 of every row (counting sort)
+void launch_pellet_rows(const Dev &d, hipStream_t s) {
+  const long n = (long)d.A * d.Pcap;
+  hipLaunchKernelGGL(k_prow_count, dim3(nblk(n, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_prow_scan, dim3(d.cols, d.A), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_prow_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, d);
 }
 
 
@@ -4283,9 +3808,9 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   // current buffer) + the rest of spawnStuff as extra blocks: player respawns
   // with the FOV cache, virus spawns (fused into the pellet threads the FOV
   // cache stretched the kernel; as separate blocks they only add to the grid)
-  const int nbP = nblk(d.Pcap, 256), nbB = nblk(d.H, 256), nbF = nblk(d.NP, 256);
+  const int nbF = nblk(d.NP, 256);
   const int nbV = d.virus_enabled ? nblk((long)d.A * d.Vcap, 256) : 0;
-  hipLaunchKernelGGL(k_pel_update, dim3(d.A * (nbP + nbB) + nbF + nbV), dim3(256), 0, s, d, nbP, nbB, nbF);
+  hipLaunchKernelGGL(k_pel_update, dim3(d.A * d.cols + nbF + nbV), dim3(256), 0, s, d, nbF);
 }
 void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
   launch_tick_pre(d, s, scr_k, scr_v, rp);
@@ -4390,10 +3915,10 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int fir
       const int bx = center_bucket_coord(r.x, d.cols), by = center_bucket_coord(r.y, d.cols);
       if (!tile_holds_bucket(d, bx, by)) continue;
       const Food F(d, 0);
-      const int b = by * d.cols + bx, lo = min(d.pstart[b], F.n0), hi = min(d.pstart[b + 1], F.n0);
+      const int e = by * (d.cols + 1) + bx, lo = d.pstart[e], hi = d.pstart[e + 1];
       bool found = false;
       for (int t = lo; t < hi && !found; t++)
-        if (d.pel[F.pb][F.g(t)].seq == r.seq) {
+        if (d.pel[F.gp(t)].seq == r.seq) {
           uint8_t *pd = d.pel_dead + F.g(t);  // (flag set through its 32-bit word: the first setter notes the kill)
           unsigned *w = (unsigned *)((uintptr_t)pd & ~(uintptr_t)3);
           const unsigned sh = (unsigned)((uintptr_t)pd & 3) * 8;
@@ -4466,7 +3991,8 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   (void)hipMemsetAsync(d.b_flags, 0, sizeof(uint32_t) * (size_t)d.A * d.Ecap, s);
   (void)hipMemsetAsync(d.p_split, 0, sizeof(int) * d.NP, s);
   (void)hipMemsetAsync(d.p_eject, 0, sizeof(int) * d.NP, s);
-  (void)hipMemsetAsync(d.pel_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Pcap, s);
+  (void)hipMemsetAsync(d.pel_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.PD, s);
+  (void)hipMemsetAsync(d.pel_dead, 0, (size_t)d.A * d.PD, s);
   (void)hipMemsetAsync(d.b_owner, 0, sizeof(uint64_t) * (size_t)d.A * d.Ecap, s);
   (void)hipMemsetAsync(d.scan_state, 0, sizeof(unsigned long long) * 2 * (size_t)d.A * d.scan_tiles, s);
   (void)hipMemsetAsync(d.pl_state, 0, sizeof(unsigned long long) * (size_t)d.A * d.pl_tiles, s);
@@ -4477,7 +4003,7 @@ void launch_reset(const Dev &d, hipStream_t s, uint64_t seed) {
   hipLaunchKernelGGL(k_spawn_pellets, dim3(nblk((long)d.A * d.Pcap, 256)), dim3(256), 0, s, d);
   if (d.virus_enabled) hipLaunchKernelGGL(k_spawn_viruses, dim3(nblk((long)d.A * d.Vcap, 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_pnew_commit, dim3(nblk(d.A, 64)), dim3(64), 0, s, d);
-  launch_pellet_rebuild(d, s, PR_RESET);  // staging -> buffer 0
+  launch_pellet_rows(d, s);  // staging -> the row store
   launch_player_fov(d, s);
 }
 

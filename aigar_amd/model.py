@@ -353,6 +353,9 @@ class Field:
     def reset(self):  # field.py:69-83
         self._resets += 1
         self.stepper.reset(self.seed + 7919 * self._resets)
+        # the reference's players survive Field.reset with their commandPoint and
+        # split / eject flags (initializePlayer only gives them new cells)
+        self.stepper.set_commands(self._cmd)
         self._cache = {}
 
     def update(self):  # field.py:85-92

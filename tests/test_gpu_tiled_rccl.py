@@ -69,10 +69,11 @@ def test_tile_run_over_rccl_matches_oracle(extra):
         o.set_commands(_policy_commands(stp))
         o.step(1)
         assert np.array_equal(tiles.merge_events([stp.events_raw()]), o.events()), "tick %d: events differ" % t
+        want = o.observe()  # (every tick: the last-frame channels carry the previous observation)
         if t % 10 == 9 or t == 34:
             dif = parity.diff_states(stp.get_state(), o.get_state())
             assert not dif, "tick %d: %s" % (t, dif[:3])
-            assert parity.obs_close(obs.cpu().numpy(), o.observe()), "tick %d: observations differ" % t
+            assert parity.obs_close(obs.cpu().numpy(), want), "tick %d: observations differ" % t
     ms, n = stp.kernel_time("exchange")
     assert n == 5 * (1 + extra), (ms, n)
     stp.profile(False)
