@@ -114,10 +114,11 @@ def test_torch_transport_nccl_world_size_one():
             tiles.tiled_tick([stp], tr, obs=[obs], extra_passes=0)
             o.step(1)
             assert np.array_equal(tiles.merge_events([stp.events_raw()]), o.events()), "tick %d" % t
+            want = o.observe()  # (every tick, as the device: the last-frame channels carry the previous one)
         torch.cuda.synchronize()
         dif = parity.diff_states(stp.get_state(), o.get_state())
         assert not dif, dif
-        assert parity.obs_close(obs.cpu().numpy(), o.observe())
+        assert parity.obs_close(obs.cpu().numpy(), want)
         assert tr.avg_exchange_ms() is not None
         stp.close()
         o.close()

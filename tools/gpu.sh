@@ -30,7 +30,7 @@ for S in "$@"; do
     suite*)
       T=tests; [ "$S" != suite ] && T=$(echo ${S#suite:} | tr , ' ')
       timeout -k 10 900 python -u -m pytest $T -m gpu -x -v --timeout 300 --timeout-method thread \
-        > $O/${TAG}_pytest_gpu.log 2>&1 || { grep -E "FAILED|ERROR|^E  " $O/${TAG}_pytest_gpu.log | head -20; fail suite $?; }
+        > $O/${TAG}_pytest_gpu.log 2>&1 || { rc=$?; grep -E "FAILED|ERROR|^E  " $O/${TAG}_pytest_gpu.log | head -20; fail suite $rc; }
       tail -1 $O/${TAG}_pytest_gpu.log ;;
     bench)
       timeout -k 10 400 python -u bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || fail bench $? $O/${TAG}_bench.err
