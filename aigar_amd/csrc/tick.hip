@@ -3550,10 +3550,18 @@ __device__ __forceinline__ int block_excl1(int v, int *wsum, int &total) {
   __syncthreads();
   return before + inc - v;
 }
+constexpr int PU_JREC = 64;  // joining records per row kept whole in LDS (beyond: loaded again)
+constexpr int PU_LDS = 512;  // row slots whose records the update parks in LDS (longer rows: two rounds)
+constexpr int PU_K = PU_LDS / 256;  // consecutive slots per thread
 __device__ void pel_row_update(const Dev &d, int a, int r) {
   __shared__ int s_flag[2];
   __shared__ int s_sj[PU_ROW_STG];
   __shared__ short s_sbx[PU_ROW_STG];
+  __shared__ PelRec s_jrec[PU_JREC];
+  __shared__ int s_jcol[PU_JREC];
+  __shared__ PelRec s_rec[PU_LDS];
+  __shared__ int s_rcol[PU_LDS];
+  __shared__ uint8_t s_rdead[PU_LDS];
   __shared__ int s_ost[kPelRowCols + 1];  // the row's old bucket starts (absolute slots)
   __shared__ int s_live[kPelRowCols], s_stc[kPelRowCols];  // per bucket: survivors, joining records
   __shared__ int s_lpre[kPelRowCols], s_nofs[kPelRowCols];  // survivors before the bucket; its new start - row base
@@ -3564,6 +3572,8 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
   const int nk = min(c.n_kill, d.Pcap);
   int *e0 = d.pstart + (size_t)a * d.PH1 + (size_t)r * (C + 1);
   const size_t S0 = (size_t)a * d.PS, D0 = (size_t)a * d.PD, Q0 = (size_t)a * d.Pcap;
+  // round 1: the row's bucket starts, the tick's kills, every staged record (whole:
+  // the joins' records are then in LDS when the row is written)
   if (tid == 0) s_flag[0] = s_flag[1] = 0;
   for (int bx = tid; bx <= C; bx += blockDim.x) s_ost[bx] = e0[bx];
   __syncthreads();
@@ -3574,28 +3584,32 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
     if (k >= lo && k < hi) s_flag[0] = 1;
   }
   for (int j = tid; j < nst; j += blockDim.x) {
-    double x, y;
+    PelRec rec;
+    int col = -1;
     bool live = true;
     if (j < nconv) {
-      x = d.pn[Q0 + j].x;
-      y = d.pn[Q0 + j].y;
+      rec = d.pn[Q0 + j];
+      col = d.pn_col[Q0 + j];
       live = !d.pel_dead[D0 + d.PS + j];  // (a conversion eaten this tick does not join)
-    } else if (spec) {
+    } else if (spec) {  // a spawn drawn ahead by k_tick_begin
       const size_t o = (size_t)a * kSpawnAhead + (j - nconv);
-      x = d.spec_x[o];
-      y = d.spec_y[o];
+      rec = PelRec{d.spec_x[o], d.spec_y[o], d.spec_m[o], c.seq_base_spawn + (j - nconv)};
     } else {
-      x = d.pn[Q0 + j].x;
-      y = d.pn[Q0 + j].y;
+      rec = d.pn[Q0 + j];
+      col = d.pn_col[Q0 + j];
     }
-    const int by = center_bucket_coord(y, C);
+    const int by = center_bucket_coord(rec.y, C);
     if (live && by == r) {
-      const int bx = center_bucket_coord(x, C);
+      const int bx = center_bucket_coord(rec.x, C);
       if (tile_holds_bucket(d, bx, by)) {
         const int k = atomicAdd(&s_flag[1], 1);
         if (k < PU_ROW_STG) {
           s_sj[k] = j;
           s_sbx[k] = (short)bx;
+          if (k < PU_JREC) {
+            s_jrec[k] = rec;
+            s_jcol[k] = col;
+          }
         }
       }
     }
@@ -3616,19 +3630,17 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
     }
     return l;
   };
-  for (int i = lo + tid; i < hi; i += blockDim.x)
-    if (!d.pel_dead[D0 + i]) atomicAdd(&s_live[bucket_of(i)], 1);
-  for (int k = tid; k < ns; k += blockDim.x) atomicAdd(&s_stc[s_sbx[k]], 1);
-  __syncthreads();
-  int total;
-  {
+  const int lim = nb + d.PR;
+  // the row's bucket starts from per-bucket survivor + join counts (s_live / s_stc
+  // complete: the caller's scan begins with a barrier)
+  auto bucket_scans = [&]() {
     int v[4], w[4];
     for (int k = 0; k < 4; k++) {
       const int bx = tid * 4 + k;
       v[k] = bx < C ? s_live[bx] + s_stc[bx] : 0;
       w[k] = bx < C ? s_live[bx] : 0;
     }
-    total = block_scan4(v, wsum);
+    const int total = block_scan4(v, wsum);
     (void)block_scan4(w, wsum);
     for (int k = 0; k < 4; k++) {
       const int bx = tid * 4 + k;
@@ -3637,29 +3649,78 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
         s_lpre[bx] = w[k];
       }
     }
-  }
-  if (total > d.PR && tid == 0) set_err(d, a, ERR_PELLET_CAP);
-  __syncthreads();
-  const int lim = nb + d.PR;
-  // survivors: slot i of bucket bx -> nb + new start + (survivors of bx before i)
-  int carry = 0;
-  for (int c0 = lo; c0 < hi; c0 += blockDim.x) {
-    const int i = c0 + tid;
-    bool live = false;
-    if (i < hi) live = !d.pel_dead[D0 + i];
-    int tot;
-    const int ex = carry + block_excl1(live ? 1 : 0, wsum, tot);
-    carry += tot;
-    if (i < hi) {
-      if (live) {
-        const int bx = bucket_of(i);
-        const int pos = nb + s_nofs[bx] + (ex - s_lpre[bx]);
-        if (pos < lim) {
-          d.pel[S0 + pos] = d.pel[S0 + i];
-          d.pel_col[S0 + pos] = d.pel_col[S0 + i];
-        }
+    if (total > d.PR && tid == 0) set_err(d, a, ERR_PELLET_CAP);
+    __syncthreads();
+    return total;
+  };
+  for (int k = tid; k < ns; k += blockDim.x) atomicAdd(&s_stc[s_sbx[k]], 1);
+  int total;
+  if (hi - lo <= PU_LDS) {
+    // round 2 (rows of <= PU_LDS slots; C3's hold ~420): every slot's liveness,
+    // record and colour in ONE round of loads, the records parked in LDS until
+    // their new positions are known (registers: the launch spilled)
+    for (int i = lo + tid; i < hi; i += blockDim.x) {
+      const bool dead = d.pel_dead[D0 + i];
+      s_rec[i - lo] = d.pel[S0 + i];
+      s_rcol[i - lo] = d.pel_col[S0 + i];
+      s_rdead[i - lo] = dead ? 1 : 0;
+    }
+    __syncthreads();
+    // each thread's PU_K consecutive slots: bucket, survivor count
+    const int i0 = lo + PU_K * tid;
+    uint32_t livem = 0;
+    int b0 = i0 < hi ? bucket_of(i0) : 0, bk[PU_K];
+#pragma unroll
+    for (int k = 0; k < PU_K; k++) {
+      const int i = i0 + k;
+      if (i >= hi) continue;
+      while (s_ost[b0 + 1] <= i) b0++;  // (consecutive slots: the next bucket is near)
+      bk[k] = b0;
+      if (!s_rdead[i - lo]) {
+        livem |= 1u << k;
+        atomicAdd(&s_live[b0], 1);
       } else {
         d.pel_dead[D0 + i] = 0;  // eaten: dropped, and its flag clean for the next time this home is used
+      }
+    }
+    int tot;
+    int ex = block_excl1(__popc(livem), wsum, tot);  // (its barriers complete the bucket counts)
+    total = bucket_scans();
+#pragma unroll
+    for (int k = 0; k < PU_K; k++)
+      if ((livem >> k) & 1) {
+        const int bx = bk[k], pos = nb + s_nofs[bx] + (ex - s_lpre[bx]);
+        ex++;
+        if (pos < lim) {
+          d.pel[S0 + pos] = s_rec[i0 + k - lo];
+          d.pel_col[S0 + pos] = s_rcol[i0 + k - lo];
+        }
+      }
+  } else {  // (longer rows: the same in chunks of 256 slots, the records loaded after the count)
+    for (int i = lo + tid; i < hi; i += blockDim.x)
+      if (!d.pel_dead[D0 + i]) atomicAdd(&s_live[bucket_of(i)], 1);
+    __syncthreads();
+    total = bucket_scans();
+    // survivors: slot i of bucket bx -> nb + new start + (survivors of bx before i)
+    int carry = 0;
+    for (int c0 = lo; c0 < hi; c0 += blockDim.x) {
+      const int i = c0 + tid;
+      bool live = false;
+      if (i < hi) live = !d.pel_dead[D0 + i];
+      int tot;
+      const int ex = carry + block_excl1(live ? 1 : 0, wsum, tot);
+      carry += tot;
+      if (i < hi) {
+        if (live) {
+          const int bx = bucket_of(i);
+          const int pos = nb + s_nofs[bx] + (ex - s_lpre[bx]);
+          if (pos < lim) {
+            d.pel[S0 + pos] = d.pel[S0 + i];
+            d.pel_col[S0 + pos] = d.pel_col[S0 + i];
+          }
+        } else {
+          d.pel_dead[D0 + i] = 0;
+        }
       }
     }
   }
@@ -3672,7 +3733,10 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
     if (pos >= lim) continue;
     PelRec rec;
     int col = -1;
-    if (j >= nconv && spec) {  // a spawn drawn ahead by k_tick_begin
+    if (k < PU_JREC) {
+      rec = s_jrec[k];
+      col = s_jcol[k];
+    } else if (j >= nconv && spec) {
       const size_t o = (size_t)a * kSpawnAhead + (j - nconv);
       rec = PelRec{d.spec_x[o], d.spec_y[o], d.spec_m[o], c.seq_base_spawn + (j - nconv)};
     } else {
