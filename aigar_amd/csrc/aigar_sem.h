@@ -70,6 +70,16 @@ AIGAR_D bool overlap(double ax, double ay, double am, double ar, double bx, doub
   return d2 * 1.1 < R * R;
 }
 AIGAR_D bool can_eat(double m, double other) { return m > 1.25 * other; }  // cell.py:163-164
+// Cell.isInFov.  The reference's FOV queries (getPelletsInFov & co.,
+// field.py:434-456) are a hash query around the FOV box -- objects whose bucket
+// footprint meets Q = footprint(fx, fy, fs / 2) -- filtered by isInFov, and
+// isInFov IMPLIES that overlap, so the queries test isInFov alone: per axis,
+// x - r <= xmax gives floor(max(0, x - r) / 20) <= floor(xmax / 20) = Q's last
+// bucket, and x + r >= xmin gives Q's first bucket floor(max(0, xmin) / 20) <=
+// floor((x + r) / 20) = the footprint's last (the same rounded x - r, x + r and
+// fx -+ fs / 2 on both sides; the field-size clamps only pull both last buckets
+// to (size - 1) / 20).  tests/test_fov_membership.py checks it against the
+// reference's getIdsForArea on 2 M random and bucket-edge cases.
 AIGAR_D bool in_fov(double x, double y, double r, double fx, double fy, double fs) {  // cell.py:169-177
   double h = fs / 2, xmin = fx - h, xmax = fx + h, ymin = fy - h, ymax = fy + h;
   return !(x + r < xmin || x - r > xmax || y + r < ymin || y - r > ymax);

@@ -384,8 +384,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
         sq = kd == 1 ? 0 : S[gr];
         uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
         if (kd == 0) r = pellet_radius(m);
+        // (the hash query's footprint test is implied by isInFov: aigar_sem.h in_fov)
         ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && pool_owner(g) == gp) &&
-             rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs);
+             in_fov(x, y, r, fx, fy, fs);
       }
       uint32_t msk = 0;
       if (ok) {
@@ -526,6 +527,15 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       colx += gs;
       rowy += gs;
     }
+  // per column / row (lane j): the wall channel's clipped extents -- a square's
+  // free area is (rb - lb) * (bb - tb) of its column's and its row's values,
+  // the same doubles (bot.py:444-450) -- and whether the square lies inside
+  // the field (bits of a ballot per axis): one multiply and a few integer ops
+  // per square instead of eight clamps and four compares
+  const double wcol = py_max(py_min(colx + gs / 2, fieldSize), 0.0) - py_min(py_max(colx - gs / 2, 0.0), fieldSize);
+  const double hrow = py_max(py_min(rowy + gs / 2, fieldSize), 0.0) - py_min(py_max(rowy - gs / 2, 0.0), fieldSize);
+  const unsigned long long in_col = __ballot(!(colx + gs / 2 < 0 || colx - gs / 2 > fieldSize));
+  const unsigned long long in_row = __ballot(!(rowy + gs / 2 < 0 || rowy - gs / 2 > fieldSize));
   const double inv_G = 1.0 / G, inv_cols = 1.0 / cols;
   // t / n for 0 <= t, n < 2^20: double reciprocal, then one correction step
   auto idiv = [](int t, int n, double inv_n) {
@@ -543,22 +553,29 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // (squares t = lane, lane + 64: one pass over each list, vp0 / vp1 ...)
   double vp0 = 0, vp1 = 0, vs0 = 0, vs1 = 0, ve0 = 0, ve1 = 0, vv0 = 0, vv1 = 0;
   auto squares = [&](auto hist_regs, auto pre, auto PEL, auto CEL, auto VIR) __attribute__((always_inline)) {
-  for (int t = lane; t < GG; t += 64) {
+  for (int t0 = 0; t0 < GG; t0 += 64) {
+    // every lane runs the shuffles (a shuffle from a lane outside the loop's
+    // active set reads 0): lanes past the grid take the last square and store nothing
+    const int t = min(t0 + lane, GG - 1);
+    const bool act = t0 + lane < GG;
     const int c = idiv(t, G, inv_G), r = t - c * G;
-    double mx, my;
+    double mx, my, freeA = 0;
     if (G <= 64) {  // (wave-uniform)
       mx = __shfl(colx, r);
       my = __shfl(rowy, c);
+      freeA = __shfl(wcol, r) * __shfl(hrow, c);
     } else {
       mx = left + gs / 2;
       my = top + gs / 2;
       for (int i = 0; i < r; i++) mx += gs;
       for (int i = 0; i < c; i++) my += gs;
     }
+    if (!act) continue;
     const int iy = idiv(t, cols, inv_cols), ix = t - iy * cols;
     uint32_t need = (1u << ix) | (1u << (16 + iy));
     double vp = 0, ve = 0, vs = 0, vv = 0;
-    bool within = !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
+    const bool within = G <= 64 ? ((in_col >> r) & (in_row >> c) & 1) != 0
+                                : !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
     if constexpr (decltype(pre)::value) {
       vp = t < 64 ? vp0 : vp1;
       vs = t < 64 ? vs0 : vs1;
@@ -611,9 +628,11 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
 #ifdef AIGAR_OBS_DIAG_NOWALL  // (cost diagnostics only, results invalid)
     double vw = 0.0;
 #else
-    double lb = py_min(py_max(mx - gs / 2, 0.0), fieldSize), tb = py_min(py_max(my - gs / 2, 0.0), fieldSize);
-    double rb = py_max(py_min(mx + gs / 2, fieldSize), 0.0), bb = py_max(py_min(my + gs / 2, fieldSize), 0.0);
-    double freeA = (rb - lb) * (bb - tb);
+    if (G > 64) {
+      double lb = py_min(py_max(mx - gs / 2, 0.0), fieldSize), tb = py_min(py_max(my - gs / 2, 0.0), fieldSize);
+      double rb = py_max(py_min(mx + gs / 2, fieldSize), 0.0), bb = py_max(py_min(my + gs / 2, fieldSize), 0.0);
+      freeA = (rb - lb) * (bb - tb);
+    }
     // round(1 - freeA / (gs*gs), 3).  A square inside the field has freeA within
     // a few ulps of gs*gs, and the result is a zero whose sign is that of
     // 1 - fl(freeA / gs2): negative iff fl(freeA / gs2) > 1, i.e. iff the exact
@@ -679,11 +698,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       {
         auto sq = [&](int t, bool &ok, uint32_t &need) {
           const int c = idiv(t, G, inv_G), r = t - c * G;
-          const double mx = __shfl(colx, r), my = __shfl(rowy, c);
           const int iy = idiv(t, cols, inv_cols), ix = t - iy * cols;
           need = (1u << ix) | (1u << (16 + iy));
-          ok = t < GG && ix < 16 &&
-               !(mx + gs / 2 < 0 || mx - gs / 2 > fieldSize || my + gs / 2 < 0 || my - gs / 2 > fieldSize);
+          ok = t < GG && ix < 16 && ((in_col >> r) & (in_row >> c) & 1) != 0;
         };
         sq(lane, ok0, nd0);
         sq(lane + 64, ok1, nd1);
@@ -883,7 +900,7 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
     const uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
     if ((fl & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
     if (kd == 1 && (int)(g % NP) == gp) return;
-    if (!(rect_hit(footprint(x, y, r, d.size), Q) && in_fov(x, y, r, fx, fy, fs))) return;
+    if (!in_fov(x, y, r, fx, fy, fs)) return;  // (implies the hash query's footprint test: aigar_sem.h)
     if (kd != 0 && !(bm > 1.25 * m)) return;  // the biggest own cell must be able to eat it
     const double sd = (x - bx) * (x - bx) + (y - by) * (y - by);
     const double k = m / (sd != 0 ? sd : 1);

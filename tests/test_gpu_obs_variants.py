@@ -70,6 +70,19 @@ def test_wide_grid_matches_oracle(G, bots, seed):
     assert states.shape == (8 * bots, 9 * G * G)
 
 
+@pytest.mark.parametrize("G,seed", [(8, 21), (13, 22), (14, 23), (16, 24)])
+def test_default_kernel_other_grid_sizes(G, seed):
+    """k_observe (16-bit square masks) at grid sizes beside the default 11: the
+    paired-square fast path (GG <= 128) and the generic loop (up to 4 squares per
+    lane; G = 14 leaves 4 lanes in the last round, whose shuffles must still read
+    the column / row values of the other lanes)."""
+    ch = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
+          | _abi.OBS_ENEMY_LF)
+    cfg = make_config(bots=48, virus=True, max_viruses=12, channels=ch, extras=0x1F, grid_squares=G)
+    states = _run(cfg, 30, seed, 0.04, 0.04, obs_every=3)
+    assert states.shape == (10 * 48, 7 * G * G + 11)
+
+
 def test_wide_grid_overflow_pool_and_big_views():
     """Big cells (wide views, thousands of visible pellets: the lists leave LDS for
     the global pool) at 42 squares per side."""
