@@ -120,6 +120,7 @@ def load(build_if_missing=False):
         "aigar_tile_comm_init": [vp, C.c_char_p, vp, i32, i32],
         "aigar_tile_run": [vp, i32, C.POINTER(_abi.RunParams), i32, vp, i32],
         "aigar_tile_run_graphed": [vp],
+        "aigar_tile_loopback": [vp],
     }
     for name, args in sig.items():
         f = getattr(L, name, None)
@@ -445,6 +446,11 @@ class Stepper:
 
     def tile_run_graphed(self):
         return bool(self.L.aigar_tile_run_graphed(self.h))
+
+    def tile_loopback(self):
+        """Timing rehearsal (include/aigar.h aigar_tile_loopback): tile_run without a
+        communicator, every other tile's message empty."""
+        self._chk(self.L.aigar_tile_loopback(self.h))
 
     def tile_end(self, out=None):
         p, dt = None, 0

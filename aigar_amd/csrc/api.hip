@@ -142,6 +142,7 @@ struct aigar_handle {
   void *rccl_comm = nullptr;
   int rccl_ranks = 0;
   bool rccl_bad = false;  // an all-gather failed while a graph was captured
+  bool loopback = false;  // timing rehearsal: the exchange copies this tile's message to its own slot only
   hipGraphExec_t tr_graph = nullptr;
   aigar_run_params tr_key{};
   void *tr_out = nullptr;
@@ -876,6 +877,12 @@ extern "C" int aigar_tile_comm_init(aigar_handle *h, const char *path, const voi
 
 // every tile's current-pass message into every tile's inbox (tile k at k * bytes)
 static int tile_allgather(aigar_handle *h, hipStream_t s, int recs) {
+  if (h->loopback) {  // (aigar_tile_loopback: the other slots hold empty messages)
+    const size_t bytes = (size_t)recs * sizeof(TileRec);
+    HIPCHK(hipMemcpyAsync((char *)h->d.inbox + (size_t)h->d.tile_id * bytes, h->d.outbox, bytes,
+                          hipMemcpyDeviceToDevice, s));
+    return 0;
+  }
   const int r = g_rccl.all_gather(h->d.outbox, (void *)h->d.inbox, (size_t)recs * sizeof(TileRec), kNcclUint8,
                                   h->rccl_comm, s);
   if (r) {
@@ -923,7 +930,7 @@ static int issue_tile_step(aigar_handle *h, hipStream_t s, const aigar_run_param
 extern "C" int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_params *p, int extra_passes,
                               void *obs_out, int dtype) {
   if (need_tiled(h) || !p) return p ? -1 : fail("null argument");
-  if (!h->rccl_comm) return fail("tile_run: no RCCL communicator (aigar_tile_comm_init)");
+  if (!h->rccl_comm && !h->loopback) return fail("tile_run: no RCCL communicator (aigar_tile_comm_init)");
   if (n_steps < 0 || extra_passes < 0 || extra_passes > 64) return fail("tile_run: bad n_steps / extra_passes");
   if (p->policy != AIGAR_POLICY_NONE && p->policy != AIGAR_POLICY_RANDOM)
     return fail("tile_run: policy must be NONE or RANDOM (the greedy policy reads pellets other tiles hold)");
@@ -961,6 +968,19 @@ extern "C" int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_para
 }
 
 extern "C" int aigar_tile_run_graphed(aigar_handle *h) { return h && h->tr_graph ? 1 : 0; }
+
+extern "C" int aigar_tile_loopback(aigar_handle *h) {
+  if (need_tiled(h)) return -1;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  // every slot an empty message (kind TR_HDR, no records, nothing undone, no kills)
+  HIPCHK(hipMemsetAsync((void *)h->d.inbox, 0, (size_t)h->box_recs * h->d.ntiles * sizeof(TileRec), h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->loopback = true;
+  if (h->tr_graph) (void)hipGraphExecDestroy(h->tr_graph);
+  h->tr_graph = nullptr;
+  h->tr_failed = false;
+  return 0;
+}
 
 // the tile that computed each bot's row at the last observation (-1: dead /
 // not observed); every tile computes the same assignment

@@ -388,6 +388,12 @@ int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_params *p, int 
                    int dtype);
 /* 1 if aigar_tile_run replays a captured graph, 0 if it launches directly */
 int aigar_tile_run_graphed(aigar_handle *h);
+/* Timing rehearsal only (tools/c4_solo.py): aigar_tile_run without a
+ * communicator, the exchange replaced by a copy of this tile's message into its
+ * own inbox slot, every other tile's slot an empty message.  The tile then steps
+ * alone on its GPU -- the per-GPU cost of a tiled step without the all-gather;
+ * its world is not the tiled arena's (no other tile's outcomes arrive). */
+int aigar_tile_loopback(aigar_handle *h);
 
 /* The event log as raw rows (key_hi = tick << 8 | phase, key_lo = order within the
  * phase, code, a, b), unsorted: tiled arenas merge their tiles' logs by key. */

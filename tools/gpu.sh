@@ -10,6 +10,7 @@
 #   pmc               FETCH_SIZE / WRITE_SIZE passes of every step kernel + summary
 #   c4time            tools/c4_tile_timing.py 8 40 (per-tile phases, serialized)
 #   c4prof            rocprofv3 kernel trace of tools/c4_tile_timing.py 8 20
+#   c4solo            tools/c4_solo.py 8 200 (each tile alone, aigar_tile_run graph, loopback exchange)
 #   gloo:N            bench.py --gpus N rehearsal (N ranks sharing the card over gloo)
 #   ab:SO_B[:rounds]  alternating bench runs of the in-tree build against SO_B
 set -o pipefail
@@ -54,6 +55,10 @@ for S in "$@"; do
         || fail c4time $? $O/${TAG}_c4_tiles.err
       python3 -c "import json;d=json.load(open('$O/${TAG}_c4_tiles.json'));print('max tile %.1f us' % d['max_tile_total_us'], d['untiled_us']); [print(r) for r in d['per_tile_us']]" ;;
     c4prof) prof c4prof $R/tools/c4_tile_timing.py 8 20 ;;
+    c4solo)
+      timeout -k 10 300 python -u tools/c4_solo.py 8 200 > $O/${TAG}_c4_solo.json 2> $O/${TAG}_c4_solo.err \
+        || fail c4solo $? $O/${TAG}_c4_solo.err
+      python3 -c "import json;d=json.load(open('$O/${TAG}_c4_solo.json'));print('solo max tile %.1f us, untiled %.1f us' % (d['max_tile_us_per_step'], d['untiled_us_per_step'])); [print(r) for r in d['per_tile']]" ;;
     gloo:*)
       N=${S#gloo:}
       AIGAR_DIST_BACKEND=gloo timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node $N \
