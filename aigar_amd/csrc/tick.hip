@@ -1911,10 +1911,13 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
       bool keep = false;
       double fx = 0, fy = 0, fm = 0;
       int64_t fsq = 0;
-      if (valid) {  // the record and the liveness in one round of loads
+      if (valid) {
         F.load(j, fx, fy, fm, fsq);
-        // a blob's own ejecter cell skips it (field.py:219)
-        keep = F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(fx, fy, F.rad(j, fm), d.size), q);
+        // (a pellet's liveness: every pellet in the store and the staging list is
+        // alive when a tick's first eat pass begins -- the closing update drops the
+        // eaten, tick_zero clears the staged records' flags -- so only a later pass
+        // of a tiled tick, after other tiles' kills arrived, loads it)
+        keep = (!resume || F.alive(j)) && rect_hit(footprint(fx, fy, pellet_radius(fm), d.size), q);
       }
       unsigned long long bal = __ballot(keep);
       int slot = cnt + __popcll(bal & ((1ull << lane) - 1));
@@ -2833,12 +2836,11 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
   if (!dkey) PA_STORE(a);
 }
 // the whole pass in one wavefront (nw pending players in d.work)
-__device__ __forceinline__ void pp_serial_body(const Dev &d, int a, uint32_t *pend, uint32_t *odirty, int nw) {
-  // candidates of the current turn, with their state at turn start (only the
-  // turn's own cell changes them: what it eats dies, and it stops when eaten)
-  __shared__ int64_t s_key[PP_LCAP];
-  __shared__ int s_val[PP_LCAP], s_srt[PP_LCAP];
-  __shared__ double s_x[PP_LCAP], s_y[PP_LCAP], s_m[PP_LCAP], s_r[PP_LCAP];
+// L: the candidates of the current turn, with their state at turn start (only
+// the turn's own cell changes them: what it eats dies, and it stops when eaten)
+// -- LDS shared with the parallel groups' lists (the two paths never run together)
+__device__ __forceinline__ void pp_serial_body(const Dev &d, int a, uint32_t *pend, uint32_t *odirty, int nw,
+                                               const PPL &L) {
   const int lane = threadIdx.x & 63, NW = (d.B + 31) / 32;
   for (int i = lane; i < NW; i += 64) pend[i] = 0;
   wave_fence();
@@ -2850,7 +2852,7 @@ __device__ __forceinline__ void pp_serial_body(const Dev &d, int a, uint32_t *pe
   if (nw == 0) return;
   ArenaCtl &c = d.ctl[a];
   double rmax = c.rmax_cell;
-  pp_turns(d, a, pend, PPL{s_key, s_val, s_srt, s_x, s_y, s_m, s_r, PP_LCAP}, odirty, rmax, nullptr, 0);
+  pp_turns(d, a, pend, L, odirty, rmax, nullptr, 0);
   c.rmax_cell = rmax;
 }
 
@@ -2878,7 +2880,7 @@ extern "C" int aigar_debug_ppdiag(unsigned long long *out) {
 #define PP_DIAG(k)
 #endif
 constexpr int PPG_SEEDS = 64;  // most pending players for the parallel pass
-constexpr int PPG_PL = 16;     // players per closure
+constexpr int PPG_PL = 16;     // players per closure (32 measured: the crowded world's overflowing closures exceed it too)
 constexpr int PPG_CELLS = 64;  // cells per closure (also the turn candidate cap)
 #ifndef AIGAR_PPG_WAVES
 #define AIGAR_PPG_WAVES 16
@@ -2895,7 +2897,7 @@ __device__ __forceinline__ bool pp_closure(const Dev &d, int a, int *pl, int &np
   const int *it = d.citems + (size_t)a * kMaxCells * B;
   const double rmax0 = d.ctl[a].rmax_cell;
   wave_fence();
-  for (int iter = 0; iter < 8; iter++) {
+  for (int iter = 0; iter < 12; iter++) {
     // the group's cells: (player j, slot k) pairs, four per lane, one load round
     uint32_t fl[4];
     double cx[4], cy[4], cm[4], cr[4];
@@ -3009,9 +3011,11 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   __syncthreads();
   const int nw = s_nw, dead0 = s_dead0;
   const bool par = d.pp_par && odirty && nw >= PPG_MIN && nw <= PPG_SEEDS && nwv >= PPG_WAVES;
+  static_assert(PPG_WAVES * PPG_CELLS >= PP_LCAP, "the serial pass's candidate lists live in the groups' LDS");
+  const PPL serial_l{&g_key[0][0], &g_val[0][0], &g_srt[0][0], &g_x[0][0], &g_y[0][0], &g_m[0][0], &g_r[0][0], PP_LCAP};
   if (!par) {
     if (tid == 0 && nw > 0) PP_DIAG(nw < PPG_MIN ? 0 : 1);
-    if (tid < 64) pp_serial_body(d, a, pend, odirty, nw);
+    if (tid < 64) pp_serial_body(d, a, pend, odirty, nw, serial_l);
     return;
   }
   // closures; per player the lowest seed whose closure holds it
@@ -3102,7 +3106,7 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   PT_MARK(5, 6);
   if (tid == 0) PP_DIAG(s_bad ? 5 : 6);
   if (s_bad) {  // a closure overflowed, or two groups may meet: the serial pass
-    if (tid < 64) pp_serial_body(d, a, pend, odirty, nw);
+    if (tid < 64) pp_serial_body(d, a, pend, odirty, nw, serial_l);
     return;
   }
   if (w < PPG_WAVES) {

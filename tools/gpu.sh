@@ -12,7 +12,8 @@
 #   c4prof            rocprofv3 kernel trace of tools/c4_tile_timing.py 8 20
 #   c4solo            tools/c4_solo.py 8 200 (each tile alone, aigar_tile_run graph, loopback exchange)
 #   gloo:N            bench.py --gpus N rehearsal (N ranks sharing the card over gloo)
-#   ab:SO_B[:rounds]  alternating bench runs of the in-tree build against SO_B
+#   ab:SO_B[:rounds]  alternating bench runs of the in-tree build against SO_B (extra bench args: $AB_ARGS)
+#   ppdiag            tools/pp_diag.py on tools/var/lib_ppdiag.so (why the parallel pp pass fell back)
 set -o pipefail
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT; [ -z "$R" ] && R=$(pwd)
@@ -72,10 +73,13 @@ for S in "$@"; do
         for v in A B; do
           so=""; [ $v = B ] && so=$R/$B
           AIGAR_SO=$so timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pixels \
-            --batched-arenas 0 --no-c4 > $O/${TAG}_ab_${v}$i.json 2>/dev/null || fail "ab $v" $?
+            --batched-arenas 0 --no-c4 $AB_ARGS > $O/${TAG}_ab_${v}$i.json 2>/dev/null || fail "ab $v" $?
           python3 -c "import json;d=json.loads(open('$O/${TAG}_ab_${v}$i.json').read().strip().splitlines()[-1]);b=d['breakdown_ms_per_step'];print('$v', round(d['value']/1e6,2), 'M/s  ms/step %.4f tick %.4f obs %.4f' % (d['ms_per_step'], b['tick'], b['observe']))"
         done
       done ;;
+    ppdiag)
+      timeout -k 10 300 python -u tools/pp_diag.py > $O/${TAG}_ppdiag.txt 2>&1 || fail ppdiag $? $O/${TAG}_ppdiag.txt
+      cat $O/${TAG}_ppdiag.txt ;;
     *) fail "unknown step $S" 2 ;;
   esac
 done
