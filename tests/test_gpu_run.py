@@ -96,22 +96,56 @@ def test_run_rejects_host_buffers_and_bad_policy():
     g.close()
 
 
-def test_run_many_steps_in_one_call():
+@pytest.mark.parametrize("policy", ["random", "greedy"])
+def test_run_many_steps_in_one_call(policy):
     """Many steps in ONE aigar_run call (graph replays back to back): the last
     rows (whose last-frame channels chain through every step's history) and the
-    world must equal the separate calls'."""
+    world must equal the separate calls'.  Greedy: inside a call every step's
+    observation also makes the next step's Greedy moves (k_observe<..., GR>),
+    so steps 2..n take moves the fused observation staged."""
     cfg = _cfg(bots=512)
     fused, sep = _pair(cfg, 12)
     oa = torch.zeros((fused.NP, fused.obs_len), dtype=torch.float64, device="cuda")
     ob = torch.zeros_like(oa)
     for n in (1, 7, 24):
-        fused.run(n, "random", oa, p_split=0.05, p_eject=0.05, seed=5)
+        fused.run(n, policy, oa, p_split=0.05, p_eject=0.05, seed=5, greedy_split=True)
         for _ in range(n):
-            sep.policy_random(0.05, 0.05, 5)
+            if policy == "random":
+                sep.policy_random(0.05, 0.05, 5)
+            else:
+                sep.policy_greedy(True)
             sep.step(1)
             sep.observe(ob)
         torch.cuda.synchronize()
         assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0)), n
-    assert parity.diff_states(fused.get_state(), sep.get_state(), ftol=0.0) == []
+        assert parity.diff_states(fused.get_state(), sep.get_state(), ftol=0.0) == [], n
+    fused.close()
+    sep.close()
+
+
+def test_greedy_run_at_c3_matches_separate_calls():
+    """The bench's greedy line: the matured C3 world (tick 50), 4096 Greedy bots
+    with ENABLE_GREEDY_SPLIT, 40 steps in two aigar_run calls (the fused
+    observation stages every move after a call's first) against the policy
+    launch + tick + observation as separate calls: rows, world and commands
+    identical, with deaths and respawns on the way."""
+    import bench
+    cfg = bench.make_cfg("c3")
+    fused, sep = _lib.Stepper(cfg), _lib.Stepper(cfg)
+    for s in (fused, sep):
+        s.set_stream(torch.cuda.current_stream().cuda_stream)
+        bench.start_world(s, "c3", 1, 1)
+    oa = torch.zeros((fused.NP, fused.obs_len), dtype=torch.float64, device="cuda")
+    ob = torch.zeros_like(oa)
+    for n in (15, 25):
+        fused.run(n, "greedy", oa, greedy_split=True)
+        for _ in range(n):
+            sep.policy_greedy(True)
+            sep.step(1)
+            sep.observe(ob)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0)), n
+        assert parity.diff_states(fused.get_state(), sep.get_state(), ftol=0.0) == [], n
+    assert fused.counters()["ticks"] == sep.counters()["ticks"]
     fused.close()
     sep.close()
