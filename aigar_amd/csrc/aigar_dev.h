@@ -12,8 +12,9 @@
 //           home, sorted by centre bucket, so bucket (bx, by) is the range
 //           [pstart[a*PH1 + by*(cols+1) + bx], the next entry) and a grid row's
 //           buckets bx0..bx1 are ONE range (entry cols of a row = the row's end).
-//           The closing update rewrites only the rows whose pellets changed, each
-//           into its other home (field.py:303-313, 327-344 change a few per tick).
+//           The closing update rewrites only the rows whose pellets changed, from
+//           the first changed slot on, in place (a long suffix: the whole row into
+//           its other home) (field.py:303-313, 327-344 change a few per tick).
 //           Dead flags / reservation keys: a*PD + slot, staged records a*PD + PS + j.
 //   blob    a*Ecap + i,   virus a*Vcap + i   (list order == creation order)
 //   grids   a*(H+1) + bucket   (H = cols*cols, 20-unit buckets)

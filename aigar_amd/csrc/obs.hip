@@ -214,8 +214,13 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 
 #ifdef AIGAR_OBS_WPE
 #define OBS_ATTR __attribute__((amdgpu_waves_per_eu(AIGAR_OBS_WPE, 8)))
-#else  // 4 waves/SIMD: 4096 bots = 16 waves per CU, one residency round on 256 CUs
-#define OBS_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
+#else
+// WT (launches of <= 16,384 bots): 4 waves/SIMD -- 4096 bots = 16 waves per CU,
+// one residency round on 256 CUs, and the prologue's early loads fit; !WT (many
+// arenas: a streaming launch of many residency rounds, bound by the waves in
+// flight): 5 waves/SIMD (96 VGPRs; 36 B per lane spilled) -- k_observe 37.3 ->
+// 39.4 % of HBM peak at 16 C3 arenas (profiles/r04_ab_notes.txt)
+#define OBS_ATTR __attribute__((amdgpu_waves_per_eu(WT ? 4 : 5, 8)))
 #endif
 // WT: the store policy of the row and the history (below), chosen per launch by
 // the number of bots (launch_observe)
@@ -322,12 +327,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     o += o < 0 ? NP : 0;
     return o >= NP ? o - NP : o;
   };
-  // last-frame history grids: independent of the queries, fetched up front
+  // last-frame history grids: independent of the queries
   // (first two squares of each lane; larger grids read the rest in the loop)
   // (GG <= 128: the loop below then issues no load, so no wait on its own stores)
   double h_slf0 = 0, h_slf1 = 0, h_elf0 = 0, h_elf1 = 0;  // (scalars: no stack slot)
   double h_sslf0 = 0, h_sslf1 = 0, h_eslf0 = 0, h_eslf1 = 0;
-  {
+  auto load_hist = [&]() __attribute__((always_inline)) {
     const uint32_t och = d.obs_ch;
     const bool pslf = och & (AIGAR_OBS_SELF_LF | AIGAR_OBS_SELF_SLF), pelf = och & (AIGAR_OBS_ENEMY_LF | AIGAR_OBS_ENEMY_SLF);
     const bool psslf = och & AIGAR_OBS_SELF_SLF, peslf = och & AIGAR_OBS_ENEMY_SLF;
@@ -341,7 +346,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     if (peslf && in0) h_eslf0 = d.o_en_slf[hb];
     if (psslf && in1) h_sslf1 = d.o_self_slf[hb + 64];
     if (peslf && in1) h_eslf1 = d.o_en_slf[hb + 64];
-  }
+  };
+// (their loads issued after the walk: early, the eight doubles stayed live through
+// the walk -- 127 VGPRs; late, 110 -- and the A/B favoured late, profiles/r04_ab_notes.txt)
 
   // ---- getPelletsInFov / getEnemyPlayerCellsInFov / getVirusesInFov
   // (field.py:434-456) as ONE walk: every grid row the FOV touches (pellet,
@@ -453,11 +460,28 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     }
   }
   wave_fence();  // lists written by all lanes -> read by all lanes
-  // rank pellets by creation sequence (the sum order of the reference)
+  load_hist();
   const bool in_lds = PL.seq == &p_sx[0].seq;  // (else the list overflowed into the global pool)
+  // Every visible pellet weighing a whole number of units (spawns weigh 1-3; a
+  // blob conversion need not): the pellet channel's sums are then exact in any
+  // order, so each pellet adds its mass into the squares it covers (LDS integer
+  // atomics below) -- no ranking by creation sequence, no per-square scan over
+  // the list.  Otherwise the reference's creation-order sums.
+  bool pint = false;
+#ifndef AIGAR_OBS_ORDERED_ONLY  // (A/B builds: the creation-order scan for every bot)
+  if (in_lds && GG <= OBS_PCAP && G <= 16) {
+    bool bad = false;
+    for (int i = lane; i < np; i += 64) {
+      const double m = p_m[i];
+      bad |= !(m >= 1.0 && m <= 65536.0 && m == floor(m));
+    }
+    pint = __ballot(bad) == 0;
+  }
+#endif
+  // rank pellets by creation sequence (the sum order of the reference)
   const double *sm = nullptr;
   const uint32_t *smk = nullptr;
-  if (in_lds) {  // np <= OBS_PCAP = 4 x 64: keep (rank, m, mask) in registers, then store in order
+  if (in_lds && !pint) {  // np <= OBS_PCAP = 4 x 64: keep (rank, m, mask) in registers, then store in order
     int rk4[OBS_PCAP / 64];
     double m4[OBS_PCAP / 64];
     uint32_t k4[OBS_PCAP / 64];
@@ -483,7 +507,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       }
     sm = &p_sx[0].m;
     smk = &p_px[0].mask;
-  } else {
+  } else if (!in_lds) {
     for (int i = lane; i < np; i += 64) {
       int64_t sq = PL.seq[i];
       int rk = 0;
@@ -544,6 +568,29 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     q += ((q + 1) * n <= t) ? 1 : 0;
     return q;
   };
+  // the whole-unit pellets' sums (pint): square t = iy * cols + ix of every
+  // (column bit ix, row bit iy) of a pellet's mask -- the squares whose `need`
+  // bits the mask holds -- inside the field and with ix < 16, as in the scan
+  int *const s_pcnt = &p_px[0].perm;  // (the ranking's slots: unused on this path)
+  if (pint) {
+    for (int t = lane; t < GG; t += 64) s_pcnt[t] = 0;
+    wave_fence();
+    for (int i = lane; i < np; i += 64) {
+      const uint32_t mk = p_mask[i];
+      const int mi = (int)p_m[i];
+      for (uint32_t X = mk & 0xFFFFu; X; X &= X - 1) {
+        const int ix = __ffs(X) - 1;
+        if (ix >= cols) break;  // (bits ascend)
+        for (uint32_t Y = mk >> 16; Y; Y &= Y - 1) {
+          const int t = (__ffs(Y) - 1) * cols + ix;
+          if (t >= GG) break;
+          const int c = idiv(t, G, inv_G), r = t - c * G;
+          if ((in_col >> r) & (in_row >> c) & 1) atomicAdd(&s_pcnt[t], mi);
+        }
+      }
+    }
+    wave_fence();
+  }
   // instantiated twice: with the LDS lists themselves (ds_read, no wait on the
   // row stores in flight) and with generic pointers (a list in the overflow pool)
   // The per-square scans read list entry k through accessors: PEL(k) -> (mass,
@@ -582,17 +629,21 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       ve = t < 64 ? ve0 : ve1;
       vv = t < 64 ? vv0 : vv1;
     } else if (within && ix < 16) {
-      double s = 0;
-      bool anyp = false;
-      for (int k = 0; k < np; k++) {  // creation order
-        double m;
-        uint32_t mk;
-        PEL(k, m, mk);
-        const bool hit = (mk & need) == need;
-        s = hit ? s + m : s;
-        anyp |= hit;
+      if (pint) {
+        vp = (double)s_pcnt[t];
+      } else {
+        double s = 0;
+        bool anyp = false;
+        for (int k = 0; k < np; k++) {  // creation order
+          double m;
+          uint32_t mk;
+          PEL(k, m, mk);
+          const bool hit = (mk & need) == need;
+          s = hit ? s + m : s;
+          anyp |= hit;
+        }
+        if (anyp) vp = s;
       }
-      if (anyp) vp = s;
       bool fe = false, fo = false;
       for (int k = 0; k < nc; k++) {
         double m;
@@ -682,11 +733,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   }
   };
   const bool all_lds = in_lds && CL.mask == c_mask && VL.mask == v_mask;
-  if (all_lds && np <= 64 && nc <= 64 && nv <= 64 && GG <= 128) {
+  if (all_lds && (pint || np <= 64) && nc <= 64 && nv <= 64 && GG <= 128) {
     // common case: entry k of every list sits in lane k's registers and is read
     // with v_readlane into scalar registers (no LDS round trip per entry)
-    const double rpm = lane < np ? sm[lane] : 0.0, rcm = lane < nc ? c_mass[lane] : 0.0;
-    const uint32_t rpk = lane < np ? smk[lane] : 0u, rck = lane < nc ? c_mask[lane] : 0u;
+    const bool rp = !pint && lane < np;
+    const double rpm = rp ? sm[lane] : 0.0, rcm = lane < nc ? c_mass[lane] : 0.0;
+    const uint32_t rpk = rp ? smk[lane] : 0u, rck = lane < nc ? c_mask[lane] : 0u;
     const int rco = lane < nc ? c_own[lane] : 0;
     const double rvr = lane < nv ? v_rad[lane] : 0.0, rvm = lane < nv ? v_mass[lane] : 0.0;
     const int64_t rvs = lane < nv ? v_seqs[lane] : 0;
@@ -705,19 +757,24 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
         sq(lane, ok0, nd0);
         sq(lane + 64, ok1, nd1);
       }
-      double s0 = 0, s1 = 0;
-      bool a0 = false, a1 = false;
-      for (int k = 0; k < np; k++) {  // creation order
-        const double m = readlane_d(rpm, k);
-        const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)rpk, k);
-        const bool h0 = ok0 && (mk & nd0) == nd0, h1 = ok1 && (mk & nd1) == nd1;
-        s0 = h0 ? s0 + m : s0;
-        s1 = h1 ? s1 + m : s1;
-        a0 |= h0;
-        a1 |= h1;
+      if (pint) {  // (GG <= 128 here; the counts of squares outside the field or past ix 15 stayed 0)
+        vp0 = (double)s_pcnt[lane];
+        vp1 = lane + 64 < GG ? (double)s_pcnt[lane + 64] : 0.0;
+      } else {
+        double s0 = 0, s1 = 0;
+        bool a0 = false, a1 = false;
+        for (int k = 0; k < np; k++) {  // creation order
+          const double m = readlane_d(rpm, k);
+          const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)rpk, k);
+          const bool h0 = ok0 && (mk & nd0) == nd0, h1 = ok1 && (mk & nd1) == nd1;
+          s0 = h0 ? s0 + m : s0;
+          s1 = h1 ? s1 + m : s1;
+          a0 |= h0;
+          a1 |= h1;
+        }
+        vp0 = a0 ? s0 : 0.0;
+        vp1 = a1 ? s1 : 0.0;
       }
-      vp0 = a0 ? s0 : 0.0;
-      vp1 = a1 ? s1 : 0.0;
       bool fe0 = false, fo0 = false, fe1 = false, fo1 = false;
       for (int k = 0; k < nc; k++) {
         const double m = readlane_d(rcm, k);

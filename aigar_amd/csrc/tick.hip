@@ -3528,11 +3528,14 @@ __device__ __forceinline__ void respawn_fov_thread(const Dev &d, int gp) {
 // (respawn_fov_thread), then the virus spawns.  A row block finds whether a
 // killed slot (kill_list) lies in its row or a joining staged record (a blob
 // conversion nobody ate, a spawn; tiles: in the held range) has its centre in
-// it; if so it writes the row anew into its other home -- survivors by bucket
-// in their old order, each bucket's new records behind them (consumers rank
-// candidates by creation sequence, so order inside a bucket carries no meaning)
-// -- and the row's bucket starts.  Rows nothing touched are left alone: a
-// usual tick rewrites a few dozen of the 240 rows instead of the whole store.
+// it; if so it writes the row anew -- survivors by bucket in their old order,
+// each bucket's new records behind them (consumers rank candidates by creation
+// sequence, so order inside a bucket carries no meaning) -- and the row's bucket
+// starts.  Only the suffix from the first changed slot (the first kill, or the
+// old end of the first bucket a record joins) moves: it is parked in LDS and
+// written back in the row's home, the slots before it untouched; a suffix
+// longer than PU_LDS slots moves the whole row into its other home instead.
+// Rows nothing touched are left alone (their bucket starts not even read).
 constexpr int PU_ROW_STG = 512;  // joining records per row and tick (more: ERR_PELLET_CAP)
 constexpr int kPelRowCols = 1024;  // buckets per row the update handles (aigar_create checks)
 __device__ __forceinline__ int block_excl1(int v, int *wsum, int &total) {
@@ -3557,8 +3560,8 @@ __device__ __forceinline__ int block_excl1(int v, int *wsum, int &total) {
 constexpr int PU_JREC = 64;  // joining records per row kept whole in LDS (beyond: loaded again)
 constexpr int PU_LDS = 512;  // row slots whose records the update parks in LDS (longer rows: two rounds)
 constexpr int PU_K = PU_LDS / 256;  // consecutive slots per thread
-__device__ void pel_row_update(const Dev &d, int a, int r) {
-  __shared__ int s_flag[2];
+__device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
+  __shared__ int s_flag[3];
   __shared__ int s_sj[PU_ROW_STG];
   __shared__ short s_sbx[PU_ROW_STG];
   __shared__ PelRec s_jrec[PU_JREC];
@@ -3576,20 +3579,22 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
   const int nk = min(c.n_kill, d.Pcap);
   int *e0 = d.pstart + (size_t)a * d.PH1 + (size_t)r * (C + 1);
   const size_t S0 = (size_t)a * d.PS, D0 = (size_t)a * d.PD, Q0 = (size_t)a * d.Pcap;
-  // round 1: the row's bucket starts, the tick's kills, every staged record (whole:
-  // the joins' records are then in LDS when the row is written)
-  if (tid == 0) s_flag[0] = s_flag[1] = 0;
-  for (int bx = tid; bx <= C; bx += blockDim.x) s_ost[bx] = e0[bx];
-  __syncthreads();
-  const int lo = s_ost[0], hi = s_ost[C];
+  // round 1, ONE round of independent loads: the row's bucket starts, the
+  // tick's first kills and staged records (a staged record joining the row is
+  // kept whole in LDS: it is there when the row is written)
   const int *kl = d.kill_list + Q0;
-  for (int t = tid; t < nk; t += blockDim.x) {
-    const int k = kl[t];
-    if (k >= lo && k < hi) s_flag[0] = 1;
+  if (tid == 0) {
+    s_flag[0] = s_flag[1] = 0;
+    s_flag[2] = INT_MAX;  // the row's first changed slot
   }
-  for (int j = tid; j < nst; j += blockDim.x) {
-    PelRec rec;
-    int col = -1;
+  for (int bx = tid; bx <= C; bx += blockDim.x) {
+    s_ost[bx] = e0[bx];
+    if (bx < C) s_stc[bx] = 0;
+  }
+  const int kill0 = tid < nk ? kl[tid] : -1;
+  // staged record j: whether it joins this row (its centre bucket's column, or -1)
+  auto staged = [&](int j, PelRec &rec, int &col) {
+    col = -1;
     bool live = true;
     if (j < nconv) {
       rec = d.pn[Q0 + j];
@@ -3603,27 +3608,61 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
       col = d.pn_col[Q0 + j];
     }
     const int by = center_bucket_coord(rec.y, C);
-    if (live && by == r) {
-      const int bx = center_bucket_coord(rec.x, C);
-      if (tile_holds_bucket(d, bx, by)) {
-        const int k = atomicAdd(&s_flag[1], 1);
-        if (k < PU_ROW_STG) {
-          s_sj[k] = j;
-          s_sbx[k] = (short)bx;
-          if (k < PU_JREC) {
-            s_jrec[k] = rec;
-            s_jcol[k] = col;
-          }
-        }
+    if (!live || by != r) return -1;
+    const int bx = center_bucket_coord(rec.x, C);
+    return tile_holds_bucket(d, bx, by) ? bx : -1;
+  };
+  auto stage = [&](int j, int bx, const PelRec &rec, int col) {
+    const int k = atomicAdd(&s_flag[1], 1);
+    if (k < PU_ROW_STG) {
+      s_sj[k] = j;
+      s_sbx[k] = (short)bx;
+      if (k < PU_JREC) {
+        s_jrec[k] = rec;
+        s_jcol[k] = col;
       }
     }
+  };
+  PelRec rec0;
+  int col0 = -1, bx0 = -1;
+  if (tid < nst) bx0 = staged(tid, rec0, col0);
+  __syncthreads();
+  PT_MARK(8, 1);
+  const int lo = s_ost[0], hi = s_ost[C];
+  auto kill = [&](int k) {
+    if (k >= lo && k < hi) {
+      s_flag[0] = 1;
+      atomicMin(&s_flag[2], k);
+    }
+  };
+  kill(kill0);
+  for (int t = tid + blockDim.x; t < nk; t += blockDim.x) kill(kl[t]);
+  if (bx0 >= 0) stage(tid, bx0, rec0, col0);
+  for (int j = tid + blockDim.x; j < nst; j += blockDim.x) {
+    PelRec rec;
+    int col;
+    const int bx = staged(j, rec, col);
+    if (bx >= 0) stage(j, bx, rec, col);
   }
   __syncthreads();
+  PT_MARK(8, 2);
   const int ns_all = s_flag[1];
   if (!s_flag[0] && ns_all == 0) return;  // (uniform) untouched row
   const int ns = min(ns_all, PU_ROW_STG);
-  const int home = C * d.PR, nb = lo >= home ? lo - home : lo + home;  // the other home of the row
-  for (int bx = tid; bx < C; bx += blockDim.x) s_live[bx] = s_stc[bx] = 0;
+  // a join goes behind its bucket's survivors: the row changes from that bucket's old end
+  for (int k = tid; k < ns; k += blockDim.x) {
+    atomicAdd(&s_stc[s_sbx[k]], 1);
+    atomicMin(&s_flag[2], s_ost[s_sbx[k] + 1]);
+  }
+  __syncthreads();
+  const int f = min(s_flag[2], hi);
+  // in place (the row's home) when the changed suffix [f, hi) fits LDS: the slots
+  // before f keep their records and bucket starts and are neither read nor
+  // written; else the whole row into its other home
+  const bool inplace = hi - f <= PU_LDS;
+  const int home = C * d.PR, nb = inplace ? lo : lo >= home ? lo - home : lo + home;
+  for (int bx = tid; bx < C; bx += blockDim.x)
+    s_live[bx] = inplace ? max(0, min(s_ost[bx + 1], f) - s_ost[bx]) : 0;  // (slots before f: all live)
   __syncthreads();
   auto bucket_of = [&](int i) {  // old bucket of slot i: s_ost[bx] <= i < s_ost[bx + 1]
     int l = 0, h = C;  // invariant: s_ost[l] <= i < s_ost[h]
@@ -3657,21 +3696,20 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
     __syncthreads();
     return total;
   };
-  for (int k = tid; k < ns; k += blockDim.x) atomicAdd(&s_stc[s_sbx[k]], 1);
   int total;
-  if (hi - lo <= PU_LDS) {
-    // round 2 (rows of <= PU_LDS slots; C3's hold ~420): every slot's liveness,
-    // record and colour in ONE round of loads, the records parked in LDS until
-    // their new positions are known (registers: the launch spilled)
-    for (int i = lo + tid; i < hi; i += blockDim.x) {
+  if (inplace) {
+    // round 2: the suffix's liveness, records and colours in ONE round of loads,
+    // parked in LDS until their new positions are known (registers: the launch
+    // spilled) -- and before any of the suffix is overwritten
+    for (int i = f + tid; i < hi; i += blockDim.x) {
       const bool dead = d.pel_dead[D0 + i];
-      s_rec[i - lo] = d.pel[S0 + i];
-      s_rcol[i - lo] = d.pel_col[S0 + i];
-      s_rdead[i - lo] = dead ? 1 : 0;
+      s_rec[i - f] = d.pel[S0 + i];
+      s_rcol[i - f] = d.pel_col[S0 + i];
+      s_rdead[i - f] = dead ? 1 : 0;
     }
     __syncthreads();
-    // each thread's PU_K consecutive slots: bucket, survivor count
-    const int i0 = lo + PU_K * tid;
+    // each thread's PU_K consecutive suffix slots: bucket, survivor count
+    const int i0 = f + PU_K * tid;
     uint32_t livem = 0;
     int b0 = i0 < hi ? bucket_of(i0) : 0, bk[PU_K];
 #pragma unroll
@@ -3680,24 +3718,24 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
       if (i >= hi) continue;
       while (s_ost[b0 + 1] <= i) b0++;  // (consecutive slots: the next bucket is near)
       bk[k] = b0;
-      if (!s_rdead[i - lo]) {
+      if (!s_rdead[i - f]) {
         livem |= 1u << k;
         atomicAdd(&s_live[b0], 1);
       } else {
-        d.pel_dead[D0 + i] = 0;  // eaten: dropped, and its flag clean for the next time this home is used
+        d.pel_dead[D0 + i] = 0;  // eaten: dropped, and its flag clean for whatever lands on the slot
       }
     }
     int tot;
-    int ex = block_excl1(__popc(livem), wsum, tot);  // (its barriers complete the bucket counts)
+    int ex = (f - lo) + block_excl1(__popc(livem), wsum, tot);  // (its barriers complete the bucket counts)
     total = bucket_scans();
 #pragma unroll
     for (int k = 0; k < PU_K; k++)
       if ((livem >> k) & 1) {
         const int bx = bk[k], pos = nb + s_nofs[bx] + (ex - s_lpre[bx]);
         ex++;
-        if (pos < lim) {
-          d.pel[S0 + pos] = s_rec[i0 + k - lo];
-          d.pel_col[S0 + pos] = s_rcol[i0 + k - lo];
+        if (pos < lim && pos != i0 + k) {
+          d.pel[S0 + pos] = s_rec[i0 + k - f];
+          d.pel_col[S0 + pos] = s_rcol[i0 + k - f];
         }
       }
   } else {  // (longer rows: the same in chunks of 256 slots, the records loaded after the count)
@@ -3750,7 +3788,10 @@ __device__ void pel_row_update(const Dev &d, int a, int r) {
     d.pel[S0 + pos] = rec;
     d.pel_col[S0 + pos] = col;
   }
-  for (int bx = tid; bx < C; bx += blockDim.x) e0[bx] = nb + min(s_nofs[bx], d.PR);
+  for (int bx = tid; bx < C; bx += blockDim.x) {
+    const int st = nb + min(s_nofs[bx], d.PR);
+    if (st != s_ost[bx]) e0[bx] = st;  // (in place: the starts up to f's bucket stay)
+  }
   if (tid == 0) {
     e0[C] = nb + min(total, d.PR);
     atomicAdd(&c.n_pel, min(total, d.PR) - (hi - lo));
@@ -3772,7 +3813,7 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbF) {
   }
   const int a = blockIdx.x / d.cols, r = blockIdx.x - a * d.cols;
   if (r == 0 && threadIdx.x == 0) d.ctl[a].tick += 1;  // (nothing in this launch reads it)
-  pel_row_update(d, a, r);
+  pel_row_update(d, a, r PT_ARGS);
   PT_MARK(8, 3);
 }
 
