@@ -8,11 +8,11 @@
 //                             field.py:112-181, player.py:30-72; + updateHashTables for
 //                             blobs and viruses (field.py:121-132; centre-bucket counting
 //                             sort, membership tested exactly per query)
-//   k_merge_vb                mergePlayerCells + virus<-blob activity  field.py:183-198;
-//                             its last block: virusBlobOverlap's serial pass
-//                             field.py:246-253, 316-325
-//   k_pv_active               playerVirusOverlap       field.py:225-231, 333-370 (activity per
-//                             player; the serial pass in the last block)
+//   k_merge_pv                mergePlayerCells + virus<-blob activity + cell<-virus activity
+//                             field.py:183-198, 246-253, 225-231 (a player's thread merges,
+//                             then tests its cells); its last block: virusBlobOverlap's and
+//                             playerVirusOverlap's serial passes (field.py:316-325, 333-370)
+//                             (k_merge_vb: the merges alone, viruses disabled)
 //   k_food_prep/commit        playerPelletOverlap + playerBlobOverlap field.py:207-222 as one
 //                             "deterministic reservations" pass: each cell reserves the foods
 //                             it could ever eat; a cell commits once it owns them all (=> every
@@ -1425,8 +1425,9 @@ __device__ __forceinline__ void vb_active(const Dev &d, int gi) {
 // the serial passes are device bodies run by one wavefront per arena: as their
 // own launches (k_*_serial) or in the tail / head of a neighbouring kernel
 // (launch_tick: fold), which saves a dependent launch per idle pass
-__device__ void vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
-  if ((threadIdx.x & 63) != 0) return;
+// (returns, on lane 0, whether the pass had work: a virus may then have grown or split)
+__device__ bool vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
+  if ((threadIdx.x & 63) != 0) return false;
   ArenaCtl &c = d.ctl[a];
   int nw = min(c.n_pend, d.Wcap);
   c.n_pend = 0;
@@ -1434,7 +1435,7 @@ __device__ void vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
   int *w = d.work + (size_t)a * d.Wcap;
   int64_t *ck = scr_k + (size_t)a * d.Wcap;
   int *cv = scr_v + (size_t)a * d.Wcap;
-  if (nw == 0) return;
+  if (nw == 0) return false;
   // active viruses in list order; viruses appended by splits are visited too
   for (int k = 0; k < nw; k++) ck[k] = w[k];
   isort_kv(ck, w, nw);
@@ -1509,6 +1510,7 @@ __device__ void vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
       }
     }
   }
+  return true;
 }
 
 // mergePlayerCells (per player) and the virus<-blob activity test (per virus)
@@ -1620,29 +1622,59 @@ __device__ void pv_player(const Dev &d, int gp) {
     d.c_active[ci] = any;
     anyp |= any;
   }
-  if (anyp) {
-    const int w = atomicAdd(&d.ctl[a].n_pend, 1);
-    if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
+  if (anyp) {  // (its own work list: virusBlobOverlap's runs in the same launch)
+    const int w = atomicAdd(&d.ctl[a].n_pend2, 1);
+    if (w < d.Wcap) d.work2[(size_t)a * d.Wcap + w] = gp - a * d.B;
     else set_err(d, a, ERR_WORK_CAP);
   }
 }
+// The activity test again for every player of arena a, by one wavefront, after
+// virusBlobOverlap's serial pass had work: a virus that grew or split changes
+// which cells overlap an edible virus at playerVirusOverlap's start.
+__device__ void pv_redo(const Dev &d, int a) {
+  const int lane = threadIdx.x & 63;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (lane 0's virus writes)
+  if (lane == 0) __hip_atomic_store(&d.ctl[a].n_pend2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int p = lane; p < d.B; p += 64) pv_player(d, a * d.B + p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the lanes' work-list writes, read by lane 0)
+}
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
-__global__ void __launch_bounds__(256) k_pv_active(Dev d, int64_t *scr_k, int *scr_v, int fold) {
-  FLOOR(3);
-  const int gp = GTID;
-  if (gp < d.NP) pv_player(d, gp);
-  if (fold && last_block(d.ticket + 2, gridDim.x))
-    for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) pv_serial_body(d, a, scr_k, scr_v);
+// mergePlayerCells, the virus<-blob activity test and the cell<-virus activity
+// test in ONE launch (field.py:183-198, 246-253, 225-231): a player's thread
+// merges its cells, then tests them against the viruses -- a player's merges
+// touch only its own cells, and the virus test reads only its own cells and
+// the viruses.  The viruses are those of the phase's start unless
+// virusBlobOverlap's serial pass (the last block) had work, which is rare (0
+// per tick at C3, random or Greedy bots): then the arena's test runs again
+// (pv_redo) before playerVirusOverlap's serial pass.
+__global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *scr_v) {
+  FLOOR(2);
+  const int gi = GTID;
+  if (gi < d.NP) {
+    merge_player(d, gi);
+    pv_player(d, gi);
+  } else {
+    vb_active(d, gi - d.NP);
+  }
+  if (last_block(d.ticket + 0, gridDim.x))
+    for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) {
+      const bool vb = vb_serial_body(d, a, scr_k, scr_v);
+      if (__shfl(vb ? 1 : 0, 0)) pv_redo(d, a);
+      pv_serial_body(d, a, scr_k, scr_v);
+    }
 }
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
   if ((threadIdx.x & 63) != 0) return;
   ArenaCtl &c = d.ctl[a];
-  int nw = min(c.n_pend, d.Wcap);
-  c.n_pend = 0;
+  int nw = min(c.n_pend2, d.Wcap);
+  c.n_pend2 = 0;
   c.stat[1] += nw;
   if (nw == 0) return;
   const int NP = d.NP;
-  int *w = d.work + (size_t)a * d.Wcap;
+  int *w = d.work2 + (size_t)a * d.Wcap;
   int64_t *ck = scr_k + (size_t)a * d.Wcap;
   int *cv = scr_v + (size_t)a * d.Wcap;
   for (int k = 0; k < nw; k++) ck[k] = w[k];
@@ -3899,12 +3931,10 @@ void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, co
                      rp ? *rp : RandomPolicy{0, 0, 0, 0});
   // + the virus grid (extra block) and the blob grid (last block) of updateHashTables
   hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + (d.virus_enabled ? 1 : 0), d.A), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_merge_vb, dim3(nblk((long)d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0), 256)),
-                     dim3(256), 0, s, d, scr_k, scr_v, d.virus_enabled ? 1 : 0);  // + virusBlobOverlap's serial pass
-  if (d.virus_enabled) {
-    // playerVirusOverlap: activity test + its serial pass in the last block
-    hipLaunchKernelGGL(k_pv_active, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, scr_k, scr_v, 1);
-  }
+  if (d.virus_enabled)  // merges, both virus activity tests, both serial passes (last block)
+    hipLaunchKernelGGL(k_merge_pv, dim3(nblk((long)d.NP + (long)d.A * d.Vcap, 256)), dim3(256), 0, s, d, scr_k, scr_v);
+  else
+    hipLaunchKernelGGL(k_merge_vb, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, scr_k, scr_v, 0);
 }
 // the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
