@@ -215,12 +215,12 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 #ifdef AIGAR_OBS_WPE
 #define OBS_ATTR __attribute__((amdgpu_waves_per_eu(AIGAR_OBS_WPE, 8)))
 #else
-// WT (launches of <= 16,384 bots): 4 waves/SIMD -- 4096 bots = 16 waves per CU,
-// one residency round on 256 CUs, and the prologue's early loads fit; !WT (many
-// arenas: a streaming launch of many residency rounds, bound by the waves in
-// flight): 5 waves/SIMD (96 VGPRs; 36 B per lane spilled) -- k_observe 37.3 ->
-// 39.4 % of HBM peak at 16 C3 arenas (profiles/r04_ab_notes.txt)
-#define OBS_ATTR __attribute__((amdgpu_waves_per_eu(WT ? 4 : 5, 8)))
+// 4 waves/SIMD: 4096 bots = 16 waves per CU, one residency round on 256 CUs.
+// The streaming variant (!WT, many arenas) ran at 5 waves/SIMD for a while (96
+// VGPRs, 36 B per lane spilled: 37.3 -> 39.4 % of HBM peak at 16 C3 arenas);
+// with the order-free pellet sums it spilled 72 B and 4 waves measured better
+// again (38.5 -> 40.0 %, profiles/r04_ab_notes.txt)
+#define OBS_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
 // WT: the store policy of the row and the history (below), chosen per launch by
 // the number of bots (launch_observe)
