@@ -107,3 +107,47 @@ def test_wide_grid_overflow_pool_and_big_views():
         assert parity.obs_close(g.observe(), o.observe()), "tick %d" % t
     g.close()
     o.close()
+
+
+def test_pellet_sums_whole_units_and_converted():
+    """k_observe's pellet channel takes two paths: when every pellet a bot sees
+    weighs whole units (spawns, 1-3) the sums are scattered into the squares in
+    any order (exact: integer sums); a bot that sees a blob-made pellet (14.4)
+    keeps the creation-order scan.  Both must give the reference's doubles
+    bit for bit, so the pellet channel is compared EXACTLY here (not within
+    1e-5): a world where the left half of the field holds converted pellets
+    among the spawned ones, many of them per square, observed as loaded and
+    after a few ticks."""
+    cfg = make_config(bots=24, field_size=400, max_pellets=4000.0, channels=_abi.OBS_PELLET | _abi.OBS_SELF,
+                      extras=0)
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    o.reset(31)
+    st = o.get_state()
+    pf = np.array(st["pellets_f"], copy=True)
+    conv = pf[:, 0] < 200
+    sel = conv & (np.arange(len(pf)) % 3 == 0)  # a third of the left half's pellets are blob-made
+    pf[sel, 2] = 18 * 0.8
+    pf[sel, 3] = np.sqrt(pf[sel, 2] / np.pi)
+    st["pellets_f"] = pf
+    o.load_state(st)
+    g.load_state(st)
+    GG = 121
+    rng = np.random.default_rng(31)
+    n_mixed = n_whole = 0
+    for t in range(4):
+        og, oo = g.observe(), o.observe()
+        assert np.array_equal(np.isnan(og), np.isnan(oo))
+        pg, po = np.nan_to_num(og[:, :GG]), np.nan_to_num(oo[:, :GG])
+        assert np.array_equal(pg, po), "tick %d: pellet channel differs (max %g)" % (t, np.abs(pg - po).max())
+        assert parity.obs_close(og, oo)
+        frac = np.abs(po - np.round(po)) > 0
+        n_mixed += int(frac.any(axis=1).sum())
+        n_whole += int(((po > 0).any(axis=1) & ~frac.any(axis=1)).sum())
+        cmd = parity.synthetic_commands(rng, None, 24, 400, 0.0, 0.0)
+        g.set_commands(cmd)
+        o.set_commands(cmd)
+        g.step(1)
+        o.step(1)
+    assert n_mixed > 0 and n_whole > 0, (n_mixed, n_whole)  # both paths ran
+    g.close()
+    o.close()
