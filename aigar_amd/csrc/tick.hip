@@ -3680,11 +3680,26 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
   PT_MARK(8, 2);
   const int ns_all = s_flag[1];
   if (!s_flag[0] && ns_all == 0) return;  // (uniform) untouched row
-  const int ns = min(ns_all, PU_ROW_STG);
+  // More joining records than the LDS list holds (a large refill, e.g. the first
+  // tick after load_state of a depleted world): the list is dropped and the
+  // staged records are walked again, counted here and placed in chunks below.
+  const bool over = ns_all > PU_ROW_STG;  // (uniform)
+  const int ns = over ? 0 : ns_all;
   // a join goes behind its bucket's survivors: the row changes from that bucket's old end
   for (int k = tid; k < ns; k += blockDim.x) {
     atomicAdd(&s_stc[s_sbx[k]], 1);
     atomicMin(&s_flag[2], s_ost[s_sbx[k] + 1]);
+  }
+  if (over) {
+    for (int j = tid; j < nst; j += blockDim.x) {
+      PelRec rec;
+      int col;
+      const int bx = staged(j, rec, col);
+      if (bx >= 0) {
+        atomicAdd(&s_stc[bx], 1);
+        atomicMin(&s_flag[2], s_ost[bx + 1]);
+      }
+    }
   }
   __syncthreads();
   const int f = min(s_flag[2], hi);
@@ -3819,6 +3834,34 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
     }
     d.pel[S0 + pos] = rec;
     d.pel_col[S0 + pos] = col;
+  }
+  if (over) {
+    // the overflow's joins in chunks of blockDim staged records, in staging order:
+    // a record's rank in its bucket = the bucket's joins of earlier chunks
+    // (s_lpre, free once the survivors are placed) + its bucket mates earlier in
+    // its chunk (s_sbx, free once the list is dropped)
+    __syncthreads();
+    for (int bx = tid; bx < C; bx += blockDim.x) s_lpre[bx] = 0;
+    for (int c0 = 0; c0 < nst; c0 += blockDim.x) {
+      const int j = c0 + tid;
+      PelRec rec;
+      int col = -1, bx = -1;
+      if (j < nst) bx = staged(j, rec, col);
+      s_sbx[tid] = (short)bx;
+      __syncthreads();
+      if (bx >= 0) {
+        int rk = 0;
+        for (int q = 0; q < tid; q++) rk += s_sbx[q] == bx;
+        const int pos = nb + s_nofs[bx] + s_live[bx] + s_lpre[bx] + rk;
+        if (pos < lim) {
+          d.pel[S0 + pos] = rec;
+          d.pel_col[S0 + pos] = col;
+        }
+      }
+      __syncthreads();
+      if (bx >= 0) atomicAdd(&s_lpre[bx], 1);
+      __syncthreads();
+    }
   }
   for (int bx = tid; bx < C; bx += blockDim.x) {
     const int st = nb + min(s_nofs[bx], d.PR);

@@ -872,6 +872,7 @@ class Model:
         self.spectatedPlayer = None
         self.path = None
         self.screenWidth = self.screenHeight = None
+        self._field_kw = dict(field_kw)  # (kept for initParameters: a rebuilt Field keeps the sizes / flags)
         self.field = Field(self.virusEnabled, parameters, seed=seed, device=device, **field_kw)
         self.counter = 0
         # model.py:67-71: the pixel generator exists when the CNN reads pixels
@@ -957,7 +958,8 @@ class Model:
         self.parameters = parameters
         self.virusEnabled = bool(getattr(parameters, "VIRUS_SPAWN", False))
         self.resetLimit = getattr(parameters, "RESET_LIMIT", self.resetLimit)
-        self.field = Field(self.virusEnabled, parameters, seed=self.field.seed, device=self.field.device)
+        self.field = Field(self.virusEnabled, parameters, seed=self.field.seed, device=self.field.device,
+                           **self._field_kw)
         for p in self.players:
             p.field = None
             self.field.addPlayer(p)

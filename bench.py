@@ -38,12 +38,23 @@ sys.path.insert(0, ROOT)
 
 from aigar_amd import _abi, replicas  # noqa: E402
 
-# the reference's own Python src/model at C3 (tick + observation of every bot, one
-# core), timed in the build container by the survey: the reference
-# itself cannot travel to the GPU box, so it is quoted beside the C-port baseline
-REFERENCE_PY_C3 = {"value": 356.0, "unit": "env-steps/s", "cores": 1, "kind": "reference",
-                   "source": "SURVEY.md §6: reference src/model (Python, Greedy bots) Field.update + "
-                             "getGridStateRepresentation for all 4096 bots, build container, 1 core"}
+# the reference's own Python src/model on THIS workload (bench.py's start world and policy,
+# Field.update + the observation of every bot, one core), timed in the build container by
+# tools/golden/ref_cpu_bench.py: the reference itself cannot travel to the GPU box, so its
+# committed figure is quoted beside the C-port baseline
+def reference_python(workload):
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_ref_python_%s.json" % workload)))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    keep = ("value", "unit", "cores", "kind", "workload", "sample", "ms_per_step", "ms_field_update",
+            "ms_observe_all_bots", "host")
+    out = {k: d[k] for k in keep if k in d}
+    out["source"] = os.path.relpath(files[-1], ROOT)
+    return out
+
+
 SNAPSHOTS = {"c3": "c3_t50"}  # matured start worlds (tools/mature.py)
 
 # C3 observation config: VIRUS_SPAWN + ENABLE_SPLIT (networkParameters.py:76-96)
@@ -550,8 +561,10 @@ def main():
         out["c4"] = c4
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_run:  # (N = 1 only)
         out["cpu_baseline"] = cpu_baseline(name, args.cpu_budget, policy=args.policy)
-        if name == "c3":
-            out["cpu_baseline"]["reference_python"] = REFERENCE_PY_C3
+        if name == "c3" and args.policy == "random":  # (the file times bench.py's random policy)
+            ref_py = reference_python(name)
+            if ref_py is not None:
+                out["cpu_baseline"]["reference_python"] = ref_py
         if name == "c5":
             out["cpu_baseline_processes"] = cpu_baseline_c5(args.cpu_budget)
     if rank == 0:

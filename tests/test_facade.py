@@ -143,3 +143,15 @@ def test_colours_follow_the_reference_rules():
     assert M.VIRUS_COLOR == (0, 255, 0)
     p = M.Player("p")
     assert p.getColor() == M.player_color(-1, 0) or sum(p.getColor()) <= 600
+
+
+def test_init_parameters_keeps_the_world_options():
+    """Model.initParameters (model.py:79-84) rebuilds the Field; the
+    options given to the Model (field size, counts, event recording) must survive."""
+    from aigar_amd.model import Model
+    m = Model(False, False, None, seed=3, field_size=500, max_pellets=200.0, max_viruses=4.0, record_events=True)
+    m.createPlayer("p0")
+    m.initParameters(types.SimpleNamespace(VIRUS_SPAWN=True, RESET_LIMIT=77))
+    f = m.field
+    assert (f.field_size, f.max_pellets, f.max_viruses, f.record_events, f.seed) == (500, 200.0, 4.0, True, 3)
+    assert f.virusEnabled and m.resetLimit == 77 and len(f.players) == 1

@@ -85,3 +85,24 @@ def test_mass_cap_and_virus_explosion():
         most = max(most, int(np.max(st["players_i"][:, 4])))
     assert events > 0
     assert most == 16  # the explosion fills the player up to the 16-cell cap (field.py:354)
+
+
+def test_refill_of_a_depleted_world_in_one_tick():
+    """a tick whose spawns put more joining records into one bucket row
+    than the closing update's LDS list holds (512; field 1000 = 50 rows, 40,000
+    pellets: ~800 joins per row) -- the whole refill lands, in order, and the world
+    stays the oracle's; it keeps stepping from the refilled rows."""
+    cfg = make_config(bots=16, field_size=1000, max_pellets=40000.0, channels=CH & ~_abi.OBS_VIRUS, extras=0x1F)
+    g, o = _pair(cfg, 33)
+    d = g.get_state()
+    assert d["n_pellets"] == 40000
+    for k in ("pellets_f", "pellets_col"):
+        if k in d:
+            d[k] = d[k][:100]
+    d["pellets_seq"] = d["pellets_seq"][:100]
+    d["n_pellets"] = 100
+    _load_both(g, o, d)
+    st = _run(g, o, 1, 16, 1000, 0.0, 0.0, 33)
+    assert g.get_state()["n_pellets"] == 40000
+    _run(g, o, 20, 16, 1000, 0.05, 0.05, 34)
+    assert st["ticks"] == 1

@@ -102,13 +102,16 @@ def test_c3_matured_world_matches_oracle(policy):
     o.close()
 
 
-def test_c5_gpu_slice_matches_eight_oracles():
+@pytest.mark.parametrize("A,ticks,every", [(8, 60, 20), (40, 20, 10)])
+def test_c5_gpu_slice_matches_eight_oracles(A, ticks, every):
     """C5's per-GPU slice: 8 independent arenas x 512 bots, field
     1697, 43,200 pellets, viruses off, stepped by the same launches; each arena
     against its own single-arena oracle (loaded from the arena's reset state, so
     it carries that arena's Philox key) for 60 ticks: events every tick, states
-    and observations every 20."""
-    A, B = 8, 512
+    and observations every 20.  A = 40 (20,480 bots) puts more than 16,384 bots in
+    one observation launch, where k_observe switches to its streaming (non-temporal)
+    store variant (obs.hip kObsWtBots): that variant against the oracles too."""
+    B = 512
     ch, ex = _abi.OBS_PELLET | _abi.OBS_WALL | _abi.OBS_ENEMY, _abi.EX_FOV | _abi.EX_MASS
     g = _lib.Stepper(make_config(n_arenas=A, bots=B, field_size=1697, max_pellets=43200.0, channels=ch, extras=ex))
     g.reset(40)
@@ -119,7 +122,7 @@ def test_c5_gpu_slice_matches_eight_oracles():
         orcs.append(o)
     rng = np.random.default_rng(40)
     nev = 0
-    for t in range(60):
+    for t in range(ticks):
         cmd = parity.synthetic_commands(rng, None, A * B, 1697, 0.01, 0.02)
         g.set_commands(cmd)
         g.step(1)
@@ -129,13 +132,13 @@ def test_c5_gpu_slice_matches_eight_oracles():
             ev = o.events()
             assert np.array_equal(g.events(a), ev), "tick %d arena %d" % (t, a)
             nev += len(ev)
-        if t % 20 == 19:
+        if t % every == every - 1:
             obs = g.observe()
             for a, o in enumerate(orcs):
                 dif = parity.diff_states(g.get_state(a), o.get_state())
                 assert not dif, (t, a, dif[:3])
                 assert parity.obs_close(obs[a * B:(a + 1) * B], o.observe()), (t, a)
-    assert nev > 8 * 60 * 5
+    assert nev > A * ticks * 5
     g.close()
     for o in orcs:
         o.close()

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from aigar_amd import _abi
-from oracle_lib import make_config
+from oracle_lib import Oracle, make_config
 import parity
 
 pytestmark = pytest.mark.gpu
@@ -149,3 +149,53 @@ def test_greedy_run_at_c3_matches_separate_calls():
     assert fused.counters()["ticks"] == sep.counters()["ticks"]
     fused.close()
     sep.close()
+
+
+def _commands(stp):
+    st = stp.get_state()
+    pf, pi = np.asarray(st["players_f"]), np.asarray(st["players_i"])
+    return np.c_[pf[:, 0], pf[:, 1], pi[:, 2], pi[:, 3]].astype(np.float64)
+
+
+def test_bench_graph_matches_oracle():
+    """bench.py's timed path itself -- the C3 workload's config
+    (events off, as timed), data/c3_t50.npz loaded by bench.start_world, the aigar_run
+    graph with the random policy fused into k_tick_begin and the bench's own split /
+    eject probabilities and salt -- against the oracle for 25 steps.  The commands
+    the fused policy made are read back after every replay and given to the oracle;
+    the world and every bot's observation row are compared every step.  A second
+    stepper replays the same graph 25 times in ONE call (as the timed region does)
+    and must end identical."""
+    import bench
+    _, _, _, _, ps, pe, _, _, _ = bench.WORKLOADS["c3"]
+    salt = 1234  # bench.py --seed default, rank 0
+    cfg = bench.make_cfg("c3")
+    stp, one = _lib.Stepper(cfg), _lib.Stepper(cfg)
+    for s in (stp, one):
+        s.set_stream(torch.cuda.current_stream().cuda_stream)
+        bench.start_world(s, "c3", salt, 1)
+    o = Oracle(cfg)
+    o.load_state(parity.load_snapshot("c3_t50"))
+    assert parity.diff_states(stp.get_state(), o.get_state(), ftol=0.0) == []
+    obs = torch.full((stp.NP, stp.obs_len), -7.0, dtype=torch.float64, device="cuda")
+    splits = ejects = 0
+    for t in range(25):
+        stp.run(1, "random", obs, p_split=ps, p_eject=pe, seed=salt, greedy_split=True)
+        torch.cuda.synchronize()
+        cmd = _commands(stp)
+        splits += int(cmd[:, 2].sum())
+        ejects += int(cmd[:, 3].sum())
+        o.set_commands(cmd)
+        o.step(1)
+        want = o.observe()
+        dif = parity.diff_states(stp.get_state(), o.get_state())
+        assert not dif, "step %d: %s" % (t, dif[:3])
+        assert parity.obs_close(obs.cpu().numpy(), want), "step %d: observation rows differ" % t
+    assert splits > 0 and ejects > 0, (splits, ejects)
+    obs1 = torch.full_like(obs, -7.0)
+    one.run(25, "random", obs1, p_split=ps, p_eject=pe, seed=salt, greedy_split=True)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(obs1, nan=-7.0), torch.nan_to_num(obs, nan=-7.0))
+    assert parity.diff_states(one.get_state(), stp.get_state(), ftol=0.0) == []
+    for s in (stp, one, o):
+        s.close()

@@ -12,7 +12,8 @@ from aigar_amd import _abi
 from oracle_lib import Oracle, golden_state, lib, make_config
 
 # (fixture, numpy seed of the scenario, ENABLE_GREEDY_SPLIT) -- tools/golden/gen_golden.py SCENARIOS
-GREEDY = [("c1_greedy", 0, False), ("greedy16", 1, False), ("greedy16_virus_split", 2, True)]
+GREEDY = [("c1_greedy", 0, False), ("greedy16", 1, False), ("greedy16_virus_split", 2, True),
+          ("c2_greedy256", 11, False)]  # (BASELINE.json configs[1]: 256 Greedy bots, 10k pellets)
 
 
 def split_likelihoods(seed, n):

@@ -27,6 +27,7 @@ import math
 import os
 import random
 import sys
+import time
 import tracemalloc
 import types
 
@@ -316,6 +317,24 @@ SCENARIOS = {
                   ck_every=30, obs=True, seed=10,
                   obs_over=dict(CNN_REPR=True, CNN_P_REPR=False, CNN_USE_L1=False, CNN_USE_L2=True),
                   obs_kind="cnn"),
+    # BASELINE.json configs[1] (C2): 256 reference Greedy bots, default field 75*sqrt(256) = 1200,
+    # 10,000 pellets, every bot's observation at every checkpoint
+    "c2_greedy256": dict(n=256, driver="greedy", max_pellets=10000, virus=False, split=False, eject=False,
+                         ticks=150, ck_every=50, obs=True, seed=11),
+    # BASELINE.json configs[2] (C3, the headline world): 4096 bots, field 4800, 100k pellets, 1152 viruses,
+    # split + eject on, started from the bench's own matured world (data/c3_t50.npz, loaded into the
+    # reference object by object) and driven like bench.py's synthetic policy: a uniform point of the
+    # bot's FOV through the reference's own Bot.set_command_point (bot.py:550-577), split p = 2.5e-3,
+    # eject p = 1e-2 per bot-tick.  Every bot is observed every tick (its last-frame
+    # grids evolve as in the device / oracle runs); the full 854-value rows are kept at the last tick.
+    "c3_4096": dict(n=4096, driver="bench", load="data/c3_t50.npz", virus=True, split=True, eject=True,
+                    p_split=2.5e-3, p_eject=1e-2, ticks=4, ck_every=4, obs=True, obs_init_stored=False, seed=12),
+    # the same world size from the late matured world (data/c3_t600.npz: 6233 cells, 580 past mass 125,
+    # 673 multi-cell players) with more splits and ejections, so that the headline size also pins
+    # splits, ejected blobs, virus eating and explosions
+    "c3_4096_t600": dict(n=4096, driver="bench", load="data/c3_t600.npz", virus=True, split=True, eject=True,
+                         p_split=0.03, p_eject=0.05, ticks=4, ck_every=4, obs=True, obs_init_stored=False,
+                         seed=13),
 }
 OBS_SIMPLE = 0x400  # include/aigar.h AIGAR_OBS_SIMPLE
 
@@ -346,6 +365,103 @@ def feed_commands(field, rng, tick):
     return cmds
 
 
+def bench_commands(field, bots, rng, sc):
+    """bench.py's synthetic policy restated over the reference's own objects: an action drawn
+    uniformly in [0,1]^2 mapped through Bot.set_command_point (bot.py:550-577), split / eject with
+    p_split / p_eject.  Dead players keep their command point (they have no FOV position)."""
+    for b in bots:
+        a0, a1 = rng.random(), rng.random()
+        s = 1.0 if rng.random() < sc["p_split"] else 0.0
+        e = 1.0 if rng.random() < sc["p_eject"] else 0.0
+        if b.player.getIsAlive():
+            b.set_command_point([a0, a1, s, e])
+
+
+def load_world(ref, rec, model, path):
+    """Load a world written by tools/mature.py (the oracle's get_state layout) into the reference's
+    objects, reproducing what a reference run that reached this state would hold:
+      * `Field` sizes, counts and the four hashes (`field.py:57-66`): pellets and blobs hashed at
+        their positions, player cells and viruses as the snapshot's `hashed` flag says (respawned
+        cells and new viruses are not hashed until the next `updateHashTables`, `field.py:121-132`);
+      * cells in each player's list order with every field the tick reads, the stored (possibly
+        stale, `cell.py:90-94`) radius kept as is; the dead-player list in its order;
+      * the creation sequence continues at `seq_next`.
+    Cells are constructed before numpy is reseeded (a cell without a player draws its colour)."""
+    z = np.load(path)
+    field = model.field
+    Cell = ref.cell.Cell
+    SHT = ref.sht.spatialHashTable
+    size = int(z["field_size"])
+    field.size = size
+    bucket = ref.field.HASH_BUCKET_SIZE
+    field.pelletHashTable = SHT(size, bucket)
+    field.blobHashTable = SHT(size, bucket)
+    field.playerHashTable = SHT(size, bucket)
+    field.virusHashTable = SHT(size, bucket)
+    field.maxCollectibleCount = float(z["max_pellets"])
+    field.maxVirusCount = float(z["max_viruses"])
+    players = field.players
+    pf, pi = z["players_f"], z["players_i"]
+    assert len(players) == len(pf)
+    for i, p in enumerate(players):
+        p.commandPoint = [float(pf[i, 0]), float(pf[i, 1])]
+        p.isAlive = bool(pi[i, 0])
+        p.respawnTime = int(pi[i, 1])
+        p.doSplit = bool(pi[i, 2])
+        p.doEject = bool(pi[i, 3])
+        p.cells = []
+
+    def fill(c, row_f, counter, seq):
+        c.radius = float(row_f[3])
+        c.velocity = [float(row_f[4]), float(row_f[5])]
+        c.splitVelocity = [float(row_f[6]), float(row_f[7])]
+        c.splitVelocityCounter = int(counter)
+        c._seq = int(seq)
+
+    by_seq = {}
+    cf, ci = z["cells_f"], z["cells_i"]
+    for k in range(len(cf)):
+        p = players[int(ci[k, 0])]
+        c = Cell(float(cf[k, 0]), float(cf[k, 1]), float(cf[k, 2]), p)
+        fill(c, cf[k], ci[k, 1], ci[k, 2])
+        c.mergeTime = float(cf[k, 8])
+        p.cells.append(c)
+        by_seq[c._seq] = c
+        if ci[k, 3]:
+            field.playerHashTable.insertObject(c)
+    for k in range(len(pi)):
+        assert len(players[k].cells) == int(pi[k, 4])
+    vf, vi = z["viruses_f"], z["viruses_i"]
+    field.viruses = []
+    for k in range(len(vf)):
+        v = Cell(float(vf[k, 0]), float(vf[k, 1]), float(vf[k, 2]), None)
+        v.setName("Virus")
+        fill(v, vf[k], vi[k, 0], vi[k, 1])
+        field.viruses.append(v)
+        if vi[k, 2]:
+            field.virusHashTable.insertObject(v)
+    bf, bi = z["blobs_f"], z["blobs_i"]
+    field.blobs = []
+    for k in range(len(bf)):
+        b = Cell(float(bf[k, 0]), float(bf[k, 1]), float(bf[k, 2]), None)
+        fill(b, bf[k], bi[k, 0], bi[k, 1])
+        b.ejecterCell = by_seq.get(int(bi[k, 2]))
+        field.blobs.append(b)
+        field.blobHashTable.insertObject(b)
+    plf, pls = z["pellets_f"], z["pellets_seq"]
+    field.pellets = []
+    for k in np.argsort(pls, kind="stable"):
+        c = Cell(float(plf[k, 0]), float(plf[k, 1]), float(plf[k, 2]), None)
+        c.setName("Pellet")
+        c.radius = float(plf[k, 3])
+        c._seq = int(pls[k])
+        field.pellets.append(c)
+        field.pelletHashTable.insertObject(c)
+    field.deadPlayers = [players[int(d)] for d in z["dead"]]
+    rec.seq = int(z["seq_next"])
+    return field
+
+
 def run_scenario(ref, rec, name, sc):
     n = sc["n"]
     mf = ref.field
@@ -372,7 +488,12 @@ def run_scenario(ref, rec, name, sc):
     else:
         for i in range(n):
             model.createPlayer("P%d" % i)
-    model.initialize()
+    if sc.get("load"):
+        field = load_world(ref, rec, model, os.path.join(os.path.dirname(__file__), "..", "..", sc["load"]))
+        np.random.seed(sc["seed"])  # the loader's colour draws are not part of the run
+        model.resetBots()
+    else:
+        model.initialize()
     field = model.field
     rng = np.random.default_rng(1000 + sc["seed"])  # scenario driver RNG (not the field's MT stream)
 
@@ -439,10 +560,14 @@ def run_scenario(ref, rec, name, sc):
         return arr
 
     if obs_bots:
-        out["obs/init"] = record_obs("init")
+        obs0 = record_obs("init")  # (also advances the bots' last-frame grids, as the test's first observe)
+        if sc.get("obs_init_stored", True):
+            out["obs/init"] = obs0
     for t in range(T):
         if driver in ("greedy", "random"):
             model.takeBotActions()
+        elif driver == "bench":
+            bench_commands(field, obs_bots, rng, sc)
         else:
             cmds = scripted_commands(field, rng, sc) if driver == "scripted" else feed_commands(field, rng, t)
             for p, (x, y, s, e) in zip(field.players, cmds):
@@ -533,9 +658,13 @@ def main():
     for name, sc in SCENARIOS.items():
         if args.only not in (None, name):
             continue
+        if args.only is None and sc.get("load"):
+            continue  # the BASELINE-size worlds take minutes: generate them with --only NAME
+        t0 = time.time()
         out, counts = run_scenario(ref, rec, name, sc)
         np.savez_compressed(os.path.join(args.out, name + ".npz"), **out)
-        print(name, "events:", counts, "final counts:", out["digest_i"][-1].tolist(), flush=True)
+        print(name, "events:", counts, "final counts:", out["digest_i"][-1].tolist(), "%.0f s" % (time.time() - t0),
+              flush=True)
 
 
 if __name__ == "__main__":
