@@ -111,6 +111,8 @@ def load(build_if_missing=False):
         "aigar_tile_set_buffers": [vp, vp, vp],
         "aigar_tile_msg_bytes": [vp, C.POINTER(C.c_int64)],
         "aigar_tile_begin": [vp, C.POINTER(_abi.RunParams)],
+        "aigar_tile_policy": [vp, i32],
+        "aigar_tile_apply_commands": [vp],
         "aigar_tile_apply": [vp, C.POINTER(i32)],
         "aigar_tile_resume": [vp],
         "aigar_tile_end": [vp, vp, i32],
@@ -402,9 +404,20 @@ class Stepper:
         self._chk(self.L.aigar_tile_set_buffers(self.h, C.c_void_p(int(outbox_ptr)), C.c_void_p(int(inbox_ptr))))
 
     def tile_begin(self, policy="none", p_split=0.0, p_eject=0.0, seed=0):
-        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM}[policy]
+        """policy "greedy": this tick's commands must have gone round already
+        (tile_policy, the exchange, tile_apply_commands)."""
+        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM, "greedy": _abi.POLICY_GREEDY}[policy]
         prm = _abi.RunParams(pol, 0, float(p_split), float(p_eject), int(seed))
         self._chk(self.L.aigar_tile_begin(self.h, C.byref(prm)))
+
+    def tile_policy(self, greedy_split=False):
+        """Greedy moves (bot.py:579-633) of the bots this tile observes, into the
+        command message the transport all-gathers next."""
+        self._chk(self.L.aigar_tile_policy(self.h, 1 if greedy_split else 0))
+
+    def tile_apply_commands(self):
+        """The other tiles' Greedy commands (after the exchange of tile_policy's messages)."""
+        self._chk(self.L.aigar_tile_apply_commands(self.h))
 
     def tile_apply(self, wait=True):
         """Apply the gathered messages; wait: return the owned cells still undone on
@@ -431,11 +444,13 @@ class Stepper:
         buf = C.create_string_buffer(bytes(uid), 128)
         self._chk(self.L.aigar_tile_comm_init(self.h, path.encode() if path else None, buf, int(nranks), int(rank)))
 
-    def tile_run(self, n=1, policy="random", out=None, p_split=0.0, p_eject=0.0, seed=0, extra_passes=0):
-        """n tiled steps over RCCL (aigar_tile_run): policy + the tick with its all-gathered
-        eat passes + the observation of this tile's bots into the DEVICE tensor out."""
-        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM}[policy]
-        prm = _abi.RunParams(pol, 0, float(p_split), float(p_eject), int(seed))
+    def tile_run(self, n=1, policy="random", out=None, p_split=0.0, p_eject=0.0, seed=0, extra_passes=0,
+                 greedy_split=False):
+        """n tiled steps over RCCL (aigar_tile_run): policy (greedy: each tile moves the bots
+        it observes, the commands all-gathered first) + the tick with its all-gathered eat
+        passes + the observation of this tile's bots into the DEVICE tensor out."""
+        pol = {"none": _abi.POLICY_NONE, "random": _abi.POLICY_RANDOM, "greedy": _abi.POLICY_GREEDY}[policy]
+        prm = _abi.RunParams(pol, 1 if greedy_split else 0, float(p_split), float(p_eject), int(seed))
         p, dt = None, 0
         if out is not None:
             if not getattr(out, "is_cuda", False) or tuple(out.shape) != (self.NP, self.obs_len):

@@ -84,6 +84,7 @@ struct ArenaCtl {
   int n_pel_glob, n_eaten_glob, n_out, n_out_pel, n_undone, n_undone_glob;
   int n_ho;       // observation history hand-off slots in this tile's first-pass message (dead bots first)
   int n_ho_live;  // live bots whose view centre left this tile: hand-off candidates (t_holive)
+  int n_cmd;      // Greedy commands in this tile's command message (aigar_tile_policy)
   // diagnostics, accumulated since reset (aigar_counters): serial work-list sizes of
   // virus<-blob, cell<-virus, pellet, blob, player<-player; then ticks seen
   int64_t stat[8];
@@ -122,7 +123,7 @@ struct TileRec {
   int64_t seq;        // pellet creation sequence / (header) undone owned cells
   double x, y;        // pellet position / cell mass, radius / lastFovSize / (header) pellet kills, hand-off slots
 };
-enum : int32_t { TR_HDR = 0, TR_PELLET = 1, TR_BLOB = 2, TR_CELL = 3, TR_HIST = 4 };
+enum : int32_t { TR_HDR = 0, TR_PELLET = 1, TR_BLOB = 2, TR_CELL = 3, TR_HIST = 4, TR_CMD = 5 };
 constexpr int kHcapMax = 256;  // hand-off slots per message (LDS list of the plan kernel)
 
 // a pellet (field.py:303-313, 107-110): position, mass and creation sequence

@@ -21,6 +21,8 @@ void launch_tick(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *s
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp);
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v);
 void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first);
+void launch_tile_policy(const Dev &d, hipStream_t s, int greedy_split, uint8_t *mask, int cap);
+void launch_tile_cmd_apply(const Dev &d, hipStream_t s, int box_recs);
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch,
@@ -96,8 +98,14 @@ struct aigar_handle {
   hipStream_t stream = nullptr;
   bool own_stream = true;
   uint32_t obs_calls = 0;
-  int rounds = 2;  // reservation rounds before the serial fallback; empty rounds exit at once
-                   // (tools/micro/exp_rounds.sh, greedy_rounds.sh)
+  // reservation rounds of the eat phase before the serial fallback (food_rounds):
+  // 0 = by population -- 1 until the handle's Greedy policy ran, then 2 (Greedy
+  // bots crowd the same pellets: 18 cells per C3 tick failed a single round and
+  // took the serial pass, 0.9 with two rounds, profiles/r05_v2g_*); an empty
+  // round exits at once but costs a dependent launch
+  int rounds = 0;
+  bool greedy_seen = false;
+  int graph_rounds = 0;  // the rounds the step graph was captured with
   int64_t *scr_k = nullptr;
   int *scr_v = nullptr;
   double *d_cmd = nullptr, *d_stats = nullptr;
@@ -143,6 +151,7 @@ struct aigar_handle {
   int rccl_ranks = 0;
   bool rccl_bad = false;  // an all-gather failed while a graph was captured
   bool loopback = false;  // timing rehearsal: the exchange copies this tile's message to its own slot only
+  bool cmd_ready = false;  // this tick's Greedy commands were exchanged and applied (aigar_tile_apply_commands)
   hipGraphExec_t tr_graph = nullptr;
   aigar_run_params tr_key{};
   void *tr_out = nullptr;
@@ -283,8 +292,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
   if (getenv("AIGAR_TILE_GRAPH")) h->tile_graph = true;
   h->d.pp_par = getenv("AIGAR_PP_SERIAL") ? 0 : 1;
-  // tuning knob; >= 2: the player-cell grid counts ride on round 1, its scatter on round 2
-  if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(2, std::min(16, atoi(r)));
+  // tuning knob: a fixed number of reservation rounds for every population
+  if (const char *r = getenv("AIGAR_FOOD_ROUNDS")) h->rounds = std::max(1, std::min(16, atoi(r)));
   Dev &d = h->d;
   d.A = cfg->n_arenas;
   d.B = cfg->bots_per_arena;
@@ -601,21 +610,29 @@ __global__ void k_step_begin(Dev d) {
   if (a < d.A) d.ctl[a].n_ev = 0;
 }
 
+static int food_rounds(const aigar_handle *h) { return h->rounds > 0 ? h->rounds : (h->greedy_seen ? 2 : 1); }
+
 extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
   if (!h) return fail("null handle");
   if (n_ticks < 0) return fail("n_ticks < 0");
   HIPCHK(hipSetDevice(h->cfg.device));
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every step
     hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  const int rounds = food_rounds(h);
+  if (h->graph && h->graph_rounds != rounds) {  // (the population changed the eat phase's rounds)
+    (void)hipGraphExecDestroy(h->graph);
+    h->graph = nullptr;
+  }
   if (h->use_graph && !h->graph && !h->graph_failed && n_ticks > 0) {
     // capture one Field.update() (~25 kernel launches) once; replay it per tick
-    h->graph = capture_graph(h, [&](hipStream_t cs) { launch_tick(h->d, cs, h->rounds, h->scr_k, h->scr_v); });
+    h->graph = capture_graph(h, [&](hipStream_t cs) { launch_tick(h->d, cs, rounds, h->scr_k, h->scr_v); });
     if (!h->graph) h->graph_failed = true;
+    h->graph_rounds = rounds;
   }
   for (int t = 0; t < n_ticks; t++) {
     Mark m(h, "tick");
     if (h->graph) HIPCHK(hipGraphLaunch(h->graph, h->stream));
-    else launch_tick(h->d, h->stream, h->rounds, h->scr_k, h->scr_v);
+    else launch_tick(h->d, h->stream, rounds, h->scr_k, h->scr_v);
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -634,7 +651,7 @@ static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_para
   const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
 #endif
   if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr, -1);
-  launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v, &rp);
+  launch_tick(h->d, s, food_rounds(h), h->scr_k, h->scr_v, &rp);
   if (out) launch_observe(h->d, s, out, dtype, 0);  // epoch 0: the device-side epoch
 }
 
@@ -646,6 +663,7 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
   HIPCHK(hipSetDevice(h->cfg.device));
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every call (all n_steps accumulate)
     hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
+  if (p->policy == AIGAR_POLICY_GREEDY) h->greedy_seen = true;  // (food_rounds)
   const bool same = h->run_graph && memcmp(&h->run_key, p, sizeof *p) == 0 && h->run_out == obs_out &&
                     h->run_dtype == (obs_out ? dtype : -1);
   if (h->use_graph && !same && n_steps > 0) {
@@ -698,17 +716,46 @@ extern "C" int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox
   h->d.inbox = (const TileRec *)inbox;
   return 0;
 }
+// Greedy bots on tiles: each tile moves the bots it observes, the commands go
+// round in their own message (k_tile_cmd_collect / k_tile_cmd_apply, tick.hip)
+extern "C" int aigar_tile_policy(aigar_handle *h, int greedy_split) {
+  if (need_tiled(h)) return -1;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  h->greedy_seen = true;  // (food_rounds)
+  {
+    Mark m(h, "policy");
+    launch_tile_policy(h->d, h->stream, greedy_split ? 1 : 0, h->d_mask, h->box_recs - 1);
+  }
+  h->pass_recs = h->box_recs;  // (the command message: the whole buffer is exchanged)
+  h->cmd_ready = false;
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+extern "C" int aigar_tile_apply_commands(aigar_handle *h) {
+  if (need_tiled(h)) return -1;
+  if (h->pass_recs != h->box_recs) return fail("tile_apply_commands: no aigar_tile_policy before it");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  launch_tile_cmd_apply(h->d, h->stream, h->box_recs);
+  HIPCHK(hipGetLastError());
+  h->pass_recs = 0;
+  h->cmd_ready = true;
+  return 0;
+}
 extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
   if (need_tiled(h) || !p) return p ? -1 : fail("null argument");
-  if (p->policy != AIGAR_POLICY_NONE && p->policy != AIGAR_POLICY_RANDOM)
-    return fail("tile_begin: policy must be NONE or RANDOM (the greedy policy reads pellets other tiles hold)");
+  if (p->policy == AIGAR_POLICY_GREEDY && !h->cmd_ready)
+    return fail("tile_begin: GREEDY needs this tick's commands (aigar_tile_policy, all-gather, "
+                "aigar_tile_apply_commands): no tile holds every pellet a Greedy move reads");
+  if (p->policy != AIGAR_POLICY_NONE && p->policy != AIGAR_POLICY_RANDOM && p->policy != AIGAR_POLICY_GREEDY)
+    return fail("tile_begin: unknown policy %d", p->policy);
+  h->cmd_ready = false;
   HIPCHK(hipSetDevice(h->cfg.device));
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log holds this tick
     hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, h->stream, h->d);
-  const RandomPolicy rp{p->policy == AIGAR_POLICY_RANDOM, p->p_split, p->p_eject, p->seed};
+  const RandomPolicy rp{p->policy == AIGAR_POLICY_RANDOM, p->p_split, p->p_eject, p->seed};  // (GREEDY: set already)
   auto issue = [&](hipStream_t s) {
     launch_tick_pre(h->d, s, h->scr_k, h->scr_v, &rp);
-    launch_tile_pass(h->d, s, h->rounds, h->scr_k, h->scr_v, 1);
+    launch_tile_pass(h->d, s, food_rounds(h), h->scr_k, h->scr_v, 1);
   };
   const bool same = h->tb_graph && memcmp(&h->tb_key, p, sizeof *p) == 0 && h->tb_box[0] == h->d.outbox &&
                     h->tb_box[1] == h->d.inbox;
@@ -750,7 +797,7 @@ extern "C" int aigar_tile_resume(aigar_handle *h) {
   if (need_tiled(h)) return -1;
   HIPCHK(hipSetDevice(h->cfg.device));
   Mark m(h, "tile_resume");
-  launch_tile_pass(h->d, h->stream, h->rounds, h->scr_k, h->scr_v, 0);
+  launch_tile_pass(h->d, h->stream, food_rounds(h), h->scr_k, h->scr_v, 0);
   h->pass_recs = 1 + h->d.tcap + h->d.bm_words / 4;
   h->first_pass = 0;
   HIPCHK(hipGetLastError());
@@ -897,10 +944,16 @@ static int issue_tile_step(aigar_handle *h, hipStream_t s, const aigar_run_param
                            int dtype) {
   const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
   const int first_recs = 1 + h->d.tcap + h->d.hcap * h->d.hrec, later_recs = 1 + h->d.tcap + h->d.bm_words / 4;
+  if (p.policy == AIGAR_POLICY_GREEDY) {  // each tile moves the bots it observes; the commands go round first
+    Mark m(h, "policy");
+    launch_tile_policy(h->d, s, p.greedy_split ? 1 : 0, h->d_mask, h->box_recs - 1);
+    if (tile_allgather(h, s, h->box_recs)) return -1;
+    launch_tile_cmd_apply(h->d, s, h->box_recs);
+  }
   {
     Mark m(h, "tile_begin");
     launch_tick_pre(h->d, s, h->scr_k, h->scr_v, &rp);
-    launch_tile_pass(h->d, s, h->rounds, h->scr_k, h->scr_v, 1);
+    launch_tile_pass(h->d, s, food_rounds(h), h->scr_k, h->scr_v, 1);
   }
   for (int k = 0; k <= extra; k++) {
     {
@@ -913,7 +966,7 @@ static int issue_tile_step(aigar_handle *h, hipStream_t s, const aigar_run_param
     }
     if (k < extra) {
       Mark m(h, "tile_resume");
-      launch_tile_pass(h->d, s, h->rounds, h->scr_k, h->scr_v, 0);
+      launch_tile_pass(h->d, s, food_rounds(h), h->scr_k, h->scr_v, 0);
     }
   }
   {
@@ -932,8 +985,8 @@ extern "C" int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_para
   if (need_tiled(h) || !p) return p ? -1 : fail("null argument");
   if (!h->rccl_comm && !h->loopback) return fail("tile_run: no RCCL communicator (aigar_tile_comm_init)");
   if (n_steps < 0 || extra_passes < 0 || extra_passes > 64) return fail("tile_run: bad n_steps / extra_passes");
-  if (p->policy != AIGAR_POLICY_NONE && p->policy != AIGAR_POLICY_RANDOM)
-    return fail("tile_run: policy must be NONE or RANDOM (the greedy policy reads pellets other tiles hold)");
+  if (p->policy < AIGAR_POLICY_NONE || p->policy > AIGAR_POLICY_GREEDY) return fail("tile_run: unknown policy %d", p->policy);
+  if (p->policy == AIGAR_POLICY_GREEDY) h->greedy_seen = true;  // (food_rounds)
   if (obs_out && dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
   HIPCHK(hipSetDevice(h->cfg.device));
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every call (all n_steps accumulate)
@@ -1007,7 +1060,7 @@ static void launch_env_decision(aigar_handle *h, hipStream_t s, const aigar_hand
     if (k.n_greedy) launch_policy_greedy(h->d, s, k.envp.greedy_split, h->d.p_role, AIGAR_ROLE_GREEDY);
     if (k.n_random)
       launch_policy_refrandom(h->d, s, k.envp.random_skip, k.envp.random_split, k.envp.random_eject, k.envp.salt);
-    launch_tick(h->d, s, h->rounds, h->scr_k, h->scr_v);
+    launch_tick(h->d, s, food_rounds(h), h->scr_k, h->scr_v);
   }
   launch_rewards(h->d, s, k.reward, k.prm, 1, k.skip == 0 ? 1 : 2);  // end of move_NN (bot.py:220-230)
   launch_observe(h->d, s, k.obs, k.dtype, 0, (k.n_greedy || k.n_random) ? h->d_nnmask : nullptr);
@@ -1072,6 +1125,7 @@ extern "C" int aigar_set_roles(aigar_handle *h, const uint8_t *roles, int on_dev
   HIPCHK(hipStreamSynchronize(h->stream));
   h->n_greedy = ng;
   h->n_random = nr;
+  if (ng) h->greedy_seen = true;  // (food_rounds)
   return 0;
 }
 extern "C" int aigar_env_config(aigar_handle *h, const aigar_env_params *p) {
@@ -1640,6 +1694,7 @@ extern "C" int aigar_policy_greedy(aigar_handle *h, int greedy_split, const uint
     HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)h->d.NP, hipMemcpyHostToDevice, h->stream));
     m = h->d_mask;
   }
+  h->greedy_seen = true;  // (food_rounds)
   {
     Mark mk(h, "policy");
     launch_policy_greedy(h->d, h->stream, greedy_split ? 1 : 0, m, -1);

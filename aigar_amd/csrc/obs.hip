@@ -44,6 +44,9 @@ __device__ unsigned long long g_obs_ts[65536 * OBS_TS];
 
 // x / y index masks of the reference's float-hash insertion loops
 __device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, double inv_gs, double lim) {
+#ifdef AIGAR_OBS_DIAG_NOMASK  // (cost diagnostics only, results invalid)
+  return p > r ? 2u : 1u;
+#endif
   double cl = py_max(0.0, p - r);
   double bl = cl - aigar_math::mod_pos(cl, gs, inv_gs);  // (cl >= 0, gs > 0)
   double lx = py_min(lim, p + r);
@@ -85,6 +88,10 @@ struct Cand {
 
 // wave-wide append (ballot + prefix count); count is wave-uniform and keeps the true total
 __device__ __forceinline__ void list_append(const Cand &c, ObjList &L, int cap, int &count) {
+#ifdef AIGAR_OBS_DIAG_NOAPPEND  // (cost diagnostics only, results invalid)
+  count += c.keep ? 1 : 0;
+  return;
+#endif
   unsigned long long bal = __ballot(c.keep);
   int slot = count + __popcll(bal & ((1ull << __lane_id()) - 1));
   if (c.keep && slot < cap) {
@@ -271,16 +278,24 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // 2.66 -> 1.85 TB/s).
 #ifdef AIGAR_OBS_DIAG_NOSTORE  // (cost diagnostics only, results invalid: one store per lane at the end)
   double diag_sum = 0;
-  auto hist_st = [&](double *p, double v) __attribute__((always_inline)) { diag_sum += v; };
-  auto row_st = [&](int i, OutT v) __attribute__((always_inline)) { diag_sum += (double)v; };
+  auto hist_st = [&](double *p, unsigned t, double v) __attribute__((always_inline)) { diag_sum += v; };
+  auto row_st = [&](int o, unsigned t, OutT v) __attribute__((always_inline)) { diag_sum += (double)v; };
 #else
-  auto hist_st = [](double *p, double v) __attribute__((always_inline)) {
-    if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
+  // element t of a wave-uniform base (the base in SGPRs, the lane's byte offset a
+  // 32-bit VGPR: the store's saddr form, no 64-bit address arithmetic per store)
+  auto at = [](auto *base, unsigned t) __attribute__((always_inline)) {
+    using E = std::remove_pointer_t<decltype(base)>;
+    return reinterpret_cast<E *>(reinterpret_cast<char *>(base) + t * (unsigned)sizeof(E));
   };
-  auto row_st = [&](int i, OutT v) __attribute__((always_inline)) {
-    if constexpr (WT) __hip_atomic_store(row + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __builtin_nontemporal_store(v, row + i);
+  auto hist_st = [&](double *base, unsigned t, double v) __attribute__((always_inline)) {
+    if constexpr (WT) __hip_atomic_store(at(base, t), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *at(base, t) = v;
+  };
+  auto row_st = [&](int o, unsigned t, OutT v) __attribute__((always_inline)) {
+    OutT *const p = reinterpret_cast<OutT *>(reinterpret_cast<char *>(row) + (unsigned)o * (unsigned)sizeof(OutT) +
+                                              t * (unsigned)sizeof(OutT));
+    if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __builtin_nontemporal_store(v, p);
   };
 #endif
   // one round of independent loads: liveness, the FOV cache written at the end
@@ -292,7 +307,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const ArenaCtl &ctl = d.ctl[a];
   const double rmax_c = ctl.rmax_cell, rmax_v = ctl.rmax_virus;  // (the walk's grid expansions)
   if (!alive) {  // getStateRepresentation returns None for dead players
-    for (int i = lane; i < L; i += 64) row_st(i, (OutT)__builtin_nan(""));
+    for (int i = lane; i < L; i += 64) row_st(0, i, (OutT)__builtin_nan(""));
     return;
   }
   if (d.tiled) {  // C4: one tile observes the bot -- its history holder, else its view centre's tile (tile_plan_thread)
@@ -409,7 +424,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   int np, nc, nv;
   OBS_STAMP(1);
 #if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 1  // per-phase cost variants (timing only, results invalid)
-  if (fx + fy + fs + left + ox + h_slf0 + h_elf0 == -1.2345) row_st(0, (OutT)0);
+  if (fx + fy + fs + left + ox + h_slf0 + h_elf0 == -1.2345) row_st(0, 0, (OutT)0);
   return;
 #endif
   {  // (lists known to be the LDS arrays here: ds_write appends)
@@ -420,7 +435,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   }
   OBS_STAMP(2);
 #if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 2
-  if (np + nc + nv == -12345 || h_slf0 + h_elf0 == -1.2345) row_st(0, (OutT)0);
+  if (np + nc + nv == -12345 || h_slf0 + h_elf0 == -1.2345) row_st(0, 0, (OutT)0);
   return;
 #endif
   ObjList PL{&p_sx[0].seq, p_m, nullptr, p_mask, nullptr, &p_px[0].perm};
@@ -518,7 +533,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   wave_fence();
   OBS_STAMP(3);
 #if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 3
-  if (np + nc + nv == -12345 || h_slf0 + h_elf0 == -1.2345 || (sm && sm[0] == -1.0)) row_st(0, (OutT)0);
+  if (np + nc + nv == -12345 || h_slf0 + h_elf0 == -1.2345 || (sm && sm[0] == -1.0)) row_st(0, 0, (OutT)0);
   return;
 #endif
 #ifdef AIGAR_OBS_TIMING
@@ -568,6 +583,11 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     q += ((q + 1) * n <= t) ? 1 : 0;
     return q;
   };
+  // t / n for 0 <= t < 512, 1 <= n <= 128: (t * ceil(2^16 / n)) >> 16 is exact
+  // (checked for every such pair) -- a 24-bit multiply and a shift
+  const bool small = GG <= 512 && G <= 127;  // (wave-uniform; cols <= G + 1)
+  const int Mg = (65536 + G - 1) / G, Mc = (65536 + cols - 1) / cols;
+  auto sdiv = [](int t, int M) { return (int)(((unsigned)t * (unsigned)M) >> 16); };
   // the whole-unit pellets' sums (pint): square t = iy * cols + ix of every
   // (column bit ix, row bit iy) of a pellet's mask -- the squares whose `need`
   // bits the mask holds -- inside the field and with ix < 16, as in the scan
@@ -584,7 +604,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
         for (uint32_t Y = mk >> 16; Y; Y &= Y - 1) {
           const int t = (__ffs(Y) - 1) * cols + ix;
           if (t >= GG) break;
-          const int c = idiv(t, G, inv_G), r = t - c * G;
+          const int c = sdiv(t, Mg), r = t - c * G;  // (GG <= 256 here)
           if ((in_col >> r) & (in_row >> c) & 1) atomicAdd(&s_pcnt[t], mi);
         }
       }
@@ -605,7 +625,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     // active set reads 0): lanes past the grid take the last square and store nothing
     const int t = min(t0 + lane, GG - 1);
     const bool act = t0 + lane < GG;
-    const int c = idiv(t, G, inv_G), r = t - c * G;
+    const int c = small ? sdiv(t, Mg) : idiv(t, G, inv_G), r = t - c * G;
     double mx, my, freeA = 0;
     if (G <= 64) {  // (wave-uniform)
       mx = __shfl(colx, r);
@@ -618,7 +638,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       for (int i = 0; i < c; i++) my += gs;
     }
     if (!act) continue;
-    const int iy = idiv(t, cols, inv_cols), ix = t - iy * cols;
+    const int iy = small ? sdiv(t, Mc) : idiv(t, cols, inv_cols), ix = t - iy * cols;
     uint32_t need = (1u << ix) | (1u << (16 + iy));
     double vp = 0, ve = 0, vs = 0, vv = 0;
     const bool within = G <= 64 ? ((in_col >> r) & (in_row >> c) & 1) != 0
@@ -696,12 +716,12 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     else if (fabs(dlt) < 0.0003 * gs2) vw = dlt > gs2 * 0x1p-53 ? -0.0 : 0.0;
     else vw = py_round3(1 - (freeA / gs2));
 #endif
-    if (o_pel >= 0) row_st(o_pel + t, held ? (OutT)vp : (OutT)__builtin_nan(""));
-    if (o_self >= 0) row_st(o_self + t, (OutT)vs);
-    if (o_wall >= 0) row_st(o_wall + t, (OutT)vw);
-    if (o_enemy >= 0) row_st(o_enemy + t, (OutT)ve);
-    if (o_all >= 0) row_st(o_all + t, (OutT)py_max(ve, vs));
-    if (o_vir >= 0) row_st(o_vir + t, (OutT)vv);
+    if (o_pel >= 0) row_st(o_pel, t, held ? (OutT)vp : (OutT)__builtin_nan(""));
+    if (o_self >= 0) row_st(o_self, t, (OutT)vs);
+    if (o_wall >= 0) row_st(o_wall, t, (OutT)vw);
+    if (o_enemy >= 0) row_st(o_enemy, t, (OutT)ve);
+    if (o_all >= 0) row_st(o_all, t, (OutT)py_max(ve, vs));
+    if (o_vir >= 0) row_st(o_vir, t, (OutT)vv);
     double o_sl, o_ss, o_el, o_es;  // history before this frame
     if constexpr (decltype(hist_regs)::value) {
       o_sl = t < 64 ? h_slf0 : h_slf1;
@@ -715,20 +735,20 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       o_es = o_eslf >= 0 ? eslf[t] : 0.0;
     }
     if (o_sslf >= 0) {
-      row_st(o_sslf + t, (OutT)o_ss);
-      hist_st(sslf + t, o_sl);
+      row_st(o_sslf, t, (OutT)o_ss);
+      hist_st(sslf, t, o_sl);
     }
     if (o_slf >= 0) {
-      row_st(o_slf + t, (OutT)o_sl);
-      hist_st(slf + t, vs);
+      row_st(o_slf, t, (OutT)o_sl);
+      hist_st(slf, t, vs);
     }
     if (o_eslf >= 0) {
-      row_st(o_eslf + t, (OutT)o_es);
-      hist_st(eslf + t, o_el);
+      row_st(o_eslf, t, (OutT)o_es);
+      hist_st(eslf, t, o_el);
     }
     if (o_elf >= 0) {
-      row_st(o_elf + t, (OutT)o_el);
-      hist_st(elf + t, ve);
+      row_st(o_elf, t, (OutT)o_el);
+      hist_st(elf, t, ve);
     }
   }
   };
@@ -749,8 +769,8 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       uint32_t nd0, nd1;
       {
         auto sq = [&](int t, bool &ok, uint32_t &need) {
-          const int c = idiv(t, G, inv_G), r = t - c * G;
-          const int iy = idiv(t, cols, inv_cols), ix = t - iy * cols;
+          const int c = sdiv(t, Mg), r = t - c * G;  // (GG <= 128 here)
+          const int iy = sdiv(t, Mc), ix = t - iy * cols;
           need = (1u << ix) | (1u << (16 + iy));
           ok = t < GG && ix < 16 && ((in_col >> r) & (in_row >> c) & 1) != 0;
         };
@@ -938,6 +958,8 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   bx = __shfl(bx, bl);
   by = __shfl(by, bl);
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
+  // C4 (aigar_tile_policy): the tile taking this bot's move must hold every pellet of its view
+  if (d.tiled && !tile_holds_rect(d, rect_grow(Q, 1, d.cols)) && lane == 0) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
   double best = -1;
   uint64_t bord = ~0ull;
   double tx = 0, ty = 0;

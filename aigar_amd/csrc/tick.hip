@@ -1134,57 +1134,34 @@ __device__ __forceinline__ int cgrid_bucket(const Dev &d, double x, double y) {
 __device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int parity) {
   return d.cgcnt + ((size_t)a * 2 + parity) * CG_STRIDE;
 }
-// block bodies, run as extra blocks of k_food_commit rounds 1 (counts) and 2
-// (scatter): eating changes masses and radii, never positions (a radius read
-// while its cell eats still bounds the grid: the eating cell reports its grown
-// radius itself), and the player-cell grid is first read by playerPlayerOverlap
-__device__ __forceinline__ int cgrid_blocks(const Dev &d) {  // per arena, count and scatter alike
-  const int cc = cgrid_cols(d);
-  return (int)((std::max((long)kMaxCells * d.B, (long)cc * cc + 1) + 255) / 256);
+// The player-cell grid is built in three steps, none of them a launch of its own:
+//  1. counts: every live cell takes an atomic rank in its coarse bucket where its
+//     position and list are final -- mergePlayerCells' / the virus test's player
+//     threads of k_merge_pv (k_merge_vb), explosion children in its serial pass
+//     (cgrid_count_cell); the grid's radius bound is maxed there too;
+//  2. scan: one extra block per arena at the head of k_food_prep turns the
+//     counts into the bucket starts (cgrid_scan_block) and zeroes them for the
+//     next tick;
+//  3. placement: each player's thread of k_food_commit round 1 writes its cells'
+//     items (start of the bucket + rank).
+// Eating changes masses and radii, never positions (a cell that eats reports its
+// grown radius itself), and the grid is first read by playerPlayerOverlap.
+// (Until round 5 the counts were extra blocks of commit round 1 and the scatter
+// extra blocks of round 2, which made a second commit launch necessary.)
+// c_rank holds (bucket << 17) | rank: bucket < SG_CAP + 1 <= 2^13, rank < 16 * B <= 2^17
+__device__ __forceinline__ void cgrid_count_cell(const Dev &d, int a, size_t ci, double x, double y) {
+  const int per = kMaxCells * d.B, slot = (int)(ci / d.NP), p = (int)(ci - (size_t)slot * d.NP) - a * d.B;
+  const int b = cgrid_bucket(d, x, y);
+  d.c_rank[(size_t)a * per + (size_t)slot * d.B + p] = (b << 17) | atomicAdd(&cgrid_counts(d, a, 0)[b], 1);
 }
-__device__ void cgrid_count_block(const Dev &d, int a, int bx) {
-  const int i = bx * 256 + threadIdx.x, per = kMaxCells * d.B;
-  const int cc = cgrid_cols(d), par = d.ctl[a].tick & 1;
-  if (i <= cc * cc) cgrid_counts(d, a, par ^ 1)[i] = 0;  // next tick's counts
-  const bool in = i < per;
-  const int slot = in ? i / d.B : 0, p = in ? i - slot * d.B : 0;
-  const size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-  // (the slot's position and radius load beside its flags: one round of loads)
-  double x = 0, y = 0, r = 0;
-  uint32_t fl = 0;
-  if (in) {
-    fl = d.c_flags[g];
-    x = d.c_x[g];
-    y = d.c_y[g];
-    r = d.c_r[g];
-  }
-  const bool ok = in && (fl & F_ALIVE);
-  wave_atomic_max_pos(&d.ctl[a].rmax_cell, ok ? r : 0.0);
-  if (!ok) return;
-  d.c_rank[(size_t)a * per + i] = atomicAdd(&cgrid_counts(d, a, par)[cgrid_bucket(d, x, y)], 1);
-}
-__device__ void cgrid_scatter_block(const Dev &d, int a, int bx) {
-  __shared__ int sc[CG_STRIDE];
+// one block per arena: bucket starts from the counts (exclusive scan of <= SG_CAP + 1
+// values in LDS), and the counts back to zero for the next tick
+__device__ void cgrid_scan_block(const Dev &d, int a) {
   __shared__ int wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i = bx * 256 + tid, per = kMaxCells * d.B;
   const int cc = cgrid_cols(d), n = cc * cc;  // buckets (start[n] = total)
-  // this thread's cell first (independent of the scan): its loads overlap the counts'
-  const bool in = i < per;
-  const int slot = in ? i / d.B : 0, p = in ? i - slot * d.B : 0;
-  const size_t g = (size_t)slot * d.NP + (size_t)a * d.B + p;
-  double x = 0, y = 0;
-  int rk = 0;
-  uint32_t fl = 0;
-  if (in) {
-    fl = d.c_flags[g];
-    x = d.c_x[g];
-    y = d.c_y[g];
-    rk = d.c_rank[(size_t)a * per + i];
-  }
-  const bool ok = in && (fl & F_ALIVE);
-  // exclusive scan of the <= 4096 counts: 16 per thread (4 aligned int4 loads)
-  const int4 *c4 = reinterpret_cast<const int4 *>(cgrid_counts(d, a, d.ctl[a].tick & 1));
+  int *cnt = cgrid_counts(d, a, 0);
+  const int4 *c4 = reinterpret_cast<const int4 *>(cnt);
   int v[16], sum = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1208,20 +1185,28 @@ __device__ void cgrid_scatter_block(const Dev &d, int a, int bx) {
   int run = inc - sum;
   for (int k = 0; k < w; k++) run += wsum[k];
   const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  int *start = d.cstart + (size_t)a * (d.H + 1);
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     const int j = tid * 16 + k;
-    if (j < n) sc[j] = run;
+    if (j < n) {
+      start[j] = run;
+      cnt[j] = 0;
+    }
     run += v[k];
   }
-  if (tid == 0) sc[n] = total;
-  __syncthreads();
-  if (bx == 0) {
-    int *start = d.cstart + (size_t)a * (d.H + 1);
-    for (int j = tid; j <= n; j += 256) start[j] = sc[j];
+  if (tid == 0) start[n] = total;
+}
+// step 3 for player gp's n cells (k_food_commit round 1)
+__device__ __forceinline__ void cgrid_place_player(const Dev &d, int gp, int n) {
+  const int NP = d.NP, a = gp / d.B, p = gp - a * d.B, per = kMaxCells * d.B;
+  const int *start = d.cstart + (size_t)a * (d.H + 1);
+  int *items = d.citems + (size_t)a * per;
+  for (int k = 0; k < n; k++) {
+    const int slot = d.p_list[k * NP + gp];
+    const int br = d.c_rank[(size_t)a * per + (size_t)slot * d.B + p];
+    items[start[br >> 17] + (br & 0x1FFFF)] = slot * NP + gp;
   }
-  if (!ok) return;
-  d.citems[(size_t)a * per + sc[cgrid_bucket(d, x, y)] + rk] = (int)g;
 }
 
 // blocks [0, A): blob grids; [A, 2A): virus grids (when enabled)
@@ -1382,6 +1367,25 @@ __device__ __forceinline__ void merge_player(const Dev &d, int gp) {
   }
 }
 
+// step 1 of the player-cell grid for player gp's cells after its merges, when no
+// virus test visits them (k_merge_vb); returns its largest cell radius
+__device__ double cgrid_count_player(const Dev &d, int gp) {
+  const int NP = d.NP, a = gp / d.B;
+  uint8_t l4[kTailRegs];
+#pragma unroll
+  for (int k = 0; k < kTailRegs; k++) l4[k] = d.p_list[k * NP + gp];
+  const bool alive = d.p_alive[gp];
+  const int n = d.p_ncells[gp];
+  if (!alive) return 0.0;
+  double rmax = 0;
+  for (int k = 0; k < n; k++) {
+    const size_t ci = (size_t)(k < kTailRegs ? l4[k] : d.p_list[k * NP + gp]) * NP + gp;
+    cgrid_count_cell(d, a, ci, d.c_x[ci], d.c_y[ci]);
+    rmax = fmax(rmax, d.c_r[ci]);
+  }
+  return rmax;
+}
+
 // ------------------------------------------------------------ serial-phase helpers
 // insertion sort of (key, val) pairs, single thread (worklists are short)
 __device__ void isort_kv(int64_t *key, int *val, int n) {
@@ -1519,8 +1523,14 @@ __device__ bool vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 __global__ void __launch_bounds__(256) k_merge_vb(Dev d, int64_t *scr_k, int *scr_v, int fold) {
   FLOOR(2);
   const int gi = GTID;
-  if (gi < d.NP) merge_player(d, gi);
-  else if (d.virus_enabled) vb_active(d, gi - d.NP);
+  double rg = 0;
+  if (gi < d.NP) {
+    merge_player(d, gi);
+    rg = cgrid_count_player(d, gi);
+  } else if (d.virus_enabled) {
+    vb_active(d, gi - d.NP);
+  }
+  wave_atomic_max_pos(&d.ctl[min(gi, d.NP - 1) / d.B].rmax_cell, rg);
   if (fold && last_block(d.ticket + 0, gridDim.x))
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) vb_serial_body(d, a, scr_k, scr_v);
 }
@@ -1567,7 +1577,9 @@ __device__ __forceinline__ bool wave_any_in_grid(const int *st, const int *items
 // walk the coarse virus grid serially (a few viruses per neighbourhood).  One
 // thread per player keeps the grid at NP/256 blocks, so the serial pass runs
 // in the last block (fold) for the price of a small ticket fan-in.
-__device__ void pv_player(const Dev &d, int gp) {
+// count: also take the cells' ranks in the player-cell grid (step 1 of its
+// build; not in pv_redo) -- returns the player's largest cell radius (0: none)
+__device__ double pv_player(const Dev &d, int gp, bool count = true) {
   const int NP = d.NP, a = gp / d.B;
   const int *st = d.vstart + (size_t)a * (d.H + 1);
   const int *it = d.vitems + (size_t)a * d.Vcap;
@@ -1580,8 +1592,9 @@ __device__ void pv_player(const Dev &d, int gp) {
   for (int k = 0; k < kTailRegs; k++) l4[k] = d.p_list[k * NP + gp];
   const bool alive = d.p_alive[gp];
   const int n = d.p_ncells[gp];
-  if (!alive) return;
+  if (!alive) return 0.0;
   bool anyp = false;
+  double rmax = 0;
   // the first cells' records in one round, before any grid walk
   double x4[kTailRegs], y4[kTailRegs], m4[kTailRegs], r4[kTailRegs];
 #pragma unroll
@@ -1609,6 +1622,7 @@ __device__ void pv_player(const Dev &d, int gp) {
       ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
       x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
     }
+    rmax = fmax(rmax, r);
     bool any = false;
     if (m > 1.25 * vmin) {
       const Rect q = footprint(x, y, r, d.size);
@@ -1627,6 +1641,16 @@ __device__ void pv_player(const Dev &d, int gp) {
     if (w < d.Wcap) d.work2[(size_t)a * d.Wcap + w] = gp - a * d.B;
     else set_err(d, a, ERR_WORK_CAP);
   }
+  if (count) {  // (last: the returning atomics delay no load of the activity test)
+#pragma unroll
+    for (int k = 0; k < kTailRegs; k++)
+      if (k < n) cgrid_count_cell(d, a, (size_t)l4[k] * NP + gp, x4[k], y4[k]);
+    for (int k = kTailRegs; k < n; k++) {
+      const size_t ci = (size_t)d.p_list[k * NP + gp] * NP + gp;
+      cgrid_count_cell(d, a, ci, d.c_x[ci], d.c_y[ci]);
+    }
+  }
+  return rmax;
 }
 // The activity test again for every player of arena a, by one wavefront, after
 // virusBlobOverlap's serial pass had work: a virus that grew or split changes
@@ -1637,7 +1661,7 @@ __device__ void pv_redo(const Dev &d, int a) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (lane 0's virus writes)
   if (lane == 0) __hip_atomic_store(&d.ctl[a].n_pend2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (int p = lane; p < d.B; p += 64) pv_player(d, a * d.B + p);
+  for (int p = lane; p < d.B; p += 64) pv_player(d, a * d.B + p, false);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the lanes' work-list writes, read by lane 0)
 }
@@ -1653,12 +1677,15 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
 __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *scr_v) {
   FLOOR(2);
   const int gi = GTID;
+  double rg = 0;
   if (gi < d.NP) {
     merge_player(d, gi);
-    pv_player(d, gi);
+    rg = pv_player(d, gi);
   } else {
     vb_active(d, gi - d.NP);
   }
+  // the player-cell grid's radius bound (pre-eat radii; eaters report their growth)
+  wave_atomic_max_pos(&d.ctl[min(gi, d.NP - 1) / d.B].rmax_cell, rg);
   if (last_block(d.ticket + 0, gridDim.x))
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) {
       const bool vb = vb_serial_body(d, a, scr_k, scr_v);
@@ -1716,6 +1743,7 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
         double m = grow_mass(cm, d.v_m[g] * kVirusEatFactor);
         d.c_m[ci] = m;
         d.c_r[ci] = radius_of(m);
+        atomic_max_pos(&c.rmax_cell, d.c_r[ci]);  // (the player-cell grid's radius bound)
         d.v_flags[g] = 0;
         atomicOr(&d.ctl[a].dirty, DIRTY_VIRUS);
         // playerCellAteVirus (field.py:350-370)
@@ -1762,6 +1790,7 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
           d.c_seq[ni] = seq;
           d.c_flags[ni] = F_ALIVE | F_INHASH | F_NEW;  // addPlayerCell hashes it
           d.c_active[ni] = 0;
+          cgrid_count_cell(d, a, ni, px, py);  // (step 1 of the player-cell grid)
           d.p_list[(ncur + k) * NP + gp] = (uint8_t)slot;
         }
         d.p_ncells[gp] = ncur + n_new;
@@ -1908,9 +1937,13 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
   __shared__ int s_idx[4][PREP_CAND];
   __shared__ uint8_t s_sel[4][PREP_CAND];
+  // blocks [0, A) when not resuming: the player-cell grid's scan (cgrid_scan_block)
+  const int nscan = resume ? 0 : d.A;
+  if ((int)blockIdx.x < nscan) return cgrid_scan_block(d, blockIdx.x);
   PT_BEGIN(0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wi = xcd_block(blockIdx.x, gridDim.x) * 4 + w, gp = wi / PREP_WAVES, h = wi - gp * PREP_WAVES;
+  const int wi = xcd_block(blockIdx.x - nscan, gridDim.x - nscan) * 4 + w, gp = wi / PREP_WAVES,
+            h = wi - gp * PREP_WAVES;
   if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP) return;
   // this wave's first list row rides the liveness / count load round (the row
@@ -2195,7 +2228,7 @@ __device__ double food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, u
 }
 // one player's cells in reservation round `round`; returns the largest radius
 // of its cells that ate (0: none) -- the player-cell grid's radius bound
-__device__ double food_commit_player(const Dev &d, int gp, int round, int last) {
+__device__ double food_commit_player(const Dev &d, int gp, int round, int last, int place) {
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   ArenaCtl &c = d.ctl[a];
   // round r reads how many cells failed round r-1 (nothing left: skip), counts
@@ -2204,6 +2237,7 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last) 
   const bool alive = d.p_alive[gp];
   const int n = d.p_ncells[gp];
   const int s_first = d.p_list[gp];
+  if (place && alive) cgrid_place_player(d, gp, n);  // (independent of the eats: its loads overlap theirs)
   if (round > 1 && c.food_undone[(round - 1) % 3] == 0) return 0;
   if (p == 0) c.food_undone[(round + 1) % 3] = 0;
   if (!alive) return 0;
@@ -2262,19 +2296,15 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last) 
 __device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v, int rounds);
 // fold (last round only): the serial pass runs in the last of the player blocks
 // (wave 0, arena after arena; the grid's extra blocks do not take part)
+// place: the player-cell grid's placement (round 1 of a tick's first eat pass)
 __global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last, int64_t *scr_k, int *scr_v,
-                                                     int rounds, int fold) {
+                                                     int rounds, int fold, int place) {
   FLOOR(5);
   TILE_GATE(d);
   const int ncommit = (d.NP + 255) / 256;
-  if ((int)blockIdx.x >= ncommit) {  // extra blocks: player-cell grid counts (round 1), scatter (round 2)
-    const int e = blockIdx.x - ncommit, nb = cgrid_blocks(d);
-    if (round == 1) return cgrid_count_block(d, e / nb, e % nb);
-    return cgrid_scatter_block(d, e / nb, e % nb);
-  }
   PT_BEGIN(4);
   const int gp = GTID;
-  const double rg = gp < d.NP ? food_commit_player(d, gp, round, last) : 0.0;
+  const double rg = gp < d.NP ? food_commit_player(d, gp, round, last, place) : 0.0;
   PT_MARK(4, round < 7 ? round : 7);
   wave_atomic_max_pos(&d.ctl[min(gp, d.NP - 1) / d.B].rmax_cell, rg);
   if (fold && last_block(d.ticket + 1, ncommit) && threadIdx.x < 64)
@@ -3941,21 +3971,18 @@ void launch_pellet_rows(const Dev &d, hipStream_t s) {
 }
 
 
-// playerPelletOverlap + playerBlobOverlap: prep, reservation rounds (>= 2),
-// serial rest; the player-cell grid rides along as extra blocks of rounds 1
-// (counts) and 2 (scatter).  (As extra blocks of the prep they made a fifth
-// block per CU beside its four, which waited for a free slot: ~+10 us.)
+// playerPelletOverlap + playerBlobOverlap: prep, reservation rounds (>= 1),
+// serial rest; the player-cell grid's scan rides along as the prep's head
+// blocks and its placement in round 1's player threads (cgrid_count_cell).
 // (resume: a further eat pass of a tiled tick -- the cell grid is built already)
 static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr, int resume = 0, int fold = 0) {
-  rounds = std::max(rounds, 2);  // (the cell grid's scatter rides on round 2)
+  rounds = std::max(rounds, 1);
   const int g = nblk(d.NP, 256);
-  const long per = (long)kMaxCells * d.B;
-  const int cc = (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c;
-  const int ncg = resume ? 0 : nblk(std::max(per, (long)cc * cc + 1), 256) * d.A;
-  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4)), dim3(256), 0, s, d, rounds, resume);
+  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4) + (resume ? 0 : d.A)), dim3(256), 0, s, d,
+                     rounds, resume);
   for (int r = 1; r <= rounds; r++) {
-    hipLaunchKernelGGL(k_food_commit, dim3(g + (r <= 2 ? ncg : 0)), dim3(256), 0, s, d, r, r == rounds ? 1 : 0, scr.k,
-                       scr.v, rounds, fold && r == rounds ? 1 : 0);
+    hipLaunchKernelGGL(k_food_commit, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0, scr.k, scr.v, rounds,
+                       fold && r == rounds ? 1 : 0, r == 1 && !resume ? 1 : 0);
   }
   if (!fold) hipLaunchKernelGGL(k_food_serial, dim3(d.A), dim3(64), 0, s, d, scr.k, scr.v, rounds);
 }
@@ -4160,6 +4187,80 @@ __global__ void __launch_bounds__(256) k_tile_apply(Dev d, int box_recs, int fir
       }
     }
   }
+}
+// C4 with the reference's Greedy bots (bot.py:579-633, aigar_tile_policy): a
+// Greedy move reads every pellet of the bot's view, which only the tile that
+// observes the bot is sure to hold -- the observation's own rule, the history
+// holder (the last observer until this tick's plan folds it in,
+// tile_plan_thread), else the tile of the view centre (its view was checked against the
+// held pellets when it was last observed; k_policy_greedy checks it again).  So
+// each tile takes the moves of the bots it observes (k_policy_greedy under this
+// mask) and the commands are all-gathered before the tick: one message of
+// TR_CMD records (player, command point, split | eject << 1).  The policy's
+// random draws are Philox-keyed by (player, tick): the same on every tile.
+__global__ void k_tile_cmd_mask(Dev d, uint8_t *mask) {
+  const int gp = GTID;
+  if (gp >= d.NP) return;
+  bool mine = false;
+  if (d.p_alive[gp]) {  // (before this tick's hand-off plan: the last observer, if any, holds the history)
+    const int ob = d.t_obsby[gp], hold = ob >= 0 ? ob : d.t_holder[gp];
+    mine = (hold >= 0 ? hold : tile_of(d, d.p_fx[gp], d.p_fy[gp])) == d.tile_id;
+  }
+  mask[gp] = mine ? 1 : 0;
+}
+// cap: command records a message holds (the message buffer less its header)
+__global__ void __launch_bounds__(256) k_tile_cmd_collect(Dev d, const uint8_t *mask, int cap) {
+  const int gp = GTID;
+  ArenaCtl &c = d.ctl[0];
+  if (gp < d.NP && mask[gp]) {
+    const int k = atomicAdd(&c.n_cmd, 1);
+    if (k < cap) {
+      TileRec r;
+      r.kind = TR_CMD;
+      r.idx = gp;
+      r.seq = (int64_t)(d.p_split[gp] ? 1 : 0) | ((int64_t)(d.p_eject[gp] ? 1 : 0) << 1);
+      r.x = d.p_cmdx[gp];
+      r.y = d.p_cmdy[gp];
+      d.outbox[1 + k] = r;
+    } else {
+      set_err(d, 0, ERR_TILE_CAP);
+    }
+  }
+  if (last_block(d.ticket + 4, gridDim.x) && threadIdx.x == 0) {
+    TileRec &h = d.outbox[0];
+    h.kind = TR_HDR;
+    h.idx = min(c.n_cmd, cap);
+    h.seq = 0;
+    h.x = h.y = 0.0;
+    c.n_cmd = 0;
+  }
+}
+// one block per source tile: the other tiles' commands (box_recs: records per inbox slot)
+__global__ void __launch_bounds__(256) k_tile_cmd_apply(Dev d, int box_recs) {
+  const int k = blockIdx.x;
+  if (k == d.tile_id) return;
+  const TileRec *box = d.inbox + (size_t)k * box_recs;
+  const int n = min(box[0].idx, box_recs - 1);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const TileRec r = box[1 + i];
+    if (r.kind != TR_CMD || r.idx < 0 || r.idx >= d.NP) {
+      set_err(d, 0, ERR_TILE_LOOKUP);
+      continue;
+    }
+    d.p_cmdx[r.idx] = r.x;
+    d.p_cmdy[r.idx] = r.y;
+    d.p_split[r.idx] = (int)(r.seq & 1);
+    d.p_eject[r.idx] = (int)((r.seq >> 1) & 1);
+  }
+}
+void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask, int want);
+void launch_tile_policy(const Dev &d, hipStream_t s, int greedy_split, uint8_t *mask, int cap) {
+  hipLaunchKernelGGL(k_tile_cmd_mask, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, mask);
+  launch_policy_greedy(d, s, greedy_split, mask, 1);
+  hipLaunchKernelGGL(k_tile_cmd_collect, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, (const uint8_t *)mask, cap);
+}
+void launch_tile_cmd_apply(const Dev &d, hipStream_t s, int box_recs) {
+  hipLaunchKernelGGL(k_tile_cmd_apply, dim3(d.ntiles), dim3(256), 0, s, d, box_recs);
 }
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first) {
   hipLaunchKernelGGL(k_tile_apply, dim3(d.ntiles), dim3(256), 0, s, d, box_recs, first);

@@ -77,7 +77,8 @@ def merge_states(states):
     return d
 
 
-def tiled_tick(tiles, transport, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None, extra_passes=None):
+def tiled_tick(tiles, transport, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None, extra_passes=None,
+               greedy_split=False):
     """One tick of the tiles in `tiles` (all of them, or this rank's one): begin,
     then exchange / apply passes until no owned cell is undone on any tile (the
     count comes with the messages, so every tile takes the same decision), then
@@ -86,7 +87,17 @@ def tiled_tick(tiles, transport, policy="none", p_split=0.0, p_eject=0.0, seed=0
     extra_passes=K (an int): no host round trip -- K further passes are issued
     whatever happens and do nothing on the device once every cell is final; the
     tick raises (device error bit) if cells are still undone after them.  With
-    the default halo every cell is decided by the first pass (K = 0)."""
+    the default halo every cell is decided by the first pass (K = 0).
+
+    policy "greedy": the reference's Greedy bots (bot.py:579-633) -- each tile
+    moves the bots it observes (it holds their whole view), and the commands go
+    round in one exchange before the tick."""
+    if policy == "greedy":
+        for t in tiles:
+            t.tile_policy(greedy_split)
+        transport.exchange(tiles)
+        for t in tiles:
+            t.tile_apply_commands()
     for t in tiles:
         t.tile_begin(policy, p_split, p_eject, seed)
     passes = 1
@@ -172,10 +183,11 @@ class TiledArena:
         for t in self.tiles:
             t.set_commands(cmd)
 
-    def tick(self, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None, extra_passes=None):
+    def tick(self, policy="none", p_split=0.0, p_eject=0.0, seed=0, obs=None, extra_passes=None, greedy_split=False):
         """One Field.update() of the tiled arena; obs: per-tile device tensors
         (each tile writes the rows of the bots it observes)."""
-        self.passes.append(tiled_tick(self.tiles, self.transport, policy, p_split, p_eject, seed, obs, extra_passes))
+        self.passes.append(tiled_tick(self.tiles, self.transport, policy, p_split, p_eject, seed, obs, extra_passes,
+                                      greedy_split))
 
     def step(self, n=1, **kw):
         for _ in range(n):

@@ -315,7 +315,11 @@ int aigar_get_events(aigar_handle *h, int arena, int64_t *out, int cap, int *n);
  * in the tile) report their outcomes in ONE message per pass, and the caller's
  * transport all-gathers the messages (RCCL all-gather over xGMI; in-process
  * device copies for tests):
- *   aigar_tile_begin(h, p)  policy (NONE / RANDOM) + the tick up to the first
+ *   [Greedy bots (bot.py:579-633): aigar_tile_policy(h, greedy_split), the
+ *    all-gather, aigar_tile_apply_commands(h) -- each tile moves the bots it
+ *    observes (it holds their whole view) and sends their commands]
+ *   aigar_tile_begin(h, p)  policy (NONE / RANDOM; GREEDY once the commands of
+ *                           this tick were applied) + the tick up to the first
  *                           eat pass; the outbox holds the message
  *   <all-gather every tile's outbox into every tile's inbox>
  *   aigar_tile_apply(h, &u) the other tiles' outcomes; u = owned cells still
@@ -360,6 +364,14 @@ int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox);
  * and records only (no bitmap); the inbox then holds tile k's at k * these bytes */
 int aigar_tile_msg_bytes(aigar_handle *h, int64_t *bytes);
 int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p);
+/* Greedy moves of the bots this tile observes (the observation's rule: history
+ * holder, else the view centre's tile) into a command message [header: kind 0,
+ * count][kind 5 records: player, split | eject << 1, command x, y]; after the
+ * all-gather aigar_tile_apply_commands takes the other tiles' commands.  Replaces
+ * Bot.make_greedy_bot_move + set_command_point (bot.py:579-633, 550-577) for a
+ * tiled arena, where no tile holds every pellet. */
+int aigar_tile_policy(aigar_handle *h, int greedy_split);
+int aigar_tile_apply_commands(aigar_handle *h);
 int aigar_tile_apply(aigar_handle *h, int *undone);
 int aigar_tile_resume(aigar_handle *h);
 int aigar_tile_end(aigar_handle *h, void *obs_out, int dtype);
@@ -376,6 +388,7 @@ int aigar_tile_observers(aigar_handle *h, int32_t *out);
  *   aigar_tile_comm_init(h, path, id, nranks, rank)  ncclCommInitRank; nranks
  *                                    must be the tile count and rank the tile id
  *   aigar_tile_run(h, n, p, extra_passes, obs, dtype)  n tiled steps: per step
+ *       (policy GREEDY: aigar_tile_policy, all-gather, aigar_tile_apply_commands)
  *       aigar_tile_begin, all-gather, aigar_tile_apply, extra_passes gated
  *       (resume, all-gather, apply) rounds, aigar_tile_end (obs: DEVICE buffer
  *       or NULL) -- captured once as a hipGraph (RCCL is captured with it),

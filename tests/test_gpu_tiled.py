@@ -304,3 +304,48 @@ def test_dead_bots_beyond_the_hand_off_slots_raise():
             ta.tick(extra_passes=0)
             ta.observe()
     ta.close()
+
+
+def _commands(st):
+    pf, pi = np.asarray(st["players_f"]), np.asarray(st["players_i"])
+    return np.c_[pf[:, 0], pf[:, 1], pi[:, 2], pi[:, 3]].astype(np.float64)
+
+
+def test_c3_4x2_greedy_bots_on_tiles():
+    """the reference's Greedy bots (bot.py:579-633 with
+    ENABLE_GREEDY_SPLIT) driving C4's own layout.  No tile holds every pellet, so
+    each tile moves the bots it observes (their history holder, else their view
+    centre's tile: it holds the whole view) and the commands are all-gathered
+    before the tick (aigar_tile_policy / aigar_tile_apply_commands).  From the
+    matured tick-50 world, 40 ticks: every bot's command equals the oracle's own
+    Greedy move, the merged events every tick, the state every 10 ticks, every
+    bot's observation every 5 (observations hand histories, and with them the
+    moving tile, from tile to tile)."""
+    cfg = c3_config()
+    start = parity.load_snapshot("c3_t50")
+    ta, o = TiledArena(cfg, 4, 2), Oracle(cfg)
+    ta.load_state(start)
+    o.load_state(start)
+    nev, splits = 0, 0
+    for t in range(40):
+        o.policy_greedy(True)
+        want = o.commands()
+        ta.tick(policy="greedy", greedy_split=True)
+        for k, tile in enumerate(ta.tiles):
+            got = _commands(tile.get_state())
+            bad = np.argwhere(got != want)
+            assert not len(bad), "tick %d tile %d bot %d: %s vs oracle %s" % (t, k, bad[0][0], got[bad[0][0]],
+                                                                              want[bad[0][0]])
+        splits += int(want[:, 2].sum())
+        o.step(1)
+        eg, eo = ta.events(), o.events()
+        assert np.array_equal(eg, eo), "tick %d: events differ (%d vs %d)" % (t, len(eg), len(eo))
+        nev += len(eo)
+        if (t + 1) % 10 == 0:
+            dif = parity.diff_states(ta.get_state(), o.get_state())
+            assert not dif, "tick %d: %s" % (t, dif[:3])
+        if (t + 1) % 5 == 0:
+            assert parity.obs_close(ta.observe(), o.observe()), "tick %d: observations differ" % t
+    assert nev > 5000 and splits > 0, (nev, splits)
+    ta.close()
+    o.close()

@@ -124,3 +124,36 @@ def test_torch_transport_nccl_world_size_one():
         o.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_tile_run_greedy_over_rccl_matches_oracle():
+    """aigar_tile_run with policy GREEDY over the 1-rank RCCL communicator: the
+    tile moves the bots it observes, the command message goes through its own
+    ncclAllGather inside the step graph before the tick; 20 steps from the
+    matured tick-50 world, every command equal to the oracle's Greedy move."""
+    cfg = c3_config()
+    stp, o = forced_tile(cfg), Oracle(cfg)
+    snap = parity.load_snapshot("c3_t50")
+    stp.load_state(snap)
+    o.load_state(snap)
+    torch.cuda.set_device(0)
+    stp.set_stream(torch.cuda.current_stream().cuda_stream)
+    tiles.rccl_comm(stp)
+    obs = torch.full((cfg.bots_per_arena, stp.obs_len), -7.0, dtype=torch.float64, device="cuda")
+    for t in range(20):
+        o.policy_greedy(True)
+        want = o.commands()
+        stp.tile_run(1, "greedy", obs, greedy_split=True)
+        torch.cuda.synchronize()
+        got = _policy_commands(stp)
+        bad = np.argwhere(got != want)
+        assert not len(bad), "step %d bot %d: %s vs oracle %s" % (t, bad[0][0], got[bad[0][0]], want[bad[0][0]])
+        o.step(1)
+        assert np.array_equal(tiles.merge_events([stp.events_raw()]), o.events()), "step %d: events differ" % t
+        want_obs = o.observe()
+        if t % 5 == 4:
+            dif = parity.diff_states(stp.get_state(), o.get_state())
+            assert not dif, "step %d: %s" % (t, dif[:3])
+            assert parity.obs_close(obs.cpu().numpy(), want_obs), "step %d: observations differ" % t
+    assert stp.tile_run_graphed()
+    stp.sync()
