@@ -54,6 +54,7 @@ struct ArenaCtl {
   int n_pel_eaten;    // eaten in this tick's eat phase
   int n_blob;         // blob slots in use
   int n_blob_base;    // blob count before this tick's ejections
+  int n_blob_add;     // this tick's ejections (n_blob moves in k_players' last block)
   int n_vir;          // virus slots in use
   int n_vir_start;    // viruses that existed when virusBlobOverlap started
   int n_dead;         // deadPlayers list length
@@ -95,7 +96,7 @@ enum : uint32_t {
   ERR_OBS_CAP = 32, ERR_CAND_CAP = 64, ERR_SLOT = 128, ERR_PIX_CAP = 256, ERR_TILE_CAP = 512, ERR_TILE_LOOKUP = 1024,
   ERR_TILE_OBS = 2048,    // a tile observed a bot whose view reaches beyond its held pellets
   ERR_TILE_PASSES = 4096,  // a device-bounded tiled tick ended with owned cells undone
-  ERR_PREDICT = 8192,      // updatePlayers made other counts than k_tick_begin predicted (head_counts)
+  ERR_PREDICT = 8192,      // updatePlayers made other counts than k_players' arena block predicted (head_counts)
   ERR_TILE_HANDOFF = 16384  // more dead bots to hand off in one tick than a message has hand-off slots
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
@@ -153,7 +154,8 @@ struct Dev {
   int hcap, hrec, nh;  // hand-off slots per message, records per slot, history grids per bot (0..4)
   int *t_holder;  // [NP] tile holding the bot's current observation history, -1: every tile
   int *t_obsby;   // [NP] tile that observed the bot since the last plan, -1: none
-  int *t_holive;  // [hcap] live bots waiting for a hand-off slot this tick (slots left after the dead ones)
+  int *t_holive;  // [NP] live bots waiting for a hand-off slot this tick (slots left after the dead ones)
+  uint8_t *t_hodefer;  // [NP] ticks a live bot has waited for a hand-off slot (waiters go first)
   int *t_hoslot;  // [hcap] the player of each hand-off slot of this tick's first message
   int own_bx0, own_bx1, own_by0, own_by1;      // owned centre buckets [x0, x1) x [y0, y1)
   int loc_bx0, loc_bx1, loc_by0, loc_by1;      // held pellets: owned range + halo
@@ -161,7 +163,7 @@ struct Dev {
   const TileRec *inbox;  // [ntiles] outboxes (the transport fills it)
   int *ticket;  // finished-block counters of kernels whose last block runs an epilogue
   // closing pellet update (k_pel_update): the store slots killed this tick (their rows
-  // are rewritten), and this tick's first pellet spawns, drawn ahead by k_tick_begin
+  // are rewritten), and this tick's first pellet spawns, drawn ahead by k_players
   int *kill_list;     // [A][Pcap]
   double *spec_x, *spec_y, *spec_m;  // [A][64]
   double pow_n032[17];  // pow_glibc(n, 0.32) for n = 0..16 cells (getFovSize, player.py:163-167)
@@ -197,7 +199,7 @@ struct Dev {
   int64_t *c_seq;
   uint8_t *c_active;
   // Cell.split geometry of a splitting player's cells [16*NP], computed by the
-  // cell's own k_tick_begin thread (the new cell's radius and momentum): the
+  // cell's own update_cell thread (the new cell's radius and momentum): the
   // split in k_players' per-player chain then loads it instead of evaluating
   // two atan2 / sincos pairs per cell
   double *sp_r, *sp_svx, *sp_svy;
@@ -227,7 +229,7 @@ struct Dev {
   int *v_svc;
   int64_t *v_seq;
   uint32_t *v_flags;
-  uint8_t *v_active;
+  int *v_active;  // virusBlobOverlap's work-list marks (vb_active_blob; cleared by the serial pass)
   int *vcnt, *vstart, *vitems, *v_rank;
   // cell grid
   int *ccnt, *cstart, *citems, *c_rank;

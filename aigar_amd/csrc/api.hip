@@ -23,6 +23,7 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v);
 void launch_tile_pass(const Dev &d, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first);
 void launch_tile_policy(const Dev &d, hipStream_t s, int greedy_split, uint8_t *mask, int cap);
 void launch_tile_cmd_apply(const Dev &d, hipStream_t s, int box_recs);
+void launch_pel_gather(const Dev &d, hipStream_t s, int a);
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch,
@@ -432,7 +433,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(bcnt, int, A * H1); AL(bstart, int, A * H1); AL(bitems, int, E); AL(b_rank, int, E);
   AL(v_x, double, V); AL(v_y, double, V); AL(v_m, double, V); AL(v_r, double, V); AL(v_vx, double, V);
   AL(v_vy, double, V); AL(v_svx, double, V); AL(v_svy, double, V); AL(v_svc, int, V); AL(v_seq, int64_t, V);
-  AL(v_flags, uint32_t, V); AL(v_active, uint8_t, V);
+  AL(v_flags, uint32_t, V); AL(v_active, int, V);
   AL(vcnt, int, A * H1); AL(vstart, int, A * H1); AL(vitems, int, V); AL(v_rank, int, V);
   AL(ccnt, int, A * H1); AL(cstart, int, A * H1); AL(citems, int, C); AL(c_rank, int, C);
   AL(cgcnt, int, A * 2 * 4100);
@@ -458,7 +459,8 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   if (d.tiled) {
     AL(t_holder, int, NP);
     AL(t_obsby, int, NP);
-    AL(t_holive, int, d.hcap);
+    AL(t_holive, int, NP);
+    AL(t_hodefer, uint8_t, NP);
     AL(t_hoslot, int, d.hcap);
     AL(outbox, TileRec, h->box_recs);
     TileRec *ib = nullptr;
@@ -543,6 +545,8 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   HIPCHK(hipMemsetAsync(d.cgcnt, 0, sizeof(int) * A * 2 * 4100, h->stream));
   HIPCHK(hipMemsetAsync(d.vstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.bstart, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.bcnt, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.v_active, 0, sizeof(int) * A * d.Vcap, h->stream));
   HIPCHK(hipMemsetAsync(d.o_lastfov, 0, sizeof(double) * NP, h->stream));
   // Bot.reset (bot.py:125-164): currentAction None (NN) / [0, 0, 0, 0] (Greedy, Random)
   HIPCHK(hipMemsetAsync(d.o_act_cur, 0, sizeof(double) * NP * 4, h->stream));
@@ -1372,20 +1376,24 @@ extern "C" int aigar_get_state(aigar_handle *h, int arena, aigar_state *st) {
   std::vector<int> bsvc, vsvc, pcol, bcol;
   std::vector<uint32_t> bfl, vfl;
   int n_pel = 0;
-  {  // the row store: each row's live records [entry 0, entry cols) of its current home
+  {  // the row store: each row's live records [entry 0, entry cols) of its current home,
+     // packed on the device (k_pel_gather) so only the live records are copied
     std::vector<int> pst;
     std::vector<PelRec> store;
     std::vector<int> scol;
-    if (d2h(h, pst, d.pstart + (size_t)arena * d.PH1, d.PH1) || d2h(h, store, d.pel + po, d.PS) ||
-        d2h(h, scol, d.pel_col + po, d.PS))
+    if (d2h(h, pst, d.pstart + (size_t)arena * d.PH1, d.PH1)) return -1;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    long tot = 0;
+    for (int r = 0; r < d.cols; r++) tot += pst[(size_t)r * (d.cols + 1) + d.cols] - pst[(size_t)r * (d.cols + 1)];
+    if (tot > d.Pcap) return fail("get_state: %ld live pellet records exceed the capacity %d", tot, d.Pcap);
+    launch_pel_gather(d, h->stream, arena);
+    HIPCHK(hipGetLastError());
+    if (d2h(h, store, d.pn + (size_t)arena * d.Pcap, (int)tot) || d2h(h, scol, d.pn_col + (size_t)arena * d.Pcap, (int)tot))
       return -1;
     HIPCHK(hipStreamSynchronize(h->stream));  // (unpacked below)
-    for (int r = 0; r < d.cols; r++) {
-      const int lo = pst[(size_t)r * (d.cols + 1)], hi = pst[(size_t)r * (d.cols + 1) + d.cols];
-      for (int i = lo; i < hi; i++) {
-        px.push_back(store[i].x); py.push_back(store[i].y); pm.push_back(store[i].m); ps.push_back(store[i].seq);
-        pcol.push_back(scol[i]);
-      }
+    for (long i = 0; i < tot; i++) {
+      px.push_back(store[i].x); py.push_back(store[i].y); pm.push_back(store[i].m); ps.push_back(store[i].seq);
+      pcol.push_back(scol[i]);
     }
     n_pel = (int)px.size();
   }

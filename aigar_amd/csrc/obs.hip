@@ -200,8 +200,13 @@ __device__ __forceinline__ void wave_fov_walk_k(const Dev &d, int a, Rect Q, dou
     const int excl = inc - len, total = __shfl(inc, 63);
     for (int t0 = 0; t0 < total; t0 += 64) {
       const int t = t0 + lane;
-      int rw = 0;
-      for (int k = 1; k < nr; k++) rw = (__builtin_amdgcn_readlane(excl, k) <= t) ? k : rw;  // (k uniform: v_readlane)
+      // the batch's items lie in rows kb .. ke-1 (excl is non-decreasing): kb holds
+      // item t0, ke is the first row starting at or after t0 + 64; only those rows
+      // are searched, not all nr
+      const int kb = __popcll(__ballot(lane < nr && excl <= t0)) - 1;
+      const int ke = __popcll(__ballot(lane < nr && excl < t0 + 64));
+      int rw = kb;
+      for (int k = kb + 1; k < ke; k++) rw = (__builtin_amdgcn_readlane(excl, k) <= t) ? k : rw;  // (k uniform: v_readlane)
       const int idx = __shfl(lo, rw) + (t - __shfl(excl, rw));
       const int kd = __shfl(kind, rw);
       const bool valid = t < total;

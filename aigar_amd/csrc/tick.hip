@@ -1,9 +1,11 @@
 // tick.hip -- Field.update() (field.py:85-92) as a sequence of gfx950 kernels.
 //
 // Phase map (kernel <- reference), in launch order:
-//   k_tick_begin              updateViruses + updateBlobs + per-cell part of Player.update
-//                             field.py:94-110, player.py:39-44
-//   k_players                 rest of updatePlayers (split, eject, move, push-apart) +
+//   k_players                 one block per 256 players, one per arena and one per 512 blob
+//                             slots: updateViruses + updateBlobs (field.py:94-110) and the
+//                             tick's bookkeeping in the extra blocks, the player blocks first the per-cell part
+//                             of Player.update (player.py:39-44), then the
+//                             rest of updatePlayers (split, eject, move, push-apart) +
 //                             creation-sequence numbers (canonical order) + blob append
 //                             field.py:112-181, player.py:30-72; + updateHashTables for
 //                             blobs and viruses (field.py:121-132; centre-bucket counting
@@ -237,24 +239,27 @@ __device__ __forceinline__ void update_virus(const Dev &d, int gi) {
 }
 
 // ------------------------------------------------------------ T2 blobs
-__device__ __forceinline__ void update_blob(const Dev &d, int gi) {
+// (returns whether the blob lives on as a blob, with its new position in x, y)
+__device__ __forceinline__ bool update_blob(const Dev &d, int gi, double &x, double &y) {
   int a = gi / d.Ecap, i = gi - a * d.Ecap;
-  if (i >= d.ctl[a].n_blob || !(d.b_flags[gi] & F_ALIVE)) return;
+  if (i >= d.ctl[a].n_blob || !(d.b_flags[gi] & F_ALIVE)) return false;
   if (d.b_svc[gi] == 0) {  // stopped blob becomes a pellet (addPellet)
     int j = atomicAdd(&d.ctl[a].n_pnew, 1);
     if (j >= d.Pcap) {  // (the staging list; eat-phase index PS + j, see Food)
       set_err(d, a, ERR_PELLET_CAP);
-      return;
+      return false;
     }
     size_t pj = (size_t)a * d.Pcap + j;
     d.pn[pj] = PelRec{d.b_x[gi], d.b_y[gi], d.b_m[gi], d.b_seq[gi]};
     d.pn_col[pj] = d.b_col[gi];  // (addPellet(blob): the same object, its colour kept)
     d.b_flags[gi] = 0;
     atomicOr(&d.ctl[a].dirty, DIRTY_BLOB);
-    return;
+    return false;
   }
   int svc = d.b_svc[gi];
-  double svx = d.b_svx[gi], svy = d.b_svy[gi], x = d.b_x[gi], y = d.b_y[gi];
+  double svx = d.b_svx[gi], svy = d.b_svy[gi];
+  x = d.b_x[gi];
+  y = d.b_y[gi];
   update_momentum(svc, svx, svy);
   update_pos(x, y, d.b_vx[gi], d.b_vy[gi], svx, svy, svc, (double)d.size, (double)d.size);
   d.b_svc[gi] = svc;
@@ -262,6 +267,20 @@ __device__ __forceinline__ void update_blob(const Dev &d, int gi) {
   d.b_svy[gi] = svy;
   d.b_x[gi] = x;
   d.b_y[gi] = y;
+  return true;
+}
+// The blob grid (coarse, 2^cshift fine buckets per side) is built in two steps:
+// each blob takes its rank in a per-arena count array (Dev::bcnt) where its
+// position is final -- k_players' blob blocks (updateBlobs) and the ejecting
+// player's thread -- and an extra block per arena of the merge launch scans the
+// counts (re-zeroing them) and places the items (blob_grid_place).
+__device__ __forceinline__ int blob_cell(const Dev &d, double x, double y) {
+  const int s = d.cshift, cc = (d.cols + (1 << s) - 1) >> s;
+  return (center_bucket_coord(y, d.cols) >> s) * cc + (center_bucket_coord(x, d.cols) >> s);
+}
+__device__ __forceinline__ void blob_count(const Dev &d, int a, size_t g, double x, double y) {
+  const int b = blob_cell(d, x, y);
+  d.b_rank[g] = (b << 12) | atomicAdd(&d.bcnt[(size_t)a * (d.H + 1) + b], 1);  // rank < 4096 (else ERR_SLOT)
 }
 
 // ------------------------------------------------------------ T4 players
@@ -286,40 +305,23 @@ __device__ __forceinline__ void predicted_counts(int heavy, int n0, bool split, 
   nsplit = split ? min(c36, kMaxCells - n0) : 0;
   nb = eject ? 2 * min(nsplit, c70) + (c36 - nsplit) + c35 : 0;
 }
-__device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPolicy &rp PT_PARAMS) {
-  const int NP = d.NP;
-  if (gi >= kMaxCells * NP) return;
-  const int gp = gi % NP;
-  const size_t ci = (size_t)gi;
-  const bool head = gi < NP;  // the player's slot-0 thread
-  const bool live = d.c_flags[ci] & F_ALIVE;
-  if (!d.p_alive[gp] || (!live && !(rp.on && head))) return;  // (dead players keep their command: makeMove)
-  // every load of the cell up front, before any store: one memory round trip,
-  // not one per store the compiler cannot prove disjoint
-  double m = d.c_m[ci], r = d.c_r[ci], svx = d.c_svx[ci], svy = d.c_svy[ci], mt = d.c_mt[ci];
-  const double x = d.c_x[ci], y = d.c_y[ci];
-  int svc = d.c_svc[ci];
-  double cmdx, cmdy;
-  bool split;
-  PT_MARK(2, 2);
-  if (rp.on) {
-    const Command c = random_command(d, gp, rp);  // (the player's live cells and slot 0 only)
-    PT_MARK(2, 3);
-    if (head) {  // slot 0 stores the player's command
-      d.p_cmdx[gp] = c.x;
-      d.p_cmdy[gp] = c.y;
-      d.p_split[gp] = c.split;
-      d.p_eject[gp] = c.eject;
-    }
-    if (!live) return;
-    cmdx = c.x;
-    cmdy = c.y;
-    split = c.split;
-  } else {
-    cmdx = d.p_cmdx[gp];
-    cmdy = d.p_cmdy[gp];
-    split = d.p_split[gp] != 0;
-  }
+// one live cell ci of a live player (k_players' cell phase), the player's command given;
+// heavy: the player's predicted-count word in LDS
+// every load of a cell up front, before any store: one memory round trip, not
+// one per store the compiler cannot prove disjoint (and a thread's two cells
+// load together)
+struct CellIn {
+  double m, r, svx, svy, mt, x, y;
+  int svc;
+};
+__device__ __forceinline__ CellIn load_cell(const Dev &d, size_t ci) {
+  return CellIn{d.c_m[ci], d.c_r[ci], d.c_svx[ci], d.c_svy[ci], d.c_mt[ci], d.c_x[ci], d.c_y[ci], d.c_svc[ci]};
+}
+__device__ __forceinline__ void update_cell(const Dev &d, size_t ci, const CellIn &in, double cmdx, double cmdy,
+                                            bool split, int *heavy) {
+  double m = in.m, r = in.r, svx = in.svx, svy = in.svy;
+  const double mt = in.mt, x = in.x, y = in.y;
+  int svc = in.svc;
   if (m >= 4) {  // Cell.decayMass (cell.py:123-126)
     m = m * kDecay;
     r = radius_of(m);
@@ -327,16 +329,14 @@ __device__ __forceinline__ void update_cell(const Dev &d, int gi, const RandomPo
     d.c_r[ci] = r;
   }
   if (m >= 35)  // k_players' predicted counts (predicted_counts)
-    atomicAdd(&d.p_heavy[gp], (m > 36 ? 1 : 0) | (m >= 70 ? 1 << 8 : 0) | (m > 36 ? 0 : 1 << 16));
+    atomicAdd(heavy, (m > 36 ? 1 : 0) | (m >= 70 ? 1 << 8 : 0) | (m > 36 ? 0 : 1 << 16));
   update_momentum(svc, svx, svy);
   d.c_svc[ci] = svc;
   d.c_svx[ci] = svx;
   d.c_svy[ci] = svy;
   if (mt > 0) d.c_mt[ci] = mt - 1;
   double vx, vy, ca, sa;
-  PT_MARK(2, 4);
   set_move_direction(x, y, m, r, cmdx, cmdy, vx, vy, ca, sa);
-  PT_MARK(2, 5);
   d.c_vx[ci] = vx;
   d.c_vy[ci] = vy;
   if (split && m > 36) {  // Cell.split's geometry (cell.py:72-85), for update_player's split
@@ -530,7 +530,7 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, const Player
       used |= 1u << slot;
       size_t ni = (size_t)slot * NP + gp;
       // Cell.split (cell.py:72-85); its angle, radius and momentum were computed by
-      // the cell's k_tick_begin thread (update_cell: the same values, bit for bit)
+      // the cell's own update_cell thread (the same values, bit for bit)
       double x = cx[ci], y = cy[ci];
       double nm = cm[ci] / 2, nr = d.sp_r[ci];
       double svx = d.sp_svx[ci], svy = d.sp_svy[ci];
@@ -642,24 +642,28 @@ __device__ void spawn_ahead(const Dev &d, int a, int j) {
   d.spec_y[o] = (double)(int64_t)mulhi(u[1], (uint64_t)d.size);
   d.spec_m[o] = (sr > 50 - 4) ? (double)(50 - sr) : 1.0;  // randomSize (field.py:20-26)
 }
-// per-tick resets, by extra threads at the end of k_tick_begin's grid (in the
-// update threads their loads delayed every cell's first round): the spawn
+// per-tick resets, by k_players' arena block (in the cell threads their loads
+// delayed every cell's first round): the spawn
 // occupancy restarts (k_pp_active rebuilds it; its last reader was the previous
 // tick's spawns); the dead flags of the last closing update's blob conversions
 // (that update's blocks read them while building their lists, so none of them
 // may clear one) are cleared
-constexpr int kTickZero = 16 * 256;
-__device__ void tick_zero(const Dev &d, int gi) {
-  for (long i = gi; i < (long)d.A * d.H; i += kTickZero) d.occ_cnt[i] = 0;
-  for (long i = gi; i < (long)d.A * d.occ_words; i += kTickZero) d.occ[i] = 0;
-  for (long t = gi; t < (long)d.A * d.Ecap; t += kTickZero) {
-    const int a = (int)(t / d.Ecap), j = (int)(t - (long)a * d.Ecap);
-    const ArenaCtl &c = d.ctl[a];
-    if (j < c.pu_nconv) d.pel_dead[(size_t)a * d.PD + d.PS + j] = 0;
+// (arena a; part k of nk: the occupancy is one bucket count per fine bucket --
+// 320k at C3, ~14 us for one block's stores -- so every extra block of the
+// arena zeroes a slice of it)
+__device__ void tick_zero(const Dev &d, int a, int k, int nk) {
+  const int T = blockDim.x;
+  const int h0 = (int)((long)d.H * k / nk), h1 = (int)((long)d.H * (k + 1) / nk);
+  for (int i = h0 + threadIdx.x; i < h1; i += T) d.occ_cnt[(size_t)a * d.H + i] = 0;
+  const int w0 = (int)((long)d.occ_words * k / nk), w1 = (int)((long)d.occ_words * (k + 1) / nk);
+  for (int i = w0 + threadIdx.x; i < w1; i += T) d.occ[(size_t)a * d.occ_words + i] = 0;
+  if (k == 0) {
+    const int nconv = d.ctl[a].pu_nconv;
+    for (int j = threadIdx.x; j < nconv; j += T) d.pel_dead[(size_t)a * d.PD + d.PS + j] = 0;
   }
 }
 // C4: the tick's first pass opens with the observation hand-off plan: extra
-// threads of k_tick_begin, one per player.  A bot's history is current on
+// threads of k_players' arena block, one per player.  A bot's history is current on
 // t_holder (-1: on every tile), or on the tile that observed it since the last
 // plan (t_obsby) -- that update is replicated, every tile makes it.  The holder
 // hands the history off when the bot is dead (it respawns anywhere at the end of
@@ -669,9 +673,10 @@ __device__ void tick_zero(const Dev &d, int gi) {
 // on every tile.  Dead bots come first: they take slots here (more than hcap in
 // one tick is ERR_TILE_HANDOFF, never a silent deferral -- the stale holder could
 // not observe a bot respawned outside its pellets).  Live bots only queue here
-// (t_holive); tile_plan_live, in the message's last block, gives them the slots
-// the dead left, and the rest keep their holder a tick longer: their centre moved
-// at most one tick's distance from the tile, which the halo covers.
+// (t_holive, room for every player); tile_plan_live, in the message's last block,
+// gives them the slots the dead left, and the rest keep their holder a tick
+// longer: their centre moved at most one tick's distance from the tile, which the
+// halo covers, and they go first at the next plan (t_hodefer), so none waits long.
 __device__ void tile_plan_thread(const Dev &d, int gp) {
   ArenaCtl &c = d.ctl[0];
   if (gp == 0) {  // the first pass's counters
@@ -690,7 +695,7 @@ __device__ void tile_plan_thread(const Dev &d, int gp) {
   if (d.p_alive[gp]) {
     if (tile_of(d, d.p_fx[gp], d.p_fy[gp]) == h) return;
     const int q = atomicAdd(&c.n_ho_live, 1);
-    if (q < d.hcap) d.t_holive[q] = gp;
+    if (q < d.NP) d.t_holive[q] = gp;
     return;
   }
   const int sl = atomicAdd(&c.n_ho, 1);
@@ -702,23 +707,36 @@ __device__ void tile_plan_thread(const Dev &d, int gp) {
   d.t_hoslot[sl] = gp;  // (its history is copied into the slot by tile_plan_live, block-parallel)
 }
 // The first pass's hand-off slots, in the message's last block: the live bots
-// take the slots the dead left (lowest player index first, so the choice does
-// not depend on atomic order), then the whole block copies every slot's
-// history -- [TR_HIST record: player, lastFovSize][nh grids] -- element by
-// element (a thread per bot copying its ~250 doubles serially took ~4 us)
+// take the slots the dead left -- every queued bot is ranked, the ones that
+// waited at an earlier plan first, then by player index (the choice does not
+// depend on atomic order, and a bot passed over goes first next tick) -- then
+// the whole block copies every slot's history -- [TR_HIST record: player,
+// lastFovSize][nh grids] -- element by element (a thread per bot copying its
+// ~250 doubles serially took ~4 us)
+constexpr int kHoLds = 2048;  // queued live bots ranked in LDS (more: ranked from global memory)
 __device__ void tile_plan_live(const Dev &d) {
   ArenaCtl &c = d.ctl[0];
-  __shared__ int s_q[kHcapMax];
-  const int nd = min(c.n_ho, d.hcap), nq = min(c.n_ho_live, d.hcap), room = d.hcap - nd;
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) s_q[i] = d.t_holive[i];
+  __shared__ int s_q[kHoLds];
+  const int nd = min(c.n_ho, d.hcap), nq = min(c.n_ho_live, d.NP), room = d.hcap - nd;
+  // key: (did not wait before) << 30 | player
+  auto key_of = [&](int gp) { return (d.t_hodefer[gp] ? 0 : 1 << 30) | gp; };
+  const bool lds = nq <= kHoLds;
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {  // (the keys first: the ranking below updates t_hodefer)
+    const int k = key_of(d.t_holive[i]);
+    if (lds) s_q[i] = k;
+    else d.t_holive[i] = k;
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) {  // rank by player index
-    const int gp = s_q[i];
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const int k = lds ? s_q[i] : d.t_holive[i], gp = k & ((1 << 30) - 1);
     int r = 0;
-    for (int j = 0; j < nq; j++) r += s_q[j] < gp;
+    for (int j = 0; j < nq; j++) r += (lds ? s_q[j] : d.t_holive[j]) < k;
     if (r < room) {
       d.t_holder[gp] = -1;
       d.t_hoslot[nd + r] = gp;
+      d.t_hodefer[gp] = 0;
+    } else {
+      d.t_hodefer[gp] = (uint8_t)min(255, d.t_hodefer[gp] + 1);
     }
   }
   __syncthreads();
@@ -739,32 +757,6 @@ __device__ void tile_plan_live(const Dev &d) {
   }
   if (threadIdx.x == 0) c.n_ho = ns;
 }
-__global__ void __launch_bounds__(256) k_tick_begin(Dev d, RandomPolicy rp) {
-  FLOOR(0);
-  PT_BEGIN(2);
-  int gi = GTID;
-  if (gi < kMaxCells * d.NP) {
-    update_cell(d, gi, rp PT_ARGS);
-    PT_MARK(2, 1);
-    return;
-  }
-  gi -= kMaxCells * d.NP;
-  if (d.virus_enabled) {
-    if (gi < d.A * d.Vcap) {
-      update_virus(d, gi);
-      return;
-    }
-    gi -= d.A * d.Vcap;
-  }
-  if (gi < d.A * d.Ecap) return update_blob(d, gi);
-  gi -= d.A * d.Ecap;
-  if (gi < d.A * kSpawnAhead) return spawn_ahead(d, gi / kSpawnAhead, gi % kSpawnAhead);
-  gi -= d.A * kSpawnAhead;
-  if (gi < kTickZero) return tick_zero(d, gi);
-  gi -= kTickZero;
-  if (d.tiled) tile_plan_thread(d, gi);  // C4: the observation hand-off plan
-}
-
 // rank of this thread among the flagged threads of the block (thread order);
 // *total = number flagged.  Ballot per wave + one pass over <= 16 wave counts.
 __device__ __forceinline__ int block_rank(bool flag, int *sh, int *total) {
@@ -836,25 +828,130 @@ __device__ __forceinline__ unsigned long long pl_word(unsigned long long st, uin
   return st | ((unsigned long long)(ep & 0x3FFFu) << 48) | ((unsigned long long)(vs & 0xFFFFFFu) << 24) |
          (unsigned long long)(vb & 0xFFFFFFu);
 }
-// updateHashTables for viruses and blobs rides along (the virus grid as one
-// extra block per arena -- viruses are final after k_tick_begin -- the blob
-// grid in the arena's last block, once every tile's blobs are appended).
-__global__ void __launch_bounds__(256) k_players(Dev d) {
+// The tick opens here too (round 5: the per-cell part of updatePlayers was a
+// launch of its own, k_tick_begin, one thread per pool slot over the whole GPU):
+// a player tile's cells depend only on their own players' commands, so the
+// block updates them itself before its player chains -- its 256 player threads
+// take the commands (the synthetic policy, rp.on) and queue their live cells in
+// LDS, all 512 threads then run the queue (decay, momentum, merge timer, move
+// direction with its correctly rounded pow / atan2 / sincos: one chain per cell,
+// a few hundred cells per tile), and the predicted counts collect in LDS.
+// The arena's extra blocks: the first (tile == ntiles) runs updateViruses
+// (field.py:94-100), the pellet spawns drawn ahead and the virus grid; the rest
+// updateBlobs (field.py:102-110), one blob slot per thread, and the per-tick
+// resets.  updateHashTables for viruses and blobs rides along: the virus grid
+// in the arena block, the blob grid's counts where each blob's position is final
+// (blob_count: the blob blocks, the ejecting players), its placement in the
+// merge launch (blob_grid_place).
+constexpr int kPlT = 512;  // threads per k_players block: 256 player threads + 256 cell helpers
+__global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   FLOOR(1);
   __shared__ int ws[4], wb[4];
   __shared__ int s_ps, s_pb, s_ts, s_tb, s_blob0;
   __shared__ int64_t s_seq0;
   __shared__ uint32_t s_epoch;
   __shared__ int g_cnt[SG_CAP + 1], g_sh[32];  // (the small grids' counting sort)
+  __shared__ int s_nq, s_heavy[256];
+  __shared__ double s_cx[256], s_cy[256];
+  __shared__ uint8_t s_csp[256];
+  __shared__ uint16_t s_q[256 * kMaxCells];  // the tile's live cells: local player << 4 | slot
   PT_BEGIN(1);
+#ifdef AIGAR_PHASE_TIMING  // (the cell phase and the extra blocks mark under slot 2)
+  if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[2][pt_w_][0] = (unsigned)pt0_;
+#endif
   const int tile = blockIdx.x, a = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ntiles = d.pl_tiles, NP = d.NP;
-  if (tile == ntiles) {  // the virus grid (+ its radius bound and lightest mass)
-    grid_small_build<2>(d, a, g_cnt, g_sh);
+  ArenaCtl &c = d.ctl[a];
+  // every block of the arena draws a ticket; the last one bumps the look-back
+  // epoch and sets the blob count
+  auto finish = [&]() __attribute__((always_inline)) {
+    if (last_block(&c.pl_ticket, (int)gridDim.x) && tid == 0) {
+      __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the blob count moves only now: the blob blocks bound their slots by it
+      const int nb = c.n_blob_base + c.n_blob_add;
+      if (nb > d.Ecap) set_err(d, a, ERR_BLOB_CAP);
+      c.n_blob = min(nb, d.Ecap);
+    }
+  };
+  if (tile > ntiles) {  // updateBlobs: one blob slot per thread (a loop over the pool
+    // in one block was the kernel's longest chain, ~15 us at C3), + the resets
+    const int k = tile - ntiles - 1, i = k * kPlT + tid;
+    if (i < c.n_blob) {  // (the count at the tick's start: it moves in the last block)
+      const size_t g = (size_t)a * d.Ecap + i;
+      double x, y;
+      if (update_blob(d, (int)g, x, y)) blob_count(d, a, g, x, y);
+      else d.b_rank[g] = -1;
+    }
+    tick_zero(d, a, k, gridDim.x - ntiles - 1);
+    PT_MARK(2, 4);
+    finish();
     return;
   }
-  ArenaCtl &c = d.ctl[a];
+  if (tile == ntiles) {  // the arena block
+    if (d.virus_enabled)
+      for (int i = tid; i < d.Vcap; i += kPlT) update_virus(d, a * d.Vcap + i);
+    for (int j = tid; j < kSpawnAhead; j += kPlT) spawn_ahead(d, a, j);
+    __syncthreads();  // (the virus updates -> the virus grid, in this block)
+    if (d.virus_enabled) grid_small_build<2>(d, a, g_cnt, g_sh);  // (+ its radius bound and lightest mass)
+    PT_MARK(2, 3);
+    finish();
+    return;
+  }
   unsigned long long *st = d.pl_state + (size_t)a * ntiles;
+  // ---- the cell phase (Player.decayMass + updateCellProperties, player.py:39-44)
+  const int p = tile * 256 + (tid & 255), gp = a * d.B + p;
+  PlayerHead ph{};
+  if (tid == 0) s_nq = 0;
+  if (tid < 256) s_heavy[tid] = 0;
+  __syncthreads();
+  if (tid < 256 && p < d.B) {
+    ph = player_head(d, gp);  // (update_player's first round)
+    if (d.tiled) tile_plan_thread(d, gp);  // C4: the observation hand-off plan
+    if (ph.alive) {
+      if (rp.on) {  // the synthetic population's move (makeMove; dead players keep their command)
+        const Command cm = random_command(d, gp, rp);
+        d.p_cmdx[gp] = ph.cpx = cm.x;
+        d.p_cmdy[gp] = ph.cpy = cm.y;
+        d.p_split[gp] = cm.split;
+        d.p_eject[gp] = cm.eject;
+        ph.split = cm.split != 0;
+        ph.eject = cm.eject != 0;
+      }
+      s_cx[tid] = ph.cpx;
+      s_cy[tid] = ph.cpy;
+      s_csp[tid] = ph.split ? 1 : 0;
+      const int q = atomicAdd(&s_nq, ph.n);
+      for (int k = 0; k < ph.n; k++)
+        s_q[q + k] = (uint16_t)((tid << 4) | (k < kTailRegs ? ph.lst[k] : d.p_list[k * NP + gp]));
+    }
+  }
+  __syncthreads();
+  PT_MARK(2, 1);
+  {
+    const int nq = s_nq, pb = a * d.B + tile * 256;
+    auto cell_of = [&](int i) { return (size_t)(s_q[i] & 15) * NP + (pb + (s_q[i] >> 4)); };
+    auto run = [&](int i, const CellIn &in) {
+      const int lp = s_q[i] >> 4;
+      update_cell(d, cell_of(i), in, s_cx[lp], s_cy[lp], s_csp[lp] != 0, &s_heavy[lp]);
+    };
+    // a thread's first two cells in one load round (~4 cells per player: two rounds of cells per block)
+    const int i0 = tid, i1 = tid + kPlT;
+    CellIn c0{}, c1{};
+    if (i0 < nq) c0 = load_cell(d, cell_of(i0));
+    if (i1 < nq) c1 = load_cell(d, cell_of(i1));
+    if (i0 < nq) run(i0, c0);
+    if (i1 < nq) run(i1, c1);
+    for (int i = tid + 2 * kPlT; i < nq; i += kPlT) run(i, load_cell(d, cell_of(i)));
+  }
+  __syncthreads();
+  PT_MARK(2, 2);
+  if (tid >= 256) {  // (the helpers join the player part's three barriers and the last-block ticket only)
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    finish();
+    return;
+  }
   if (tid == 0) {
     s_epoch = __hip_atomic_load(&c.pl_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_seq0 = c.seq_next;
@@ -864,19 +961,12 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
       c.n_kill = 0;     // this tick's pellet kills (read by the last tick's closing update, done by now)
     }
   }
-  const int p = tile * 256 + tid, gp = a * d.B + p;
-  // the new cells / blobs each player will create, predicted by its k_tick_begin
-  // threads (predicted_counts): the block scan and the tile's aggregate for the
+  // the new cells / blobs each player will create, predicted by the cell phase
+  // (predicted_counts): the block scan and the tile's aggregate for the
   // look-back are published before the player chains run, so the look-back after
   // them finds every predecessor's aggregate instead of waiting for the slowest tile
   int pn = 0, pb = 0;
-  PlayerHead ph{};
-  if (p < d.B) {
-    ph = player_head(d, gp);  // (update_player's first round, issued with the counts)
-    const int heavy = d.p_heavy[gp];
-    if (ph.alive) predicted_counts(heavy, ph.n, ph.split, ph.eject, pn, pb);
-    if (heavy) d.p_heavy[gp] = 0;  // (the next tick's k_tick_begin adds to it again)
-  }
+  if (p < d.B && ph.alive) predicted_counts(s_heavy[tid], ph.n, ph.split, ph.eject, pn, pb);
   const int vs = pn + pb, vb = pb;
   int is = vs, ib = vb;
 #pragma unroll
@@ -970,12 +1060,7 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     c.seq_base_upd = seq0;
     c.seq_next = seq0 + tot;
     c.n_blob_base = blob0;
-    if (blob0 + totb > d.Ecap) {
-      c.err |= ERR_BLOB_CAP;
-      c.n_blob = d.Ecap;
-    } else {
-      c.n_blob = blob0 + totb;
-    }
+    c.n_blob_add = totb;  // (n_blob moves in the last block)
   }
   // the seq pass: a register-tail player's flags are final already and its list
   // is in flst (fn cells): only its new cells (the last nn) are numbered here
@@ -996,11 +1081,11 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
     }
     for (int j = 0; j < nb; j++) {
       int bi = blob0 + boff + j;
-      if (bi >= d.Ecap) break;  // ERR_BLOB_CAP set above
+      if (bi >= d.Ecap) break;  // ERR_BLOB_CAP set in the last block
       size_t g = (size_t)a * d.Ecap + bi, si = (size_t)j * NP + gp;
-      const double bm = kEjectMass * 0.8;
-      d.b_x[g] = d.sb_x[si];
-      d.b_y[g] = d.sb_y[si];
+      const double bm = kEjectMass * 0.8, bx = d.sb_x[si], by = d.sb_y[si];
+      d.b_x[g] = bx;
+      d.b_y[g] = by;
       d.b_m[g] = bm;
       d.b_r[g] = radius_of(bm);
       d.b_vx[g] = 0;
@@ -1012,13 +1097,11 @@ __global__ void __launch_bounds__(256) k_players(Dev d) {
       d.b_ej[g] = d.c_seq[(size_t)d.sb_slot[si] * NP + gp];
       d.b_col[g] = p;
       d.b_flags[g] = F_ALIVE;
+      blob_count(d, a, g, bx, by);
     }
   }
   PT_MARK(1, 6);
-  if (last_block(&c.pl_ticket, ntiles)) {  // the arena's last block: look-back epoch, blob grid
-    if (tid == 0) __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    grid_small_build<1>(d, a, g_cnt, g_sh);
-  }
+  finish();
 }
 
 // ------------------------------------------------------------ grids
@@ -1121,11 +1204,10 @@ __device__ __forceinline__ void grid_small_build(const Dev &d, int a, int *cnt, 
   __syncthreads();
 }
 // Player-cell grid, coarse (2^cshift_c fine buckets per side, <= SG_CAP cells).
-// k_cgrid_count takes atomic ranks in a small count array -- one per tick
-// parity; the other parity is re-zeroed here for the next tick -- and every
-// k_cgrid_scatter block re-scans those <= SG_CAP + 1 counts in LDS, so the
-// grid needs two launches and no multi-block scan.  Consumers apply the exact
-// footprint test, so the coarser buckets only add candidates.
+// Atomic ranks go into a small count array per arena; one block re-scans those
+// <= SG_CAP + 1 counts in LDS, so the grid needs no multi-block scan.
+// Consumers apply the exact footprint test, so the coarser buckets only add
+// candidates.
 __device__ __forceinline__ int cgrid_cols(const Dev &d) { return (d.cols + (1 << d.cshift_c) - 1) >> d.cshift_c; }
 __device__ __forceinline__ int cgrid_bucket(const Dev &d, double x, double y) {
   const int sh = d.cshift_c;
@@ -1404,26 +1486,57 @@ __device__ void isort_kv(int64_t *key, int *val, int n) {
 }
 
 // ------------------------------------------------------------ T11 virus <- blob
-__device__ __forceinline__ void vb_active(const Dev &d, int gi) {
-  if (gi >= d.A * d.Vcap) return;
-  int a = gi / d.Vcap, i = gi - a * d.Vcap;
-  if (i == 0) d.ctl[a].n_vir_start = d.ctl[a].n_vir;
-  if (i >= d.ctl[a].n_vir || !(d.v_flags[gi] & F_ALIVE)) return;
-  double vx = d.v_x[gi], vy = d.v_y[gi], vm = d.v_m[gi], vr = d.v_r[gi];
-  Rect q = footprint(vx, vy, vr, d.size);
-  bool any = false;
-  const int *st = d.bstart + (size_t)a * (d.H + 1);
-  const int *it = d.bitems + (size_t)a * d.Ecap;
-  grid_visit(st, it, d.cols, q, 1, [&](int j) {
-    size_t g = (size_t)a * d.Ecap + j;
-    if (any || !(d.b_flags[g] & F_ALIVE)) return;
-    if (!rect_hit(footprint(d.b_x[g], d.b_y[g], d.b_r[g], d.size), q)) return;
-    if (overlap(vx, vy, vm, vr, d.b_x[g], d.b_y[g], d.b_m[g], d.b_r[g])) any = true;
-  }, d.cshift);
-  if (any) {
-    int w = atomicAdd(&d.ctl[a].n_pend, 1);
+// virusBlobOverlap's activity test (field.py:316-325) from the blob side: one
+// thread per blob slot walks the virus grid around the blob's footprint and
+// marks every virus it overlaps -- the same pairs as the virus side's walk of the
+// blob grid (both tests are symmetric: footprint-rect hit, then overlap), but
+// without the blob grid, which is built in the same launch.  A virus joins the
+// work list once (v_active: set here, cleared by the serial pass).
+__device__ __forceinline__ void vb_active_blob(const Dev &d, int gb) {
+  if (gb >= d.A * d.Ecap) return;
+  const int a = gb / d.Ecap, j = gb - a * d.Ecap;
+  const ArenaCtl &c = d.ctl[a];
+  if (j >= c.n_blob || !(d.b_flags[gb] & F_ALIVE)) return;
+  const double bx = d.b_x[gb], by = d.b_y[gb], bm = d.b_m[gb], br = d.b_r[gb];
+  const Rect qb = footprint(bx, by, br, d.size);
+  const int *st = d.vstart + (size_t)a * (d.H + 1);
+  const int *it = d.vitems + (size_t)a * d.Vcap;
+  const int nv = c.n_vir;
+  grid_visit(st, it, d.cols, qb, expand_for(c.rmax_virus), [&](int i) {
+    const size_t g = (size_t)a * d.Vcap + i;
+    if (i >= nv || !(d.v_flags[g] & F_ALIVE)) return;
+    const double vx = d.v_x[g], vy = d.v_y[g], vr = d.v_r[g];
+    if (!rect_hit(footprint(vx, vy, vr, d.size), qb)) return;
+    if (!overlap(vx, vy, d.v_m[g], vr, bx, by, bm, br)) return;
+    if (atomicExch(&d.v_active[g], 1) != 0) return;
+    const int w = atomicAdd(&d.ctl[a].n_pend, 1);
     if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = i;
     else set_err(d, a, ERR_WORK_CAP);
+  }, d.cshift);
+}
+// the blob grid's second step (blob_count): one block per arena loads the
+// counts (re-zeroing them for the next tick), scans them in LDS, stores the
+// bucket starts and places every ranked blob
+__device__ void blob_grid_place(const Dev &d, int a, int *cnt, int *sh) {
+  const int tid = threadIdx.x, T = blockDim.x, s = d.cshift;
+  const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
+  const int n = d.ctl[a].n_blob;
+  int *gc = d.bcnt + (size_t)a * (d.H + 1);
+  for (int i = tid; i <= Hc; i += T) {
+    cnt[i] = gc[i];
+    gc[i] = 0;
+  }
+  __syncthreads();
+  block_scan_excl(cnt, cnt, Hc + 1, sh);  // in place: bucket starts (ends with a barrier)
+  int *start = d.bstart + (size_t)a * (d.H + 1), *items = d.bitems + (size_t)a * d.Ecap;
+  const int *rank = d.b_rank + (size_t)a * d.Ecap;
+  for (int i = tid; i <= Hc; i += T) start[i] = cnt[i];
+  for (int i = tid; i < n; i += T) {
+    const int rk = rank[i];
+    if (rk < 0) continue;
+    const int b = rk >> 12, r = rk & 4095;
+    if (r == 4095) set_err(d, a, ERR_SLOT);
+    items[cnt[b] + r] = i;
   }
 }
 // the serial passes are device bodies run by one wavefront per arena: as their
@@ -1441,7 +1554,10 @@ __device__ bool vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
   int *cv = scr_v + (size_t)a * d.Wcap;
   if (nw == 0) return false;
   // active viruses in list order; viruses appended by splits are visited too
-  for (int k = 0; k < nw; k++) ck[k] = w[k];
+  for (int k = 0; k < nw; k++) {
+    ck[k] = w[k];
+    d.v_active[(size_t)a * d.Vcap + w[k]] = 0;  // (vb_active_blob's marks)
+  }
   isort_kv(ck, w, nw);
   const int *st = d.bstart + (size_t)a * (d.H + 1);
   const int *it = d.bitems + (size_t)a * d.Ecap;
@@ -1520,17 +1636,22 @@ __device__ bool vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 // mergePlayerCells (per player) and the virus<-blob activity test (per virus)
 // in one launch: merging touches only player cells, the test only viruses/blobs
 // fold: virusBlobOverlap's serial pass runs in the last block (one wave per arena)
+// (+ one block per arena at the end: the blob grid's placement, blob_grid_place)
 __global__ void __launch_bounds__(256) k_merge_vb(Dev d, int64_t *scr_k, int *scr_v, int fold) {
   FLOOR(2);
-  const int gi = GTID;
-  double rg = 0;
-  if (gi < d.NP) {
-    merge_player(d, gi);
-    rg = cgrid_count_player(d, gi);
-  } else if (d.virus_enabled) {
-    vb_active(d, gi - d.NP);
+  __shared__ int g_cnt[SG_CAP + 1], g_sh[32];
+  const int nbP = (d.NP + 255) / 256;
+  if ((int)blockIdx.x >= nbP) {
+    blob_grid_place(d, blockIdx.x - nbP, g_cnt, g_sh);
+  } else {
+    const int gi = GTID;
+    double rg = 0;
+    if (gi < d.NP) {
+      merge_player(d, gi);
+      rg = cgrid_count_player(d, gi);
+    }
+    wave_atomic_max_pos(&d.ctl[min(gi, d.NP - 1) / d.B].rmax_cell, rg);
   }
-  wave_atomic_max_pos(&d.ctl[min(gi, d.NP - 1) / d.B].rmax_cell, rg);
   if (fold && last_block(d.ticket + 0, gridDim.x))
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) vb_serial_body(d, a, scr_k, scr_v);
 }
@@ -1674,18 +1795,29 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
 // virusBlobOverlap's serial pass (the last block) had work, which is rare (0
 // per tick at C3, random or Greedy bots): then the arena's test runs again
 // (pv_redo) before playerVirusOverlap's serial pass.
+// Blocks: the players' (merges + the virus test), the blob slots' (the
+// virus<-blob activity test from the blob side) and one per arena placing the
+// blob grid (read first by virusBlobOverlap's serial pass, in the last block).
 __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *scr_v) {
   FLOOR(2);
-  const int gi = GTID;
-  double rg = 0;
-  if (gi < d.NP) {
-    merge_player(d, gi);
-    rg = pv_player(d, gi);
+  __shared__ int g_cnt[SG_CAP + 1], g_sh[32];
+  const int nbP = (d.NP + 255) / 256, nbB = (d.A * d.Ecap + 255) / 256, b = blockIdx.x;
+  if (b < nbP) {
+    const int gi = GTID;
+    double rg = 0;
+    if (gi < d.NP) {
+      merge_player(d, gi);
+      rg = pv_player(d, gi);
+    }
+    // the player-cell grid's radius bound (pre-eat radii; eaters report their growth)
+    wave_atomic_max_pos(&d.ctl[min(gi, d.NP - 1) / d.B].rmax_cell, rg);
+  } else if (b < nbP + nbB) {
+    vb_active_blob(d, (b - nbP) * 256 + threadIdx.x);
   } else {
-    vb_active(d, gi - d.NP);
+    const int a = b - nbP - nbB;
+    if (threadIdx.x == 0) d.ctl[a].n_vir_start = d.ctl[a].n_vir;  // (splits append past it)
+    blob_grid_place(d, a, g_cnt, g_sh);
   }
-  // the player-cell grid's radius bound (pre-eat radii; eaters report their growth)
-  wave_atomic_max_pos(&d.ctl[min(gi, d.NP - 1) / d.B].rmax_cell, rg);
   if (last_block(d.ticket + 0, gridDim.x))
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) {
       const bool vb = vb_serial_body(d, a, scr_k, scr_v);
@@ -3272,7 +3404,7 @@ __device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int 
 // those touch, each into its other home.  Step 1, by the arena's block of
 // k_spawn_plan after the spawn counts: this tick's pellet spawns are staged
 // (spawnPellets, field.py:303-313) -- the first kSpawnAhead were drawn by
-// k_tick_begin already (spec_*) -- and the tick's pellet bookkeeping closes.
+// k_players' arena block already (spec_*) -- and the tick's pellet bookkeeping closes.
 __device__ void spawn_pellet_at(const Dev &d, int a, int j, double *px, double *py);
 __device__ __forceinline__ void pellet_close_prep(const Dev &d, int a) {
   ArenaCtl &c = d.ctl[a];
@@ -3662,7 +3794,7 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
       rec = d.pn[Q0 + j];
       col = d.pn_col[Q0 + j];
       live = !d.pel_dead[D0 + d.PS + j];  // (a conversion eaten this tick does not join)
-    } else if (spec) {  // a spawn drawn ahead by k_tick_begin
+    } else if (spec) {  // a spawn drawn ahead by k_players' arena block
       const size_t o = (size_t)a * kSpawnAhead + (j - nconv);
       rec = PelRec{d.spec_x[o], d.spec_y[o], d.spec_m[o], c.seq_base_spawn + (j - nconv)};
     } else {
@@ -3922,6 +4054,35 @@ __global__ void __launch_bounds__(256) k_pel_update(Dev d, int nbF) {
   PT_MARK(8, 3);
 }
 
+// aigar_get_state's pellet records: every row's live range [start of bucket 0,
+// end of the last bucket) of arena a, packed in row order into the staging list
+// (free between ticks), so one copy of the live records leaves the device instead
+// of the whole two-home row store.  One block per row; its offset is the sum of
+// the earlier rows' lengths.
+__global__ void __launch_bounds__(256) k_pel_gather(Dev d, int a) {
+  __shared__ int wsum[4];
+  const int r = blockIdx.x, C = d.cols, tid = threadIdx.x;
+  const int *pst = d.pstart + (size_t)a * d.PH1;
+  int part = 0;
+  for (int q = tid; q < r; q += blockDim.x) part += pst[(size_t)q * (C + 1) + C] - pst[(size_t)q * (C + 1)];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  if ((tid & 63) == 0) wsum[tid >> 6] = part;
+  __syncthreads();
+  const int off = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const int lo = pst[(size_t)r * (C + 1)], hi = pst[(size_t)r * (C + 1) + C];
+  const size_t S0 = (size_t)a * d.PS, Q0 = (size_t)a * d.Pcap;
+  for (int i = lo + tid; i < hi; i += blockDim.x) {
+    const int o = off + (i - lo);
+    if (o >= d.Pcap) break;  // (the caller checks the total)
+    d.pn[Q0 + o] = d.pel[S0 + i];
+    d.pn_col[Q0 + o] = d.pel_col[S0 + i];
+  }
+}
+void launch_pel_gather(const Dev &d, hipStream_t s, int a) {
+  hipLaunchKernelGGL(k_pel_gather, dim3(d.cols), dim3(256), 0, s, d, a);
+}
+
 // ------------------------------------------------------------ init helpers
 __global__ void k_init_ctl(Dev d, uint64_t seed) {
   int a = GTID;
@@ -3994,17 +4155,15 @@ void launch_player_fov(const Dev &d, hipStream_t s);
 // overlap gains at this kernel size), so the graph stays linear.
 // the phases before the eat phase (field.py:94-198, 225-231, 246-253)
 void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, const RandomPolicy *rp) {
-  const long n_begin = (long)kMaxCells * d.NP + (d.virus_enabled ? (long)d.A * d.Vcap : 0) + (long)d.A * d.Ecap +
-                       (long)d.A * kSpawnAhead + kTickZero;
-  // (C4 tiles: + one block, the observation hand-off plan of the tick's first eat pass)
-  hipLaunchKernelGGL(k_tick_begin, dim3(nblk(n_begin + (d.tiled ? d.NP : 0), 256)), dim3(256), 0, s, d,
-                     rp ? *rp : RandomPolicy{0, 0, 0, 0});
-  // + the virus grid (extra block) and the blob grid (last block) of updateHashTables
-  hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + (d.virus_enabled ? 1 : 0), d.A), dim3(256), 0, s, d);
-  if (d.virus_enabled)  // merges, both virus activity tests, both serial passes (last block)
-    hipLaunchKernelGGL(k_merge_pv, dim3(nblk((long)d.NP + (long)d.A * d.Vcap, 256)), dim3(256), 0, s, d, scr_k, scr_v);
+  // the tick's first launch: per player tile its cells, then the players (+ C4:
+  // the observation hand-off plan); per arena one block for the viruses, spawns
+  // drawn ahead and the virus grid, and blocks for the blobs and the resets
+  hipLaunchKernelGGL(k_players, dim3(d.pl_tiles + 1 + (d.Ecap + kPlT - 1) / kPlT, d.A), dim3(kPlT), 0, s, d, rp ? *rp : RandomPolicy{0, 0, 0, 0});
+  if (d.virus_enabled)  // merges, both virus activity tests, the blob grid, both serial passes (last block)
+    hipLaunchKernelGGL(k_merge_pv, dim3(nblk(d.NP, 256) + nblk((long)d.A * d.Ecap, 256) + d.A), dim3(256), 0, s, d,
+                       scr_k, scr_v);
   else
-    hipLaunchKernelGGL(k_merge_vb, dim3(nblk(d.NP, 256)), dim3(256), 0, s, d, scr_k, scr_v, 0);
+    hipLaunchKernelGGL(k_merge_vb, dim3(nblk(d.NP, 256) + d.A), dim3(256), 0, s, d, scr_k, scr_v, 0);
 }
 // the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
@@ -4083,7 +4242,7 @@ __device__ void tile_header(const Dev &d) {
 // bitmaps (it may take one pass longer; ticks rarely need a second at all).
 // A later pass is gated (Dev::tile_gate): issued without asking the host whether
 // it is needed, its kernels return at once when no owned cell is undone.
-// The first pass's bookkeeping (counters, the hand-off plan) ran in k_tick_begin.
+// The first pass's bookkeeping (counters, the hand-off plan) ran in k_players.
 void launch_tile_pass(const Dev &d0, hipStream_t s, int rounds, int64_t *scr_k, int *scr_v, int first) {
   Dev d = d0;
   d.tile_gate = first ? 0 : 1;

@@ -160,7 +160,7 @@ def _commands(stp):
 def test_bench_graph_matches_oracle():
     """bench.py's timed path itself -- the C3 workload's config
     (events off, as timed), data/c3_t50.npz loaded by bench.start_world, the aigar_run
-    graph with the random policy fused into k_tick_begin and the bench's own split /
+    graph with the random policy fused into k_players and the bench's own split /
     eject probabilities and salt -- against the oracle for 25 steps.  The commands
     the fused policy made are read back after every replay and given to the oracle;
     the world and every bot's observation row are compared every step.  A second

@@ -253,7 +253,7 @@ def test_many_bots_crossing_a_border_in_one_tick():
     ta.load_state(snap)
     o.load_state(snap)
     rng = np.random.default_rng(3)
-    moves = []
+    moves, moved_sets = [], []
     prev = None
     for t in range(14):
         cmd = parity.synthetic_commands(rng, None, 256, 1200)
@@ -268,12 +268,17 @@ def test_many_bots_crossing_a_border_in_one_tick():
         by = ta.last_observers[:64].copy()
         if prev is not None:
             moves.append(int(np.sum((prev == 0) & (by == 1))))
+            if moves[-1]:
+                moved_sets.append(np.nonzero((prev == 0) & (by == 1))[0])
         prev = by
     dif = parity.diff_states(ta.get_state(), o.get_state())
     assert not dif, dif
     assert np.all(prev == 1), prev
-    # the crossing happened in one tick but the hand-offs were spread over several
+    # the crossing happened in one tick but the hand-offs were spread over several,
+    # in a fixed order: the lowest player indices first, and a bot passed over goes
+    # before any newcomer (the choice never depends on atomic order)
     assert max(moves) == 16 and sum(moves) == 64, moves
+    assert np.array_equal(np.concatenate(moved_sets), np.arange(64)), moved_sets
     ta.close()
     o.close()
 

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "aigar_amd", "libaigar_hip_pt.so")
 KERNELS = {0: ("k_food_prep", ["", "player", "cell", "pellet walk", "blob walk", "select", "reserve"]),
            1: ("k_players", ["", "player loads", "tail loads", "tail done", "update_player", "look-back", "seq + blobs"]),
-           2: ("k_tick_begin", ["", "update_cell", "cell loads", "policy", "decay+momentum", "move dir"]),
+           2: ("k_players/x", ["", "head+policy+queue", "cell updates", "arena block", "blob block", "last-block grid"]),
            3: ("k_pp_active", ["", "player", "cell", "grid test"]),
            4: ("k_food_commit", ["", "round 1", "round 2", "round 3", "round 4", "round 5", "round 6", "round 7+"]),
            5: ("k_spawn_plan", ["", "pp serial", "compaction", "virus grid", "spawn counts", "pellet close", "pp closures", "pp turns"]),
