@@ -223,7 +223,7 @@ struct Dev {
   int *b_col;  // the ejecting player (field.py:141 blob.setColor(player.getColor()))
   uint32_t *b_flags;
   uint64_t *b_owner;
-  int *bcnt, *bstart, *bitems, *b_rank;
+  int *bstart, *bitems, *b_rank;
   // viruses [A*Vcap]
   double *v_x, *v_y, *v_m, *v_r, *v_vx, *v_vy, *v_svx, *v_svy;
   int *v_svc;
@@ -233,7 +233,7 @@ struct Dev {
   int *vcnt, *vstart, *vitems, *v_rank;
   // cell grid
   int *ccnt, *cstart, *citems, *c_rank;
-  int *cgcnt;  // [A][2][4100] coarse cell-grid counts (<= 4096 cells), by tick parity
+  int *cgcnt;  // [A][2][4100] coarse grid counts (<= 4096 cells): the player cells', the blobs'
   // occupancy bitmap of the player hash [A][ceil(H/64)]
   unsigned long long *occ;  // getSpawnPos occupancy: one bit per fine bucket a live player cell touches
   int *occ_cnt;             // ... and the number of such cells per bucket (k_pp_active, kept by the pp pass)

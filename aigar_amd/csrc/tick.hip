@@ -270,7 +270,7 @@ __device__ __forceinline__ bool update_blob(const Dev &d, int gi, double &x, dou
   return true;
 }
 // The blob grid (coarse, 2^cshift fine buckets per side) is built in two steps:
-// each blob takes its rank in a per-arena count array (Dev::bcnt) where its
+// each blob takes its rank in a per-arena count array (cgrid_counts row 1) where its
 // position is final -- k_players' blob blocks (updateBlobs) and the ejecting
 // player's thread -- and an extra block per arena of the merge launch scans the
 // counts (re-zeroing them) and places the items (blob_grid_place).
@@ -278,9 +278,10 @@ __device__ __forceinline__ int blob_cell(const Dev &d, double x, double y) {
   const int s = d.cshift, cc = (d.cols + (1 << s) - 1) >> s;
   return (center_bucket_coord(y, d.cols) >> s) * cc + (center_bucket_coord(x, d.cols) >> s);
 }
+__device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int row);
 __device__ __forceinline__ void blob_count(const Dev &d, int a, size_t g, double x, double y) {
   const int b = blob_cell(d, x, y);
-  d.b_rank[g] = (b << 12) | atomicAdd(&d.bcnt[(size_t)a * (d.H + 1) + b], 1);  // rank < 4096 (else ERR_SLOT)
+  d.b_rank[g] = (b << 12) | atomicAdd(&cgrid_counts(d, a, 1)[b], 1);  // rank < 4096 (else ERR_SLOT)
 }
 
 // ------------------------------------------------------------ T4 players
@@ -1213,8 +1214,9 @@ __device__ __forceinline__ int cgrid_bucket(const Dev &d, double x, double y) {
   const int sh = d.cshift_c;
   return (center_bucket_coord(y, d.cols) >> sh) * cgrid_cols(d) + (center_bucket_coord(x, d.cols) >> sh);
 }
-__device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int parity) {
-  return d.cgcnt + ((size_t)a * 2 + parity) * CG_STRIDE;
+// row 0: the player-cell grid's counts, row 1: the blob grid's (blob_count)
+__device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int row) {
+  return d.cgcnt + ((size_t)a * 2 + row) * CG_STRIDE;
 }
 // The player-cell grid is built in three steps, none of them a launch of its own:
 //  1. counts: every live cell takes an atomic rank in its coarse bucket where its
@@ -1238,11 +1240,12 @@ __device__ __forceinline__ void cgrid_count_cell(const Dev &d, int a, size_t ci,
 }
 // one block per arena: bucket starts from the counts (exclusive scan of <= SG_CAP + 1
 // values in LDS), and the counts back to zero for the next tick
-__device__ void cgrid_scan_block(const Dev &d, int a) {
+// (256 threads) bucket starts of n <= SG_CAP counts (16-byte aligned, kept in
+// registers: 16 per thread, one int4 load round), written to start[0..n] and,
+// when lds is given, to lds[0..n]; the counts are re-zeroed for the next tick
+__device__ void count_scan_256(int *cnt, int n, int *start, int *lds) {
   __shared__ int wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int cc = cgrid_cols(d), n = cc * cc;  // buckets (start[n] = total)
-  int *cnt = cgrid_counts(d, a, 0);
   const int4 *c4 = reinterpret_cast<const int4 *>(cnt);
   int v[16], sum = 0;
 #pragma unroll
@@ -1267,17 +1270,24 @@ __device__ void cgrid_scan_block(const Dev &d, int a) {
   int run = inc - sum;
   for (int k = 0; k < w; k++) run += wsum[k];
   const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  int *start = d.cstart + (size_t)a * (d.H + 1);
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     const int j = tid * 16 + k;
     if (j < n) {
       start[j] = run;
+      if (lds) lds[j] = run;
       cnt[j] = 0;
     }
     run += v[k];
   }
-  if (tid == 0) start[n] = total;
+  if (tid == 0) {
+    start[n] = total;
+    if (lds) lds[n] = total;
+  }
+}
+__device__ void cgrid_scan_block(const Dev &d, int a) {
+  const int cc = cgrid_cols(d);
+  count_scan_256(cgrid_counts(d, a, 0), cc * cc, d.cstart + (size_t)a * (d.H + 1), nullptr);
 }
 // step 3 for player gp's n cells (k_food_commit round 1)
 __device__ __forceinline__ void cgrid_place_player(const Dev &d, int gp, int n) {
@@ -1517,20 +1527,15 @@ __device__ __forceinline__ void vb_active_blob(const Dev &d, int gb) {
 // the blob grid's second step (blob_count): one block per arena loads the
 // counts (re-zeroing them for the next tick), scans them in LDS, stores the
 // bucket starts and places every ranked blob
-__device__ void blob_grid_place(const Dev &d, int a, int *cnt, int *sh) {
+__device__ void count_scan_256(int *cnt, int n, int *start, int *lds);
+__device__ void blob_grid_place(const Dev &d, int a, int *cnt) {
   const int tid = threadIdx.x, T = blockDim.x, s = d.cshift;
-  const int cc = (d.cols + (1 << s) - 1) >> s, Hc = cc * cc;
+  const int cc = (d.cols + (1 << s) - 1) >> s;
   const int n = d.ctl[a].n_blob;
-  int *gc = d.bcnt + (size_t)a * (d.H + 1);
-  for (int i = tid; i <= Hc; i += T) {
-    cnt[i] = gc[i];
-    gc[i] = 0;
-  }
-  __syncthreads();
-  block_scan_excl(cnt, cnt, Hc + 1, sh);  // in place: bucket starts (ends with a barrier)
-  int *start = d.bstart + (size_t)a * (d.H + 1), *items = d.bitems + (size_t)a * d.Ecap;
+  int *items = d.bitems + (size_t)a * d.Ecap;
   const int *rank = d.b_rank + (size_t)a * d.Ecap;
-  for (int i = tid; i <= Hc; i += T) start[i] = cnt[i];
+  count_scan_256(cgrid_counts(d, a, 1), cc * cc, d.bstart + (size_t)a * (d.H + 1), cnt);
+  __syncthreads();
   for (int i = tid; i < n; i += T) {
     const int rk = rank[i];
     if (rk < 0) continue;
@@ -1639,10 +1644,10 @@ __device__ bool vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
 // (+ one block per arena at the end: the blob grid's placement, blob_grid_place)
 __global__ void __launch_bounds__(256) k_merge_vb(Dev d, int64_t *scr_k, int *scr_v, int fold) {
   FLOOR(2);
-  __shared__ int g_cnt[SG_CAP + 1], g_sh[32];
+  __shared__ int g_cnt[SG_CAP + 1];
   const int nbP = (d.NP + 255) / 256;
   if ((int)blockIdx.x >= nbP) {
-    blob_grid_place(d, blockIdx.x - nbP, g_cnt, g_sh);
+    blob_grid_place(d, blockIdx.x - nbP, g_cnt);
   } else {
     const int gi = GTID;
     double rg = 0;
@@ -1800,7 +1805,7 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v);
 // blob grid (read first by virusBlobOverlap's serial pass, in the last block).
 __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *scr_v) {
   FLOOR(2);
-  __shared__ int g_cnt[SG_CAP + 1], g_sh[32];
+  __shared__ int g_cnt[SG_CAP + 1];
   const int nbP = (d.NP + 255) / 256, nbB = (d.A * d.Ecap + 255) / 256, b = blockIdx.x;
   if (b < nbP) {
     const int gi = GTID;
@@ -1816,7 +1821,7 @@ __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *sc
   } else {
     const int a = b - nbP - nbB;
     if (threadIdx.x == 0) d.ctl[a].n_vir_start = d.ctl[a].n_vir;  // (splits append past it)
-    blob_grid_place(d, a, g_cnt, g_sh);
+    blob_grid_place(d, a, g_cnt);
   }
   if (last_block(d.ticket + 0, gridDim.x))
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) {
