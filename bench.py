@@ -56,6 +56,14 @@ def reference_python(workload):
 
 
 SNAPSHOTS = {"c3": "c3_t50"}  # matured start worlds (tools/mature.py)
+# The c3_t50 world was matured by Greedy bots (the survey's warm distribution);
+# under the random policy its first ~25 ticks carry ~3x the steady
+# playerPlayerOverlap work while the Greedy clusters scatter
+# (profiles/r04_v32_early_steps.txt: k_spawn_plan 36 -> 16 -> 10 us over steps
+# 0-5, 15-25, 25+).  The random population therefore first plays this many
+# untimed ticks from the snapshot -- part of setting up the world, like the load
+# -- so that warm-up and timed steps run its steady state whatever --warmup is.
+SETTLE_TICKS = 30
 
 # C3 observation config: VIRUS_SPAWN + ENABLE_SPLIT (networkParameters.py:76-96)
 C3_CH = (_abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_WALL | _abi.OBS_ENEMY | _abi.OBS_VIRUS | _abi.OBS_SELF_LF
@@ -442,6 +450,10 @@ def main():
 
     def run(n):  # n whole steps (policy + tick + observation), one graph replayed n times
         stp.run(n, args.policy, obs, p_split=ps, p_eject=pe, seed=salt, greedy_split=True)
+
+    if args.policy == "random" and name in SNAPSHOTS:
+        run(SETTLE_TICKS)  # (untimed: the random population settles from the Greedy-matured snapshot)
+        start += " + %d untimed random-policy ticks to settle" % SETTLE_TICKS
 
     def one_step():  # the same step as separate calls, each bracketed by HIP events
         if args.policy == "greedy":

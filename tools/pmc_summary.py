@@ -5,7 +5,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 128-B read requests as 64 B (MI355X_MICROARCH.md, HBM section), so the read
 figure is doubled; Infinity-Cache hits are included (the C3 world is ~10 MB).
 The step totals count the kernels of the timed env step only: launches per
-step = launches / steps (steps = the k_tick_begin launches); the snapshot load
+step = launches / steps (steps = the k_players launches: the tick's first kernel); the snapshot load
 before the timed region (`__amd_rocclr_*` copies and fills, the one-off
 reset / load kernels, < 1 launch per step) is reported apart.
 usage: pmc_summary.py DIR_FETCH DIR_WRITE [out.json]
@@ -30,7 +30,7 @@ def load(d, counter):
 
 def main():
     fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
-    steps = max((len(v) for k, v in fetch.items() if "k_tick_begin" in k), default=1)
+    steps = max((len(v) for k, v in fetch.items() if "k_players" in k), default=1)
     out, step = {}, {"read_bytes": 0.0, "write_bytes": 0.0, "traffic_bytes": 0.0, "kernels": 0, "steps": steps}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])

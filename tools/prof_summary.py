@@ -8,9 +8,9 @@ import sys
 
 path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
-# steps: given, else the number of ticks (k_tick_begin launches) in the trace
+# steps: given, else the number of ticks (k_players launches: the tick's first kernel) in the trace
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else float(
-    next((r["Calls"] for r in rows if "k_tick_begin" in r["Name"]), 110.0))
+    next((r["Calls"] for r in rows if "k_players" in r["Name"]), 110.0))
 fmt = "%-58s %7.2f %8.2f %9.2f"
 print("%-58s %7s %8s %9s" % ("kernel", "calls/s", "avg_us", "us/step"))
 tot, other = 0.0, []
