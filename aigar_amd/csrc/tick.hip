@@ -855,7 +855,7 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   __shared__ int s_nq, s_heavy[256];
   __shared__ double s_cx[256], s_cy[256];
   __shared__ uint8_t s_csp[256];
-  __shared__ uint16_t s_q[256 * kMaxCells];  // the tile's live cells: local player << 4 | slot
+  __shared__ uint16_t s_q[256 * (kMaxCells - 1)];  // the tile's queued cells: local player << 4 | slot
   PT_BEGIN(1);
 #ifdef AIGAR_PHASE_TIMING  // (the cell phase and the extra blocks mark under slot 2)
   if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[2][pt_w_][0] = (unsigned)pt0_;
@@ -902,6 +902,12 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   // ---- the cell phase (Player.decayMass + updateCellProperties, player.py:39-44)
   const int p = tile * 256 + (tid & 255), gp = a * d.B + p;
   PlayerHead ph{};
+  // a player's first cell is updated by its own thread, its record loaded beside
+  // the command's inputs; the other cells (multi-cell players) queue in LDS for
+  // the block's other threads
+  CellIn own{};
+  size_t own_ci = 0;
+  bool own_ok = false;
   if (tid == 0) s_nq = 0;
   if (tid < 256) s_heavy[tid] = 0;
   __syncthreads();
@@ -909,6 +915,11 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
     ph = player_head(d, gp);  // (update_player's first round)
     if (d.tiled) tile_plan_thread(d, gp);  // C4: the observation hand-off plan
     if (ph.alive) {
+      own_ok = ph.n > 0;
+      if (own_ok) {
+        own_ci = (size_t)ph.lst[0] * NP + gp;
+        own = load_cell(d, own_ci);
+      }
       if (rp.on) {  // the synthetic population's move (makeMove; dead players keep their command)
         const Command cm = random_command(d, gp, rp);
         d.p_cmdx[gp] = ph.cpx = cm.x;
@@ -921,28 +932,23 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
       s_cx[tid] = ph.cpx;
       s_cy[tid] = ph.cpy;
       s_csp[tid] = ph.split ? 1 : 0;
-      const int q = atomicAdd(&s_nq, ph.n);
-      for (int k = 0; k < ph.n; k++)
-        s_q[q + k] = (uint16_t)((tid << 4) | (k < kTailRegs ? ph.lst[k] : d.p_list[k * NP + gp]));
+      if (ph.n > 1) {
+        const int q = atomicAdd(&s_nq, ph.n - 1);
+        for (int k = 1; k < ph.n; k++)
+          s_q[q + k - 1] = (uint16_t)((tid << 4) | (k < kTailRegs ? ph.lst[k] : d.p_list[k * NP + gp]));
+      }
     }
   }
   __syncthreads();
   PT_MARK(2, 1);
-  {
+  if (own_ok) update_cell(d, own_ci, own, ph.cpx, ph.cpy, ph.split, &s_heavy[tid]);
+  {  // the queued cells: the helper threads take the first 256, the player threads the rest
     const int nq = s_nq, pb = a * d.B + tile * 256;
-    auto cell_of = [&](int i) { return (size_t)(s_q[i] & 15) * NP + (pb + (s_q[i] >> 4)); };
-    auto run = [&](int i, const CellIn &in) {
-      const int lp = s_q[i] >> 4;
-      update_cell(d, cell_of(i), in, s_cx[lp], s_cy[lp], s_csp[lp] != 0, &s_heavy[lp]);
-    };
-    // a thread's first two cells in one load round (~4 cells per player: two rounds of cells per block)
-    const int i0 = tid, i1 = tid + kPlT;
-    CellIn c0{}, c1{};
-    if (i0 < nq) c0 = load_cell(d, cell_of(i0));
-    if (i1 < nq) c1 = load_cell(d, cell_of(i1));
-    if (i0 < nq) run(i0, c0);
-    if (i1 < nq) run(i1, c1);
-    for (int i = tid + 2 * kPlT; i < nq; i += kPlT) run(i, load_cell(d, cell_of(i)));
+    for (int i = tid >= 256 ? tid - 256 : tid + 256; i < nq; i += kPlT) {
+      const int e = s_q[i], lp = e >> 4;
+      update_cell(d, (size_t)(e & 15) * NP + (pb + lp), load_cell(d, (size_t)(e & 15) * NP + (pb + lp)), s_cx[lp],
+                  s_cy[lp], s_csp[lp] != 0, &s_heavy[lp]);
+    }
   }
   __syncthreads();
   PT_MARK(2, 2);
@@ -1223,9 +1229,9 @@ __device__ __forceinline__ int *cgrid_counts(const Dev &d, int a, int row) {
 //     position and list are final -- mergePlayerCells' / the virus test's player
 //     threads of k_merge_pv (k_merge_vb), explosion children in its serial pass
 //     (cgrid_count_cell); the grid's radius bound is maxed there too;
-//  2. scan: one extra block per arena at the head of k_food_prep turns the
-//     counts into the bucket starts (cgrid_scan_block) and zeroes them for the
-//     next tick;
+//  2. scan: the first block of k_food_prep per arena turns the counts into
+//     the bucket starts (cgrid_scan_block) and zeroes them for the next tick,
+//     before its own players;
 //  3. placement: each player's thread of k_food_commit round 1 writes its cells'
 //     items (start of the bucket + rank).
 // Eating changes masses and radii, never positions (a cell that eats reports its
@@ -2074,12 +2080,14 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
   __shared__ int s_idx[4][PREP_CAND];
   __shared__ uint8_t s_sel[4][PREP_CAND];
-  // blocks [0, A) when not resuming: the player-cell grid's scan (cgrid_scan_block)
-  const int nscan = resume ? 0 : d.A;
-  if ((int)blockIdx.x < nscan) return cgrid_scan_block(d, blockIdx.x);
+  // blocks [0, A) when not resuming first run the player-cell grid's scan for
+  // arena blockIdx.x (cgrid_scan_block; read by the commit round), then their
+  // players: as extra blocks they were the 1025th block of a launch whose 1024
+  // fill the GPU once, and started ~5 us late
+  if (!resume && (int)blockIdx.x < d.A) cgrid_scan_block(d, blockIdx.x);
   PT_BEGIN(0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wi = xcd_block(blockIdx.x - nscan, gridDim.x - nscan) * 4 + w, gp = wi / PREP_WAVES,
+  const int wi = xcd_block(blockIdx.x, gridDim.x) * 4 + w, gp = wi / PREP_WAVES,
             h = wi - gp * PREP_WAVES;
   if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP) return;
@@ -3150,28 +3158,31 @@ __device__ __forceinline__ bool pp_closure(const Dev &d, int a, int *pl, int &np
       U.y1 = max(U.y1, __shfl_xor(U.y1, o));
     }
     bool added = false;
+    // the members in registers (lane j holds pl[j]): membership tests are
+    // readlane compares, not LDS round trips; pl[] is written back at the end
+    int mine = lane < min(npl, PPG_PL) ? pl[lane] : -1;
+    const int npl0 = npl;
     wave_grid_for(st, it, d.cols, U, expand_for(fmax(rmax0, R)), [&](bool valid, int e) {
       int q = -1;
       if (valid && (d.c_flags[e] & F_ALIVE) &&
-          rect_hit(footprint(d.c_x[e], d.c_y[e], fmax(d.c_r[e], R), d.size), U)) {
+          rect_hit(footprint(d.c_x[e], d.c_y[e], fmax(d.c_r[e], R), d.size), U))
         q = e % NP - a * B;
-        for (int j = 0; j < min(npl, PPG_PL) && q >= 0; j++)
-          if (pl[j] == q) q = -1;  // already in
-      }
+      for (int j = 0; j < min(npl, PPG_PL); j++)  // (j uniform)
+        if (__builtin_amdgcn_readlane(mine, j) == q) q = -1;  // already in
       unsigned long long nb = __ballot(q >= 0);
       while (nb) {  // new players, deduplicated in lane order
         const int l = __ffsll((long long)nb) - 1;
-        nb &= nb - 1;
         const int qq = __builtin_amdgcn_readlane(q, l);
-        bool dup = false;
-        for (int j = 0; j < min(npl, PPG_PL); j++) dup |= pl[j] == qq;
-        if (dup) continue;
-        if (npl < PPG_PL && lane == 0) pl[npl] = qq;
+        nb &= ~__ballot(q == qq);  // (every lane holding the same player)
+        if (npl < PPG_PL && lane == npl) mine = qq;
         npl++;
         added = true;
-        wave_fence();
       }
     }, d.cshift_c);
+    if (npl > npl0) {
+      if (lane < min(npl, PPG_PL) && lane >= npl0) pl[lane] = mine;
+      wave_fence();
+    }
     if (npl > PPG_PL) {
       if (lane == 0) PP_DIAG(2);
       return false;
@@ -4144,7 +4155,7 @@ void launch_pellet_rows(const Dev &d, hipStream_t s) {
 static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr, int resume = 0, int fold = 0) {
   rounds = std::max(rounds, 1);
   const int g = nblk(d.NP, 256);
-  hipLaunchKernelGGL(k_food_prep, dim3(nblk((long)d.NP * PREP_WAVES, 4) + (resume ? 0 : d.A)), dim3(256), 0, s, d,
+  hipLaunchKernelGGL(k_food_prep, dim3(std::max(nblk((long)d.NP * PREP_WAVES, 4), resume ? 0 : d.A)), dim3(256), 0, s, d,
                      rounds, resume);
   for (int r = 1; r <= rounds; r++) {
     hipLaunchKernelGGL(k_food_commit, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0, scr.k, scr.v, rounds,
