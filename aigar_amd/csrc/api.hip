@@ -1293,6 +1293,17 @@ extern "C" int aigar_sync(aigar_handle *h) {
   return check_device_errors(h);
 }
 
+// diagnostics: the first list row (the slot of every player's first cell) and
+// the cell counts, [NP] bytes and [NP] ints (tools/first_slot.py)
+extern "C" int aigar_debug_first_slots(aigar_handle *h, uint8_t *slot0, int *ncells) {
+  if (!h || !slot0 || !ncells) return fail("null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(slot0, h->d.p_list, h->d.NP, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ncells, h->d.p_ncells, sizeof(int) * h->d.NP, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 extern "C" int aigar_profile(aigar_handle *h, int enable) {
   if (!h) return fail("null handle");
   HIPCHK(hipStreamSynchronize(h->stream));
