@@ -224,6 +224,7 @@ struct Dev {
   uint32_t *b_flags;
   uint64_t *b_owner;
   int *bstart, *bitems, *b_rank;
+  uint64_t *bmap;  // [A][64] the blob grid's non-empty coarse buckets (one bit each; blob_grid_place)
   // viruses [A*Vcap]
   double *v_x, *v_y, *v_m, *v_r, *v_vx, *v_vy, *v_svx, *v_svy;
   int *v_svc;

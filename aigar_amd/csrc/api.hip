@@ -430,7 +430,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   AL(b_x, double, E); AL(b_y, double, E); AL(b_m, double, E); AL(b_r, double, E); AL(b_vx, double, E);
   AL(b_vy, double, E); AL(b_svx, double, E); AL(b_svy, double, E); AL(b_svc, int, E); AL(b_seq, int64_t, E);
   AL(b_ej, int64_t, E); AL(b_flags, uint32_t, E); AL(b_owner, uint64_t, E); AL(b_col, int, E);
-  AL(bstart, int, A * H1); AL(bitems, int, E); AL(b_rank, int, E);
+  AL(bstart, int, A * H1); AL(bitems, int, E); AL(b_rank, int, E); AL(bmap, uint64_t, A * 64);
   AL(v_x, double, V); AL(v_y, double, V); AL(v_m, double, V); AL(v_r, double, V); AL(v_vx, double, V);
   AL(v_vy, double, V); AL(v_svx, double, V); AL(v_svy, double, V); AL(v_svc, int, V); AL(v_seq, int64_t, V);
   AL(v_flags, uint32_t, V); AL(v_active, int, V);
@@ -545,6 +545,7 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   HIPCHK(hipMemsetAsync(d.cgcnt, 0, sizeof(int) * A * 2 * 4100, h->stream));
   HIPCHK(hipMemsetAsync(d.vstart, 0, sizeof(int) * A * H1, h->stream));
   HIPCHK(hipMemsetAsync(d.bstart, 0, sizeof(int) * A * H1, h->stream));
+  HIPCHK(hipMemsetAsync(d.bmap, 0, sizeof(uint64_t) * A * 64, h->stream));
   HIPCHK(hipMemsetAsync(d.v_active, 0, sizeof(int) * A * d.Vcap, h->stream));
   HIPCHK(hipMemsetAsync(d.o_lastfov, 0, sizeof(double) * NP, h->stream));
   // Bot.reset (bot.py:125-164): currentAction None (NN) / [0, 0, 0, 0] (Greedy, Random)

@@ -1248,8 +1248,10 @@ __device__ __forceinline__ void cgrid_count_cell(const Dev &d, int a, size_t ci,
 // values in LDS), and the counts back to zero for the next tick
 // (256 threads) bucket starts of n <= SG_CAP counts (16-byte aligned, kept in
 // registers: 16 per thread, one int4 load round), written to start[0..n] and,
-// when lds is given, to lds[0..n]; the counts are re-zeroed for the next tick
-__device__ void count_scan_256(int *cnt, int n, int *start, int *lds) {
+// when lds is given, to lds[0..n]; the counts are re-zeroed for the next tick;
+// bits (optional): one bit per non-empty bucket, 16 per thread (bucket b at bit
+// b % 16 of bits[b / 16]: a little-endian bitmap)
+__device__ void count_scan_256(int *cnt, int n, int *start, int *lds, uint16_t *bits) {
   __shared__ int wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int4 *c4 = reinterpret_cast<const int4 *>(cnt);
@@ -1265,6 +1267,12 @@ __device__ void count_scan_256(int *cnt, int n, int *start, int *lds) {
   }
 #pragma unroll
   for (int k = 0; k < 16; k++) sum += v[k];
+  if (bits) {
+    uint32_t bm = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) bm |= (v[k] != 0 ? 1u : 0u) << k;
+    bits[tid] = (uint16_t)bm;
+  }
   int inc = sum;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1293,7 +1301,7 @@ __device__ void count_scan_256(int *cnt, int n, int *start, int *lds) {
 }
 __device__ void cgrid_scan_block(const Dev &d, int a) {
   const int cc = cgrid_cols(d);
-  count_scan_256(cgrid_counts(d, a, 0), cc * cc, d.cstart + (size_t)a * (d.H + 1), nullptr);
+  count_scan_256(cgrid_counts(d, a, 0), cc * cc, d.cstart + (size_t)a * (d.H + 1), nullptr, nullptr);
 }
 // step 3 for player gp's n cells (k_food_commit round 1)
 __device__ __forceinline__ void cgrid_place_player(const Dev &d, int gp, int n) {
@@ -1533,14 +1541,17 @@ __device__ __forceinline__ void vb_active_blob(const Dev &d, int gb) {
 // the blob grid's second step (blob_count): one block per arena loads the
 // counts (re-zeroing them for the next tick), scans them in LDS, stores the
 // bucket starts and places every ranked blob
-__device__ void count_scan_256(int *cnt, int n, int *start, int *lds);
+__device__ void count_scan_256(int *cnt, int n, int *start, int *lds, uint16_t *bits);
 __device__ void blob_grid_place(const Dev &d, int a, int *cnt) {
   const int tid = threadIdx.x, T = blockDim.x, s = d.cshift;
   const int cc = (d.cols + (1 << s) - 1) >> s;
   const int n = d.ctl[a].n_blob;
   int *items = d.bitems + (size_t)a * d.Ecap;
   const int *rank = d.b_rank + (size_t)a * d.Ecap;
-  count_scan_256(cgrid_counts(d, a, 1), cc * cc, d.bstart + (size_t)a * (d.H + 1), cnt);
+  // (+ the non-empty buckets as a bitmap, which k_food_prep keeps in LDS to
+  // skip the blob walk of a box that holds none)
+  count_scan_256(cgrid_counts(d, a, 1), cc * cc, d.bstart + (size_t)a * (d.H + 1), cnt,
+                 reinterpret_cast<uint16_t *>(d.bmap + (size_t)a * 64));
   __syncthreads();
   for (int i = tid; i < n; i += T) {
     const int rk = rank[i];
@@ -2035,6 +2046,19 @@ struct Food {
       wave_grid_for(d.bstart + (size_t)a * (d.H + 1), d.bitems + (size_t)a * d.Ecap, d.cols, q, 1,
                     [&](bool valid, int j) { f(valid, valid ? (j | kBlobBit) : -1); }, d.cshift);
   }
+  // whether the blob grid's buckets around q (the walk's own span) hold any blob,
+  // from the bitmap bm (the arena's 64 words, in LDS): every lane tests one bucket
+  __device__ bool blobs_near(Rect q, const uint64_t *bm) const {
+    if (!any_blobs() || q.x1 < q.x0 || q.y1 < q.y0) return false;
+    const Span g = grid_span(q, 1, d.cols, d.cshift);
+    const int w = g.bx1 - g.bx0 + 1, nb = w * (g.by1 - g.by0 + 1);
+    bool any = false;
+    for (int i = threadIdx.x & 63; i < nb; i += 64) {
+      const int b = (g.by0 + i / w) * g.stride + g.bx0 + i % w;
+      any |= (bm[b >> 6] >> (b & 63)) & 1;
+    }
+    return __ballot(any) != 0;
+  }
   // order of a cell's food list: pellets by creation sequence, then blobs
   __device__ static int64_t order_key(int j, int64_t sq) { return sq | (blob(j) ? (1ll << 62) : 0); }
 };
@@ -2080,6 +2104,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   __shared__ double s_x[4][PREP_CAND], s_y[4][PREP_CAND], s_m[4][PREP_CAND];
   __shared__ int s_idx[4][PREP_CAND];
   __shared__ uint8_t s_sel[4][PREP_CAND];
+  __shared__ uint64_t s_bm[4][64];  // each wave's arena blob bitmap (blob_grid_place)
   // blocks [0, A) when not resuming first run the player-cell grid's scan for
   // arena blockIdx.x (cgrid_scan_block; read by the commit round), then their
   // players: as extra blocks they were the 1025th block of a launch whose 1024
@@ -2094,6 +2119,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   // this wave's first list row rides the liveness / count load round (the row
   // exists whatever the count: h < PREP_WAVES <= kMaxCells)
   const int s_first = uni((int)d.p_list[h * d.NP + gp]);
+  s_bm[w][lane] = d.bmap[(size_t)(gp / d.B) * 64 + lane];  // (read after the pellet walk: its waits cover it)
   if (!d.p_alive[gp]) return;  // uniform per wave
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   Food F(d, a);
@@ -2173,7 +2199,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
       }
       cnt += __popcll(bal);
     };
-    F.walk_blobs(qb, visit_b);
+    if (F.blobs_near(qb, s_bm[w])) F.walk_blobs(qb, visit_b);  // (most boxes hold no blob: no row round)
     PT_MARK(0, 4);
     // upper bound of the mass / radius this cell can reach while eating (grow is monotone);
     // before its first bite the radius may still be the stale pre-eject one (cell.py:90-94)
