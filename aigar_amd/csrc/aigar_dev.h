@@ -55,6 +55,7 @@ struct ArenaCtl {
   int n_blob;         // blob slots in use
   int n_blob_base;    // blob count before this tick's ejections
   int n_blob_add;     // this tick's ejections (n_blob moves in k_players' last block)
+  int n_blob_live;    // live blobs at this tick's blob grid (blob_grid_place): the holes' share
   int n_vir;          // virus slots in use
   int n_vir_start;    // viruses that existed when virusBlobOverlap started
   int n_dead;         // deadPlayers list length

@@ -1553,6 +1553,7 @@ __device__ void blob_grid_place(const Dev &d, int a, int *cnt) {
   count_scan_256(cgrid_counts(d, a, 1), cc * cc, d.bstart + (size_t)a * (d.H + 1), cnt,
                  reinterpret_cast<uint16_t *>(d.bmap + (size_t)a * 64));
   __syncthreads();
+  if (tid == 0) d.ctl[a].n_blob_live = cnt[cc * cc];  // (k_spawn_plan: whether the list needs compacting)
   for (int i = tid; i < n; i += T) {
     const int rk = rank[i];
     if (rk < 0) continue;
@@ -3439,7 +3440,18 @@ __device__ void spawn_pos(const Dev &d, int a, double radius, const uint64_t u[4
   oy = (double)yp;
 }
 
-__device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait);
+// the arena fields spawn_counts reads, loaded by its thread before the dead
+// list's partition (their load round overlaps it)
+struct SpawnIn {
+  int n_pel, n_pel_eaten, n_pnew, n_pel_glob, n_eaten_glob, n_vir;
+  int64_t seq_next, tick, stat3, stat5;
+  uint64_t ctr_pellet, ctr_virus;
+};
+__device__ __forceinline__ SpawnIn spawn_in(const ArenaCtl &c) {
+  return SpawnIn{c.n_pel,    c.n_pel_eaten, c.n_pnew,    c.n_pel_glob, c.n_eaten_glob, c.n_vir,
+                 c.seq_next, c.tick,        c.stat[3],   c.stat[5],    c.ctr_pellet,   c.ctr_virus};
+}
+__device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait, const SpawnIn &in);
 // ---------------------------------------------------- closing pellet update
 // Pellets never move and only a few change per tick (eaten, spawned, converted
 // from blobs): the closing update (k_pel_update) rewrites only the bucket rows
@@ -3494,6 +3506,10 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   const uint32_t dirty = c.dirty;
   for (int kind = 0; kind < 2; kind++) {
     if (!(dirty & (kind == 0 ? DIRTY_VIRUS : DIRTY_BLOB))) continue;
+    // blobs die every tick (stopped ones turn into pellets): the list keeps its
+    // holes -- every consumer tests F_ALIVE and orders by seq -- until they are
+    // half of it or it nears its capacity, so most ticks skip this pass
+    if (kind == 1 && c.n_blob < 2 * c.n_blob_live + 256 && c.n_blob < d.Ecap / 2) continue;
     int n = kind == 0 ? c.n_vir : c.n_blob;
     int cap = kind == 0 ? d.Vcap : d.Ecap;
     int out = 0;
@@ -3558,6 +3574,8 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
   // player's respawn slot (its place in the respawn order, -1 = waits) is
   // what k_pel_update's player threads read
   int n_resp = 0, n_wait = 0;
+  SpawnIn sin{};
+  if (tid == 0) sin = spawn_in(c);  // (spawn_counts' fields: their round overlaps the partition's)
   if (!init) {
     const int nd = c.n_dead;
     int *dl = d.dead + (size_t)a * d.B, *rl = d.resp_slot + (size_t)a * d.B;
@@ -3578,7 +3596,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
       n_wait += tw;
     }
   }
-  if (tid == 0) spawn_counts(d, a, init, n_resp, n_wait);
+  if (tid == 0) spawn_counts(d, a, init, n_resp, n_wait, sin);
   __syncthreads();
   PT_MARK(5, 4);
   if (close) {
@@ -3590,50 +3608,57 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
 
 // spawnStuff's counts (field.py:227-280): pellets and viruses to add, players to respawn
 // (n_resp / n_wait: the dead list's partition, done by the caller's block when !init)
-__device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait) {
+// in: every field it reads, loaded in ONE round (spawn_in) before the arithmetic
+// and the stores (read-modify-writes of the struct in place cost a round each: a
+// load after a store to the same struct cannot move above it)
+__device__ __forceinline__ void spawn_counts(const Dev &d, int a, int init, int n_resp, int n_wait, const SpawnIn &in) {
   ArenaCtl &c = d.ctl[a];
-  c.dirty = 0;
+  const int n_pel = in.n_pel, n_pel_eaten = in.n_pel_eaten, n_pnew = in.n_pnew;
+  const int n_pel_glob = in.n_pel_glob, n_eaten_glob = in.n_eaten_glob, n_vir = in.n_vir;
+  const int64_t seq_next = in.seq_next, tick = in.tick, stat3 = in.stat3, stat5 = in.stat5;
+  const uint64_t ctr_pellet = in.ctr_pellet, ctr_virus = in.ctr_virus;
+  uint32_t err = 0;
   // spawnPellets: while len(pellets) < maxCollectibleCount
   // (tiles: the global count -- every tile spawns the same global list and keeps what it holds)
-  int alive_p = d.tiled ? c.n_pel_glob - c.n_eaten_glob + c.n_pnew : c.n_pel - c.n_pel_eaten + c.n_pnew;
+  const int alive_p = d.tiled ? n_pel_glob - n_eaten_glob + n_pnew : n_pel - n_pel_eaten + n_pnew;
   int kp = 0;
   if ((double)alive_p < d.max_pellets) kp = (int)ceil(d.max_pellets) - alive_p;
-  if (alive_p + kp > d.Pcap || c.n_pnew + kp > d.Pcap) {
-    c.err |= ERR_PELLET_CAP;
-    kp = max(0, min(d.Pcap - alive_p, d.Pcap - c.n_pnew));
-  }
-  c.seq_base_spawn = c.seq_next;
-  c.seq_next += kp;
-  c.ctr_pellet_base = c.ctr_pellet;
-  c.ctr_pellet += kp;
-  c.n_spawn_p = kp;
-  c.n_pel_glob = alive_p + kp;
-  if (!init) {  // diagnostics: pellets eaten / respawned this tick (whole arena)
-    c.stat[3] += d.tiled ? c.n_eaten_glob : c.n_pel_eaten;
-    c.stat[5] += kp;
+  if (alive_p + kp > d.Pcap || n_pnew + kp > d.Pcap) {
+    err |= ERR_PELLET_CAP;
+    kp = max(0, min(d.Pcap - alive_p, d.Pcap - n_pnew));
   }
   // spawnViruses
   int kv = 0;
-  if (d.virus_enabled && (double)c.n_vir < d.max_viruses) kv = (int)ceil(d.max_viruses) - c.n_vir;
-  if (c.n_vir + kv > d.Vcap) {
-    c.err |= ERR_VIRUS_CAP;
-    kv = d.Vcap - c.n_vir;
+  if (d.virus_enabled && (double)n_vir < d.max_viruses) kv = (int)ceil(d.max_viruses) - n_vir;
+  if (n_vir + kv > d.Vcap) {
+    err |= ERR_VIRUS_CAP;
+    kv = d.Vcap - n_vir;
   }
-  c.seq_next += kv;
-  c.ctr_virus_base = c.ctr_virus;
-  c.ctr_virus += kv;
-  c.vir_base_spawn = c.n_vir;
-  c.n_spawn_v = kv;
-  c.n_vir += kv;
   // spawnPlayers: deadPlayers in order, respawnTime == 0 (init: every player, in order)
-  int np = d.B;
+  const int np = init ? d.B : n_resp;
+  c.dirty = 0;
+  if (err) c.err |= err;
+  c.seq_base_spawn = seq_next;
+  c.ctr_pellet_base = ctr_pellet;
+  c.ctr_pellet = ctr_pellet + kp;
+  c.n_spawn_p = kp;
+  c.n_pel_glob = alive_p + kp;
+  if (!init) {  // diagnostics: pellets eaten / respawned this tick (whole arena)
+    c.stat[3] = stat3 + (d.tiled ? n_eaten_glob : n_pel_eaten);
+    c.stat[5] = stat5 + kp;
+  }
+  c.ctr_virus_base = ctr_virus;
+  c.ctr_virus = ctr_virus + kv;
+  c.vir_base_spawn = n_vir;
+  c.n_spawn_v = kv;
+  c.n_vir = n_vir + kv;
   if (!init) {
-    np = n_resp;
     c.n_dead = n_wait;
-    c.tick_sp = c.tick;
+    c.tick_sp = tick;
   }
   c.n_spawn_pl = np;
-  if (!init) c.seq_next += np;  // at initialize() players already own seqs 0..B-1
+  // (at initialize() players already own seqs 0..B-1)
+  c.seq_next = seq_next + kp + kv + (init ? 0 : np);
 }
 
 __global__ void k_pnew_commit(Dev d) {
