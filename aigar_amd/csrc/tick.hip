@@ -96,6 +96,13 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
       g_ptw[6][a][k_] += pa_acc_[k_];                                           \
       g_ptw[7][a][k_] += pa_cnt_[k_];                                           \
     }
+// (the parallel pp groups' waves: summed over the waves, at index 1024 + a)
+#define PA_STORE_GROUP(a)                                                       \
+  if ((threadIdx.x & 63) == 0 && 1024 + (a) < kPtWaves)                         \
+    for (int k_ = 0; k_ < 8; k_++) {                                            \
+      atomicAdd(&g_ptw[6][1024 + (a)][k_], pa_acc_[k_]);                        \
+      atomicAdd(&g_ptw[7][1024 + (a)][k_], pa_cnt_[k_]);                        \
+    }
 #define PT_ARGS , pt0_, pt_w_
 #define PT_ARGS , pt0_, pt_w_
 #else
@@ -104,6 +111,7 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
 #define PT_PARAMS
 #define PT_ARGS
 #define PA_DECL
+#define PA_STORE_GROUP(a)
 #define PA_T(k)
 #define PA_C(k)
 #define PA_ADD(k, v)
@@ -2886,10 +2894,26 @@ struct PPL {  // a turn's candidate lists (LDS) and their capacity
   double *x, *y, *m, *r;
   int cap;
 };
+// A parallel group's cell table (LDS, one per group wave): every live cell of
+// the group's closure -- pool index, position, current mass and radius, seq,
+// liveness -- kept current by the group's own eats.  The closure holds every
+// cell a turn of the group can gather, eat, be eaten by or re-activate (the
+// closure's definition, pp_closure), so the group's candidate gathers and
+// re-activation walks scan this table instead of walking the grid (three
+// dependent global rounds each).
+constexpr int PPT_CAP = 64;  // (= PPG_CELLS: a closure holds at most that many cells)
+struct PPT {
+  int *e;
+  double *x, *y, *m, *r;
+  int64_t *seq;
+  uint8_t *al;
+  int n;
+};
 // odirty: the deferred occupancy's dirty-word bitmap (LDS, zeroed), or NULL for
 // immediate updates; dkey / n_dead0: a parallel group (see remove_cell)
+// tab: a parallel group's cell table (its gathers and walks scan it), or NULL
 __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, const PPL &L, uint32_t *odirty, double &rmax,
-                         int64_t *dkey, int n_dead0) {
+                         int64_t *dkey, int n_dead0, const PPT *tab = nullptr) {
   const int lane = threadIdx.x & 63;
   PA_DECL;
   const int B = d.B, NW = (B + 31) / 32;
@@ -2945,7 +2969,32 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
       const Rect q0 = footprint(px, py, pr, d.size);  // (cell_rect)
       PA_T(1);
       int nc = 0;
-      wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
+      int pci = -1;  // (table mode: the turn cell's table row)
+      if (tab) {
+        // candidates from the group's table: s_val holds the table row
+        for (int r0 = 0; r0 < tab->n; r0 += 64) {
+          const int t = r0 + lane;
+          bool keep = false;
+          if (t < tab->n && tab->al[t]) {
+            const int e = tab->e[t];
+            if ((size_t)e == pc) pci = t;
+            keep = (e % NP) != gp && rect_hit(footprint(tab->x[t], tab->y[t], tab->r[t], d.size), q0);
+          }
+          unsigned long long bal = __ballot(keep);
+          int slot = nc + __popcll(bal & lt);
+          if (keep && slot < L.cap) {
+            s_key[slot] = tab->seq[t];
+            s_val[slot] = t;
+            s_x[slot] = tab->x[t];
+            s_y[slot] = tab->y[t];
+            s_m[slot] = tab->m[t];
+            s_r[slot] = tab->r[t];
+          }
+          nc += __popcll(bal);
+        }
+        const unsigned long long fb = __ballot(pci >= 0);
+        pci = fb ? __builtin_amdgcn_readlane(pci, __ffsll((long long)fb) - 1) : -1;
+      } else wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
         double ex = 0, ey = 0, er = 0;
         bool keep = valid && (d.c_flags[e] & F_ALIVE) && (e % NP) != gp;
         if (keep) {
@@ -2984,7 +3033,7 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
       PA_T(3);
       for (int t = 0; t < nc; t++) {
         const int k = s_srt[t];
-        const size_t o = (size_t)s_val[k];
+        const size_t o = tab ? (size_t)tab->e[s_val[k]] : (size_t)s_val[k];
         const double ox = s_x[k], oy = s_y[k], om = s_m[k], orr = s_r[k];
         if (!overlap(px, py, pm, pr, ox, oy, om, orr)) continue;
         size_t g, v;
@@ -3022,6 +3071,14 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
         }
         rmax = fmax(rmax, mr);
         remove_cell(d, a, v, order, lane == 0, dkey, n_dead0);
+        if (tab && lane == 0) {  // (the group's table follows its eats)
+          const int gi = pc_eats ? pci : s_val[k], vi = pc_eats ? s_val[k] : pci;
+          if (gi >= 0) {
+            tab->m[gi] = m;
+            tab->r[gi] = mr;
+          }
+          if (vi >= 0) tab->al[vi] = 0;
+        }
         // re-activate every later turn whose outcome the growth of g may change
         const int gpl = (int)(g % NP);
         const double gx = pc_eats ? px : ox, gy = pc_eats ? py : oy, gm = m, gr = mr;
@@ -3029,13 +3086,22 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
         PA_T(4);
         PA_C(2);
         // (cell_rect(d, g) from the registers: g's position and its new radius)
-        wave_grid_for(st, it, d.cols, footprint(gx, gy, gr, d.size), expand_for(rmax), [&](bool valid, int e) {
-          if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gpl) return;
-          if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;
+        auto react = [&](bool valid, int e, double ex, double ey, double em, double er) {
+          if (!valid || (int)(e % NP) == gpl) return;
+          if (!overlap(gx, gy, gm, gr, ex, ey, em, er)) return;
           active_st(d, (size_t)e, 1);
           int pe = (int)(e % NP) - a * B;
           if (pe > P) atomicOr(&pend[pe >> 5], 1u << (pe & 31));
-        }, d.cshift_c);
+        };
+        if (tab) {
+          for (int t = lane; t < tab->n; t += 64)
+            react(tab->al[t] != 0, tab->e[t], tab->x[t], tab->y[t], tab->m[t], tab->r[t]);
+        } else {
+          wave_grid_for(st, it, d.cols, footprint(gx, gy, gr, d.size), expand_for(rmax), [&](bool valid, int e) {
+            if (!valid || !(d.c_flags[e] & F_ALIVE)) return;
+            react(true, e, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e]);
+          }, d.cshift_c);
+        }
         active_st(d, g, 1);
         if (gpl - a * B > P && lane == 0) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
         wave_fence();
@@ -3047,16 +3113,23 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
           if (i - 1 < d.p_ncells[gp]) {
             const size_t sk = (size_t)d.p_list[(i - 1) * NP + gp] * NP + gp;
             const double sx = d.c_x[sk], sy = d.c_y[sk], sm = d.c_m[sk], sr = d.c_r[sk];
-            wave_grid_for(st, it, d.cols, footprint(sx, sy, sr, d.size), expand_for(rmax), [&](bool valid, int e) {
-              if (!valid || !(d.c_flags[e] & F_ALIVE) || (int)(e % NP) == gp) return;
-              const double me = d.c_m[e];
-              if (!(overlap(sx, sy, sm, sr, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(sm, me) || can_eat(me, sm))))
-                return;
+            auto partner = [&](bool valid, int e, double ex, double ey, double me, double er) {
+              if (!valid || (int)(e % NP) == gp) return;
+              if (!(overlap(sx, sy, sm, sr, ex, ey, me, er) && (can_eat(sm, me) || can_eat(me, sm)))) return;
               int pe = (int)(e % NP) - a * B;
               if (pe <= P) return;
               active_st(d, (size_t)e, 1);
               atomicOr(&pend[pe >> 5], 1u << (pe & 31));
-            }, d.cshift_c);
+            };
+            if (tab) {
+              for (int t = lane; t < tab->n; t += 64)
+                partner(tab->al[t] != 0, tab->e[t], tab->x[t], tab->y[t], tab->m[t], tab->r[t]);
+            } else {
+              wave_grid_for(st, it, d.cols, footprint(sx, sy, sr, d.size), expand_for(rmax), [&](bool valid, int e) {
+                if (!valid || !(d.c_flags[e] & F_ALIVE)) return;
+                partner(true, e, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e]);
+              }, d.cshift_c);
+            }
             wave_fence();
           }
           PA_T(6);
@@ -3067,7 +3140,11 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
     }
   }
   PA_T(7);
-  if (!dkey) PA_STORE(a);
+  if (!dkey) {
+    PA_STORE(a);
+  } else {
+    PA_STORE_GROUP(a);
+  }
 }
 // the whole pass in one wavefront (nw pending players in d.work)
 // L: the candidates of the current turn, with their state at turn start (only
@@ -3235,6 +3312,12 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   __shared__ int g_val[PPG_WAVES][PPG_CELLS], g_srt[PPG_WAVES][PPG_CELLS];
   __shared__ double g_x[PPG_WAVES][PPG_CELLS], g_y[PPG_WAVES][PPG_CELLS], g_m[PPG_WAVES][PPG_CELLS],
       g_r[PPG_WAVES][PPG_CELLS];
+#if AIGAR_PP_MERGE
+  __shared__ int t_e[PPG_WAVES][PPT_CAP];  // the group waves' cell tables (PPT)
+  __shared__ double t_x[PPG_WAVES][PPT_CAP], t_y[PPG_WAVES][PPT_CAP], t_m[PPG_WAVES][PPT_CAP], t_r[PPG_WAVES][PPT_CAP];
+  __shared__ int64_t t_seq[PPG_WAVES][PPT_CAP];
+  __shared__ uint8_t t_al[PPG_WAVES][PPT_CAP];
+#endif
   ArenaCtl &c = d.ctl[a];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nwv = blockDim.x >> 6, T = blockDim.x;
   if (tid == 0) {  // (every thread reads the count before it is reset)
@@ -3352,27 +3435,75 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     for (int i = lane; i < NW; i += 64) mine[i] = 0;
     wave_fence();
 #if AIGAR_PP_MERGE
-    // group g (the g-th root) runs in wave g % PPG_WAVES: every seed of it
-    for (int sd = 0; sd < nw; sd++) {
-      const int rt = s_root[sd];
-      int g = 0;
-      for (int k = lane; k < rt; k += 64) g += s_root[k] == k;
-      for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
-      if (g % PPG_WAVES != w) continue;
-      const int P = d.work[(size_t)a * d.Wcap + sd];
-      if (lane == 0) mine[P >> 5] |= 1u << (P & 31);
+    // group g (the g-th root) runs in wave g % PPG_WAVES, one group after the
+    // other (groups are independent): its seeds' pending bits, its cell table
+    // (every live cell of its closure: one load round), its turns
+    double rmax = c.rmax_cell;
+    const PPT tab0{t_e[w], t_x[w], t_y[w], t_m[w], t_r[w], t_seq[w], t_al[w], 0};
+    int g = 0;  // roots before rt
+    for (int rt = 0; rt < nw; rt++) {
+      if (s_root[rt] != rt) continue;
+      const bool mineg = g % PPG_WAVES == w;
+      g++;
+      if (!mineg) continue;
+      for (int sd = rt; sd < nw; sd++)
+        if (s_root[sd] == rt && lane == 0) {
+          const int P = d.work[(size_t)a * d.Wcap + sd];
+          mine[P >> 5] |= 1u << (P & 31);
+        }
+      PPT tab = tab0;
+      const int npl = s_npl[rt];
+      int nt = 0;
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++) {  // (player j, slot) pairs, four per lane
+        const int pr = lane + 64 * kk, j = pr >> 4;
+        bool keep = false;
+        size_t ci = 0;
+        double x = 0, y = 0, m = 0, r = 0;
+        int64_t sq = 0;
+        if (j < npl) {
+          ci = (size_t)(pr & 15) * d.NP + (size_t)a * d.B + s_pl[rt][j];
+          keep = (d.c_flags[ci] & F_ALIVE) != 0;
+          x = d.c_x[ci];
+          y = d.c_y[ci];
+          m = d.c_m[ci];
+          r = d.c_r[ci];
+          sq = d.c_seq[ci];
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int slot = nt + __popcll(bal & ((1ull << lane) - 1));
+        if (keep && slot < PPT_CAP) {
+          tab.e[slot] = (int)ci;
+          tab.x[slot] = x;
+          tab.y[slot] = y;
+          tab.m[slot] = m;
+          tab.r[slot] = r;
+          tab.seq[slot] = sq;
+          tab.al[slot] = 1;
+        }
+        nt += __popcll(bal);
+      }
+      if (nt > PPT_CAP) {  // (a closure holds at most PPG_CELLS cells: cannot happen)
+        if (lane == 0) set_err(d, a, ERR_CAND_CAP);
+        nt = PPT_CAP;
+      }
+      tab.n = nt;
+      wave_fence();
+      pp_turns(d, a, mine, PPL{g_key[w], g_val[w], g_srt[w], g_x[w], g_y[w], g_m[w], g_r[w], PPG_CELLS}, odirty,
+               rmax, scr_k + (size_t)a * d.Wcap, dead0, &tab);
     }
+    if (lane == 0) s_rmax[w] = rmax;
 #else
     for (int sd = w; sd < nw; sd += PPG_WAVES) {
       const int P = d.work[(size_t)a * d.Wcap + sd];
       if (lane == 0) mine[P >> 5] |= 1u << (P & 31);
     }
-#endif
     wave_fence();
     double rmax = c.rmax_cell;
     pp_turns(d, a, mine, PPL{g_key[w], g_val[w], g_srt[w], g_x[w], g_y[w], g_m[w], g_r[w], PPG_CELLS}, odirty,
              rmax, scr_k + (size_t)a * d.Wcap, dead0);
     if (lane == 0) s_rmax[w] = rmax;
+#endif
   }
   __syncthreads();
   PT_MARK(5, 7);

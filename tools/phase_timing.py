@@ -61,6 +61,8 @@ def run(steps, policy="random"):
         assert L.aigar_debug_phase_times(ptr, iptr, C.byref(khz), 0) == 0
         pa_acc = pa_acc + buf[6, 0, :].astype(np.float64) if "pa_acc" in dir() else buf[6, 0, :].astype(np.float64)
         pa_cnt = pa_cnt + buf[7, 0, :].astype(np.float64) if "pa_cnt" in dir() else buf[7, 0, :].astype(np.float64)
+        pg_acc = pg_acc + buf[6, 1024, :].astype(np.float64) if "pg_acc" in dir() else buf[6, 1024, :].astype(np.float64)
+        pg_cnt = pg_cnt + buf[7, 1024, :].astype(np.float64) if "pg_cnt" in dir() else buf[7, 1024, :].astype(np.float64)
         for k in KERNELS:
             started = buf[k, :, 0] != 0
             if not started.any():
@@ -103,6 +105,12 @@ def run(steps, policy="random"):
             "%s %.2f us" % (nm, pa_acc[k] * us / steps) for k, nm in enumerate(names)))
         print("pp serial pass counts per step: turns %.2f, gathers %.2f, eats %.2f, pc eaten %.2f, candidates %.2f" % tuple(
             pa_cnt[k] / steps for k in (0, 1, 2, 3, 4)))
+    if "pg_acc" in dir():  # the parallel groups' waves, arena 0, summed over waves
+        names = ["setup", "turn start", "gather walk", "rank", "eat", "re-activation walk", "skip+reload", "rest"]
+        print("pp group waves (arena 0, per step, summed over waves): " + ", ".join(
+            "%s %.2f us" % (nm, pg_acc[k] * us / steps) for k, nm in enumerate(names)))
+        print("pp group waves counts per step: turns %.2f, gathers %.2f, eats %.2f, pc eaten %.2f, candidates %.2f" % tuple(
+            pg_cnt[k] / steps for k in (0, 1, 2, 3, 4)))
     khz_ = khz.value / 1e3
     for k in KERNELS:
         row = []
