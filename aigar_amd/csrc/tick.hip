@@ -104,8 +104,15 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
       atomicAdd(&g_ptw[7][1024 + (a)][k_], pa_cnt_[k_]);                        \
     }
 #define PT_ARGS , pt0_, pt_w_
-#define PT_ARGS , pt0_, pt_w_
+// block-level sub-marks of k_spawn_plan's pp pass (g_ptw[6][2048 + block][k]: time from the wave's start)
+#define PT_SUB(k)                                                                                 \
+  do {                                                                                            \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                   \
+    if (threadIdx.x == 0 && 2048 + blockIdx.x < kPtWaves)                                         \
+      g_ptw[6][2048 + blockIdx.x][k] = (unsigned)(wall_clock64() - pt0_);                         \
+  } while (0)
 #else
+#define PT_SUB(k)
 #define PT_BEGIN(k)
 #define PT_MARK(k, m)
 #define PT_PARAMS
@@ -2829,10 +2836,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
 }
 
 // removes cell e (pool index) from its player's list; returns true if the player died
-// (dkey: a parallel pp group -- the death takes a dead-list slot by atomic and
-// records its turn key there, for the sort into turn order after the pass)
-__device__ __forceinline__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool writer = true,
-                            int64_t *dkey = nullptr, int n_dead0 = 0) {
+__device__ __forceinline__ bool remove_cell(const Dev &d, int a, size_t e, uint64_t &order, bool writer = true) {
   const int NP = d.NP;
   int gp = (int)(e % NP);
   uint8_t slot = (uint8_t)(e / NP);
@@ -2852,17 +2856,7 @@ __device__ __forceinline__ bool remove_cell(const Dev &d, int a, size_t e, uint6
     ArenaCtl &c = d.ctl[a];
     d.p_alive[gp] = 0;
     d.p_respawn[gp] = 1;
-    if (dkey) {
-      int sl = 0;
-      if ((threadIdx.x & 63) == 0) sl = atomicAdd(&c.n_dead, 1);
-      sl = __shfl(sl, 0);
-      if ((threadIdx.x & 63) == 0) {
-        d.dead[(size_t)a * d.B + sl] = gp - a * d.B;
-        dkey[sl - n_dead0] = (int64_t)order;
-      }
-    } else {
-      d.dead[(size_t)a * d.B + c.n_dead++] = gp - a * d.B;
-    }
+    d.dead[(size_t)a * d.B + c.n_dead++] = gp - a * d.B;
     if (writer) ev_push(d, a, PH_PP, order, 9, gp - a * d.B, d.c_seq[e]);
     order++;
     return true;
@@ -2903,17 +2897,45 @@ struct PPL {  // a turn's candidate lists (LDS) and their capacity
 // dependent global rounds each).
 constexpr int PPT_CAP = 64;  // (= PPG_CELLS: a closure holds at most that many cells)
 struct PPT {
-  int *e;
-  double *x, *y, *m, *r;
-  int64_t *seq;
-  uint8_t *al;
-  int n;
+  int *e;                       // [row] pool index
+  double *x, *y, *m, *r;        // [row] position, mass, radius
+  int64_t *seq;                 // [row] creation sequence
+  uint8_t *al, *act;            // [row] alive, active (c_active)
+  int *pid;                     // [member] arena player index
+  uint8_t *pn, *pal, *pl;       // [member] live count, alive; [member][k] live list (slots)
+  int8_t *row;                  // [member][slot] the slot's table row, -1 if not live
+  int n, np;                    // rows, members
 };
+// the first pending player at or after q: one bitmap word per lane, a ballot
+// picks the first non-empty one (a turn's scan is one LDS round, not one per word)
+__device__ __forceinline__ int pend_next(const uint32_t *pend, int NW, int q) {
+  const int lane = threadIdx.x & 63;
+  for (int wb = q >> 5; wb < NW; wb += 64) {
+    const int wd = wb + lane;
+    uint32_t bits = wd < NW ? pend[wd] : 0u;
+    if (wd == (q >> 5)) bits &= (q & 31) ? ~((1u << (q & 31)) - 1) : 0xFFFFFFFFu;
+    const unsigned long long bal = __ballot(bits != 0);
+    if (bal) {
+      const int l = __ffsll((long long)bal) - 1;
+      const uint32_t bw = (uint32_t)__builtin_amdgcn_readlane((int)bits, l);
+      return (wb + l) * 32 + __ffs(bw) - 1;
+    }
+  }
+  return -1;
+}
+// srt[rank] = index, ranks by creation sequence (keys are unique)
+__device__ __forceinline__ void rank_by_key(const int64_t *key, int *srt, int nc) {
+  for (int x = threadIdx.x & 63; x < nc; x += 64) {
+    const int64_t k = key[x];
+    int rk = 0;
+    for (int y = 0; y < nc; y++) rk += key[y] < k;
+    srt[rk] = x;
+  }
+  wave_fence();
+}
 // odirty: the deferred occupancy's dirty-word bitmap (LDS, zeroed), or NULL for
-// immediate updates; dkey / n_dead0: a parallel group (see remove_cell)
-// tab: a parallel group's cell table (its gathers and walks scan it), or NULL
-__device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, const PPL &L, uint32_t *odirty, double &rmax,
-                         int64_t *dkey, int n_dead0, const PPT *tab = nullptr) {
+// immediate updates
+__device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, const PPL &L, uint32_t *odirty, double &rmax) {
   const int lane = threadIdx.x & 63;
   PA_DECL;
   const int B = d.B, NW = (B + 31) / 32;
@@ -2927,22 +2949,7 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
   PA_T(0);
   int P = -1;
   for (;;) {
-    // next pending player > P: 64 bitmap words per step, one per lane, and a
-    // ballot picks the first non-empty one (a turn's scan is one LDS round, not
-    // one per word)
-    const int q = P + 1;
-    int found = -1;
-    for (int wb = q >> 5; wb < NW && found < 0; wb += 64) {
-      const int wd = wb + lane;
-      uint32_t bits = wd < NW ? pend[wd] : 0u;
-      if (wd == (q >> 5)) bits &= (q & 31) ? ~((1u << (q & 31)) - 1) : 0xFFFFFFFFu;
-      const unsigned long long bal = __ballot(bits != 0);
-      if (bal) {
-        const int l = __ffsll((long long)bal) - 1;
-        const uint32_t bw = (uint32_t)__builtin_amdgcn_readlane((int)bits, l);
-        found = (wb + l) * 32 + __ffs(bw) - 1;
-      }
-    }
+    const int found = pend_next(pend, NW, P + 1);
     if (found < 0) break;
     P = found;
     wave_fence();
@@ -2969,32 +2976,7 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
       const Rect q0 = footprint(px, py, pr, d.size);  // (cell_rect)
       PA_T(1);
       int nc = 0;
-      int pci = -1;  // (table mode: the turn cell's table row)
-      if (tab) {
-        // candidates from the group's table: s_val holds the table row
-        for (int r0 = 0; r0 < tab->n; r0 += 64) {
-          const int t = r0 + lane;
-          bool keep = false;
-          if (t < tab->n && tab->al[t]) {
-            const int e = tab->e[t];
-            if ((size_t)e == pc) pci = t;
-            keep = (e % NP) != gp && rect_hit(footprint(tab->x[t], tab->y[t], tab->r[t], d.size), q0);
-          }
-          unsigned long long bal = __ballot(keep);
-          int slot = nc + __popcll(bal & lt);
-          if (keep && slot < L.cap) {
-            s_key[slot] = tab->seq[t];
-            s_val[slot] = t;
-            s_x[slot] = tab->x[t];
-            s_y[slot] = tab->y[t];
-            s_m[slot] = tab->m[t];
-            s_r[slot] = tab->r[t];
-          }
-          nc += __popcll(bal);
-        }
-        const unsigned long long fb = __ballot(pci >= 0);
-        pci = fb ? __builtin_amdgcn_readlane(pci, __ffsll((long long)fb) - 1) : -1;
-      } else wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
+      wave_grid_for(st, it, d.cols, q0, expand_for(rmax), [&](bool valid, int e) {
         double ex = 0, ey = 0, er = 0;
         bool keep = valid && (d.c_flags[e] & F_ALIVE) && (e % NP) != gp;
         if (keep) {
@@ -3023,17 +3005,11 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
       PA_C(1);
       PA_ADD(4, nc);
       wave_fence();
-      for (int x = lane; x < nc; x += 64) {  // rank by creation sequence (keys are unique)
-        int64_t k = s_key[x];
-        int rk = 0;
-        for (int y = 0; y < nc; y++) rk += s_key[y] < k;
-        s_srt[rk] = x;
-      }
-      wave_fence();
+      rank_by_key(s_key, s_srt, nc);
       PA_T(3);
       for (int t = 0; t < nc; t++) {
         const int k = s_srt[t];
-        const size_t o = tab ? (size_t)tab->e[s_val[k]] : (size_t)s_val[k];
+        const size_t o = (size_t)s_val[k];
         const double ox = s_x[k], oy = s_y[k], om = s_m[k], orr = s_r[k];
         if (!overlap(px, py, pm, pr, ox, oy, om, orr)) continue;
         size_t g, v;
@@ -3070,15 +3046,7 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
           pr = mr;
         }
         rmax = fmax(rmax, mr);
-        remove_cell(d, a, v, order, lane == 0, dkey, n_dead0);
-        if (tab && lane == 0) {  // (the group's table follows its eats)
-          const int gi = pc_eats ? pci : s_val[k], vi = pc_eats ? s_val[k] : pci;
-          if (gi >= 0) {
-            tab->m[gi] = m;
-            tab->r[gi] = mr;
-          }
-          if (vi >= 0) tab->al[vi] = 0;
-        }
+        remove_cell(d, a, v, order, lane == 0);
         // re-activate every later turn whose outcome the growth of g may change
         const int gpl = (int)(g % NP);
         const double gx = pc_eats ? px : ox, gy = pc_eats ? py : oy, gm = m, gr = mr;
@@ -3086,22 +3054,13 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
         PA_T(4);
         PA_C(2);
         // (cell_rect(d, g) from the registers: g's position and its new radius)
-        auto react = [&](bool valid, int e, double ex, double ey, double em, double er) {
-          if (!valid || (int)(e % NP) == gpl) return;
-          if (!overlap(gx, gy, gm, gr, ex, ey, em, er)) return;
+        wave_grid_for(st, it, d.cols, footprint(gx, gy, gr, d.size), expand_for(rmax), [&](bool valid, int e) {
+          if (!valid || (int)(e % NP) == gpl || !(d.c_flags[e] & F_ALIVE)) return;
+          if (!overlap(gx, gy, gm, gr, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e])) return;
           active_st(d, (size_t)e, 1);
           int pe = (int)(e % NP) - a * B;
           if (pe > P) atomicOr(&pend[pe >> 5], 1u << (pe & 31));
-        };
-        if (tab) {
-          for (int t = lane; t < tab->n; t += 64)
-            react(tab->al[t] != 0, tab->e[t], tab->x[t], tab->y[t], tab->m[t], tab->r[t]);
-        } else {
-          wave_grid_for(st, it, d.cols, footprint(gx, gy, gr, d.size), expand_for(rmax), [&](bool valid, int e) {
-            if (!valid || !(d.c_flags[e] & F_ALIVE)) return;
-            react(true, e, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e]);
-          }, d.cshift_c);
-        }
+        }, d.cshift_c);
         active_st(d, g, 1);
         if (gpl - a * B > P && lane == 0) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
         wave_fence();
@@ -3113,23 +3072,16 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
           if (i - 1 < d.p_ncells[gp]) {
             const size_t sk = (size_t)d.p_list[(i - 1) * NP + gp] * NP + gp;
             const double sx = d.c_x[sk], sy = d.c_y[sk], sm = d.c_m[sk], sr = d.c_r[sk];
-            auto partner = [&](bool valid, int e, double ex, double ey, double me, double er) {
-              if (!valid || (int)(e % NP) == gp) return;
-              if (!(overlap(sx, sy, sm, sr, ex, ey, me, er) && (can_eat(sm, me) || can_eat(me, sm)))) return;
+            wave_grid_for(st, it, d.cols, footprint(sx, sy, sr, d.size), expand_for(rmax), [&](bool valid, int e) {
+              if (!valid || (int)(e % NP) == gp || !(d.c_flags[e] & F_ALIVE)) return;
+              const double me = d.c_m[e];
+              if (!(overlap(sx, sy, sm, sr, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(sm, me) || can_eat(me, sm))))
+                return;
               int pe = (int)(e % NP) - a * B;
               if (pe <= P) return;
               active_st(d, (size_t)e, 1);
               atomicOr(&pend[pe >> 5], 1u << (pe & 31));
-            };
-            if (tab) {
-              for (int t = lane; t < tab->n; t += 64)
-                partner(tab->al[t] != 0, tab->e[t], tab->x[t], tab->y[t], tab->m[t], tab->r[t]);
-            } else {
-              wave_grid_for(st, it, d.cols, footprint(sx, sy, sr, d.size), expand_for(rmax), [&](bool valid, int e) {
-                if (!valid || !(d.c_flags[e] & F_ALIVE)) return;
-                partner(true, e, d.c_x[e], d.c_y[e], d.c_m[e], d.c_r[e]);
-              }, d.cshift_c);
-            }
+            }, d.cshift_c);
             wave_fence();
           }
           PA_T(6);
@@ -3140,11 +3092,193 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
     }
   }
   PA_T(7);
-  if (!dkey) {
-    PA_STORE(a);
-  } else {
-    PA_STORE_GROUP(a);
+  PA_STORE(a);
+}
+
+// The turns of one parallel group, entirely on its LDS table: the members' live
+// lists, counts and liveness, and every live cell of the closure with its
+// activity (the closure holds every cell a turn of the group can gather, eat, be
+// eaten by or re-activate -- pp_closure).  The same sequence of turns, eats and
+// re-activations as pp_turns; global memory is only written (the eats' mass,
+// list and liveness stores, the occupancy counts), never read, so a turn waits
+// on no load.  The group's deaths take slots of the pass's death list (dpl /
+// dkey, counted in *s_nd) for the sort into turn order after the pass.
+__device__ __forceinline__ void pp_group_turns(const Dev &d, int a, uint32_t *pend, int64_t *s_key, int *s_val,
+                                               int *s_srt, uint32_t *odirty, double &rmax, int *dpl, int64_t *dkey,
+                                               int *s_nd, const PPT &tab) {
+  const int lane = threadIdx.x & 63;
+  PA_DECL;
+  const int B = d.B, NW = (B + 31) / 32, NP = d.NP;
+  const unsigned long long lt = (1ull << lane) - 1;
+  auto member = [&](int p) {  // the member index of arena player p (every pp partner is a member)
+    const unsigned long long b = __ballot(lane < tab.np && tab.pid[lane] == p);
+    return b ? __ffsll((long long)b) - 1 : -1;
+  };
+  // removePlayerCell on the table (remove_cell's semantics): row's cell leaves
+  // its player's list, which closes up; the last cell's removal kills the player
+  auto remove = [&](int row, uint64_t &order) {
+    const size_t e = (size_t)tab.e[row];
+    const int gpv = (int)(e % NP), pv = gpv - a * B, jv = member(pv);
+    const int slot = (int)(e / NP);
+    const int n = tab.pn[jv];
+    const int l = lane < kMaxCells ? tab.pl[jv * kMaxCells + lane] : 0;
+    const bool keep = lane < n && l != slot;
+    const unsigned long long kb = __ballot(keep);
+    const int pos = __popcll(kb & lt), w = __popcll(kb);
+    wave_fence();  // (the list is read before it is rewritten)
+    if (keep) {
+      tab.pl[jv * kMaxCells + pos] = (uint8_t)l;
+      d.p_list[(size_t)pos * NP + gpv] = (uint8_t)l;
+    }
+    if (lane == 0) {
+      tab.pn[jv] = (uint8_t)w;
+      tab.al[row] = 0;
+      d.p_ncells[gpv] = w;
+      d.c_flags[e] = 0;
+    }
+    if (w == 0) {  // deletePlayerCell: last cell -> deadPlayers, setDead (field.py:386-388)
+      if (lane == 0) {
+        tab.pal[jv] = 0;
+        d.p_alive[gpv] = 0;
+        d.p_respawn[gpv] = 1;
+        const int sl = atomicAdd(s_nd, 1);
+        dpl[sl] = pv;
+        dkey[sl] = (int64_t)order;
+        ev_push(d, a, PH_PP, order, 9, pv, tab.seq[row]);
+      }
+      order++;
+    }
+    wave_fence();
+  };
+  PA_T(0);
+  int P = -1;
+  for (;;) {
+    const int found = pend_next(pend, NW, P + 1);
+    if (found < 0) break;
+    P = found;
+    wave_fence();
+    if (lane == 0) pend[P >> 5] &= ~(1u << (P & 31));
+    wave_fence();
+    const int gp = a * B + P, j = member(P);
+    uint64_t order = (uint64_t)P << 32;  // this turn's event / death keys
+    PA_C(0);
+    if (j < 0 || !tab.pal[j]) continue;
+    for (int i = 0;;) {  // for playerCell in player.getCells(): live list
+      if (i >= tab.pn[j]) break;
+      const int prow = tab.row[j * kMaxCells + tab.pl[j * kMaxCells + i]];
+      i++;
+      if (prow < 0 || !tab.act[prow]) continue;
+      wave_fence();
+      if (lane == 0) tab.act[prow] = 0;
+      const size_t pc = (size_t)tab.e[prow];
+      const double px = tab.x[prow], py = tab.y[prow];
+      const int64_t pseq = tab.seq[prow];
+      double pm = tab.m[prow], pr = tab.r[prow];
+      const Rect q0 = footprint(px, py, pr, d.size);  // (cell_rect)
+      PA_T(1);
+      // candidates: the table rows of other players' live cells whose footprint meets q0
+      int nc = 0;
+      for (int r0 = 0; r0 < tab.n; r0 += 64) {
+        const int t = r0 + lane;
+        bool keep = false;
+        if (t < tab.n && tab.al[t])
+          keep = (tab.e[t] % NP) != gp && rect_hit(footprint(tab.x[t], tab.y[t], tab.r[t], d.size), q0);
+        const unsigned long long bal = __ballot(keep);
+        const int slot = nc + __popcll(bal & lt);
+        if (keep) {
+          s_key[slot] = tab.seq[t];
+          s_val[slot] = t;
+        }
+        nc += __popcll(bal);
+      }
+      PA_T(2);
+      PA_C(1);
+      PA_ADD(4, nc);
+      wave_fence();
+      rank_by_key(s_key, s_srt, nc);
+      PA_T(3);
+      for (int t = 0; t < nc; t++) {
+        // (a candidate's row holds its state at turn start: only pc's row, and a
+        // victim's liveness, change before every candidate was visited)
+        const int k = s_srt[t], ro = s_val[k];
+        const double ox = tab.x[ro], oy = tab.y[ro], om = tab.m[ro], orr = tab.r[ro];
+        if (!overlap(px, py, pm, pr, ox, oy, om, orr)) continue;
+        const bool pc_eats = can_eat(pm, om);
+        if (!pc_eats && !can_eat(om, pm)) continue;
+        const int gi = pc_eats ? prow : ro, vi = pc_eats ? ro : prow;
+        const size_t g = (size_t)tab.e[gi];
+        // eatPlayerCell (field.py:346-348)
+        if (lane == 0) ev_push(d, a, PH_PP, order, 8, pc_eats ? pseq : s_key[k], pc_eats ? s_key[k] : pseq);
+        order++;
+        const double m = pc_eats ? grow_mass(pm, om) : grow_mass(om, pm);
+        const double mr = radius_of(m);
+        if (lane == 0) {
+          d.c_m[g] = m;
+          d.c_r[g] = mr;
+        }
+        // the spawn occupancy follows: the eaten cell leaves, the eater's footprint grows
+        occ_remove_def(d, a, pc_eats ? footprint(ox, oy, orr, d.size) : footprint(px, py, pr, d.size), odirty);
+        if (pc_eats) occ_grow_def(d, a, footprint(px, py, pr, d.size), footprint(px, py, mr, d.size), odirty);
+        else occ_grow_def(d, a, footprint(ox, oy, orr, d.size), footprint(ox, oy, mr, d.size), odirty);
+        if (pc_eats) {
+          pm = m;
+          pr = mr;
+        }
+        rmax = fmax(rmax, mr);
+        wave_fence();
+        if (lane == 0) {
+          tab.m[gi] = m;
+          tab.r[gi] = mr;
+        }
+        remove(vi, order);
+        PA_T(4);
+        PA_C(2);
+        // re-activate every later turn whose outcome the growth of g may change
+        const int gpl = (int)(g % NP);
+        const double gx = pc_eats ? px : ox, gy = pc_eats ? py : oy;
+        for (int t2 = lane; t2 < tab.n; t2 += 64) {
+          if (!tab.al[t2] || (int)(tab.e[t2] % NP) == gpl) continue;
+          if (!overlap(gx, gy, m, mr, tab.x[t2], tab.y[t2], tab.m[t2], tab.r[t2])) continue;
+          tab.act[t2] = 1;
+          const int pe = (int)(tab.e[t2] % NP) - a * B;
+          if (pe > P) atomicOr(&pend[pe >> 5], 1u << (pe & 31));
+        }
+        if (lane == 0) {
+          tab.act[gi] = 1;
+          if (gpl - a * B > P) atomicOr(&pend[(gpl - a * B) >> 5], 1u << ((gpl - a * B) & 31));
+        }
+        wave_fence();
+        PA_T(5);
+        if (!pc_eats) {
+          // pc left the live list: the cell that moved into its place is skipped
+          // this turn (field.py:236 + player.py:97).  Its pairs with later
+          // players are then theirs to resolve: activate those partners.
+          if (i - 1 < tab.pn[j]) {
+            const int sr_ = tab.row[j * kMaxCells + tab.pl[j * kMaxCells + i - 1]];
+            const double sx = tab.x[sr_], sy = tab.y[sr_], sm = tab.m[sr_], sr = tab.r[sr_];
+            for (int t2 = lane; t2 < tab.n; t2 += 64) {
+              if (!tab.al[t2] || (int)(tab.e[t2] % NP) == gp) continue;
+              const double me = tab.m[t2];
+              if (!(overlap(sx, sy, sm, sr, tab.x[t2], tab.y[t2], me, tab.r[t2]) && (can_eat(sm, me) || can_eat(me, sm))))
+                continue;
+              const int pe = (int)(tab.e[t2] % NP) - a * B;
+              if (pe <= P) continue;
+              tab.act[t2] = 1;
+              atomicOr(&pend[pe >> 5], 1u << (pe & 31));
+            }
+            wave_fence();
+          }
+          PA_T(6);
+          PA_C(3);
+          break;
+        }
+      }
+    }
   }
+  // (the activity marks leave with the group, as the serial pass leaves them)
+  for (int t = lane; t < tab.n; t += 64) d.c_active[tab.e[t]] = tab.act[t];
+  PA_T(7);
+  PA_STORE_GROUP(a);
 }
 // the whole pass in one wavefront (nw pending players in d.work)
 // L: the candidates of the current turn, with their state at turn start (only
@@ -3163,7 +3297,7 @@ __device__ __forceinline__ void pp_serial_body(const Dev &d, int a, uint32_t *pe
   if (nw == 0) return;
   ArenaCtl &c = d.ctl[a];
   double rmax = c.rmax_cell;
-  pp_turns(d, a, pend, L, odirty, rmax, nullptr, 0);
+  pp_turns(d, a, pend, L, odirty, rmax);
   c.rmax_cell = rmax;
 }
 
@@ -3197,9 +3331,7 @@ constexpr int PPG_CELLS = 64;  // cells per closure (also the turn candidate cap
 #define AIGAR_PPG_WAVES 16
 #endif
 constexpr int PPG_WAVES = AIGAR_PPG_WAVES;  // wavefronts running groups
-#ifndef AIGAR_PP_MERGE
-#define AIGAR_PP_MERGE 1  // closures sharing a player merge instead of falling back
-#endif
+constexpr int PP_LOWN_MAX = 8192;  // arenas up to this many players keep the pass's player owners in LDS
 constexpr int PPG_MIN = 3;     // fewer pending players: the serial pass (closures cost ~10 us)
 // (pl[0..npl): the starting players -- a seed, or merged closures)
 __device__ __forceinline__ bool pp_closure(const Dev &d, int a, int *pl, int &npl) {
@@ -3305,25 +3437,27 @@ __device__ __forceinline__ bool pp_closure(const Dev &d, int a, int *pl, int &np
 // pending bits together: disjoint groups interleave freely), then the pass's
 // deaths sorted into turn order by their keys.  Called by every thread.
 __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int *scr_v, uint32_t *pend, uint32_t *odirty PT_PARAMS) {
-  __shared__ int s_nw, s_dead0, s_bad;
+  __shared__ int s_nw, s_dead0, s_bad, s_nd;
   __shared__ int s_pl[PPG_SEEDS][PPG_PL], s_npl[PPG_SEEDS];
   __shared__ double s_rmax[PPG_WAVES];
+  // the group waves' candidate lists (key, table row, rank)
   __shared__ int64_t g_key[PPG_WAVES][PPG_CELLS];
   __shared__ int g_val[PPG_WAVES][PPG_CELLS], g_srt[PPG_WAVES][PPG_CELLS];
-  __shared__ double g_x[PPG_WAVES][PPG_CELLS], g_y[PPG_WAVES][PPG_CELLS], g_m[PPG_WAVES][PPG_CELLS],
-      g_r[PPG_WAVES][PPG_CELLS];
-#if AIGAR_PP_MERGE
-  __shared__ int t_e[PPG_WAVES][PPT_CAP];  // the group waves' cell tables (PPT)
+  // the group waves' tables (PPT); the serial pass's candidate states use the rows' arrays
+  __shared__ int t_e[PPG_WAVES][PPT_CAP];
   __shared__ double t_x[PPG_WAVES][PPT_CAP], t_y[PPG_WAVES][PPT_CAP], t_m[PPG_WAVES][PPT_CAP], t_r[PPG_WAVES][PPT_CAP];
   __shared__ int64_t t_seq[PPG_WAVES][PPT_CAP];
-  __shared__ uint8_t t_al[PPG_WAVES][PPT_CAP];
-#endif
+  __shared__ uint8_t t_al[PPG_WAVES][PPT_CAP], t_act[PPG_WAVES][PPT_CAP];
+  __shared__ int t_pid[PPG_WAVES][PPG_PL];
+  __shared__ uint8_t t_pn[PPG_WAVES][PPG_PL], t_pal[PPG_WAVES][PPG_PL], t_pl[PPG_WAVES][PPG_PL * kMaxCells];
+  __shared__ int8_t t_row[PPG_WAVES][PPG_PL * kMaxCells];
   ArenaCtl &c = d.ctl[a];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nwv = blockDim.x >> 6, T = blockDim.x;
   if (tid == 0) {  // (every thread reads the count before it is reset)
     s_nw = min(c.n_pend, d.Wcap);
     s_dead0 = c.n_dead;
     s_bad = 0;
+    s_nd = 0;
     c.n_pend = 0;
     c.stat[4] += s_nw;
     c.stat[7] += 1;
@@ -3331,17 +3465,35 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   __syncthreads();
   const int nw = s_nw, dead0 = s_dead0;
   const bool par = d.pp_par && odirty && nw >= PPG_MIN && nw <= PPG_SEEDS && nwv >= PPG_WAVES;
-  static_assert(PPG_WAVES * PPG_CELLS >= PP_LCAP, "the serial pass's candidate lists live in the groups' LDS");
-  const PPL serial_l{&g_key[0][0], &g_val[0][0], &g_srt[0][0], &g_x[0][0], &g_y[0][0], &g_m[0][0], &g_r[0][0], PP_LCAP};
+  static_assert(PPG_WAVES * PPG_CELLS >= PP_LCAP && PPG_WAVES * PPT_CAP >= PP_LCAP,
+                "the serial pass's candidate lists live in the groups' LDS");
+  static_assert(PPT_CAP <= 127 && PPG_PL <= 64, "table rows as int8, members one per lane");
+  const PPL serial_l{&g_key[0][0], &g_val[0][0], &g_srt[0][0], &t_x[0][0], &t_y[0][0], &t_m[0][0], &t_r[0][0], PP_LCAP};
   if (!par) {
     if (tid == 0 && nw > 0) PP_DIAG(nw < PPG_MIN ? 0 : 1);
     if (tid < 64) pp_serial_body(d, a, pend, odirty, nw, serial_l);
     return;
   }
   // closures; per player the lowest seed whose closure holds it
-  int *pown = scr_v + (size_t)a * d.Wcap;
-  for (int i = tid; i < d.B; i += T) __hip_atomic_store(&pown[i], INT_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (in the dynamic LDS after the pending bitmaps when the arena is small enough:
+  // the label propagation and the owner checks are then LDS rounds)
+  const bool lown = d.B <= PP_LOWN_MAX;
+  int *g_pown = scr_v + (size_t)a * d.Wcap, *s_pown = reinterpret_cast<int *>(pend + PPG_WAVES * ((d.B + 31) / 32));
+  auto pown_st = [&](int i, int v) {
+    if (lown) s_pown[i] = v;
+    else __hip_atomic_store(&g_pown[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto pown_min = [&](int i, int v) {
+    if (lown) atomicMin(&s_pown[i], v);
+    else atomicMin(&g_pown[i], v);
+  };
+  auto pown_ld = [&](int i) {
+    return lown ? __hip_atomic_load(&s_pown[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                : __hip_atomic_load(&g_pown[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (int i = tid; i < d.B; i += T) pown_st(i, INT_MAX);
   __syncthreads();
+  PT_SUB(0);
   for (int sd = w; sd < nw; sd += nwv) {
     const int P = d.work[(size_t)a * d.Wcap + sd];
     if (lane == 0) s_pl[sd][0] = P;
@@ -3352,10 +3504,10 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
       if (lane == 0) s_bad = 1;
       continue;
     }
-    for (int j = lane; j < npl; j += 64) atomicMin(&pown[s_pl[sd][j]], sd);
+    for (int j = lane; j < npl; j += 64) pown_min(s_pl[sd][j], sd);
   }
   __syncthreads();
-#if AIGAR_PP_MERGE
+  PT_SUB(1);
   // closures that share a player merge: their seeds' components (label = the
   // lowest seed, propagated along every shared player to a fixed point), each
   // component's players united in its root's list and closed again from there;
@@ -3368,7 +3520,7 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
       int chg = 0;
       for (int sd = w; sd < nw; sd += nwv)
         for (int j = lane; j < s_npl[sd]; j += 64) {
-          const int o = __hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int o = pown_ld(s_pl[sd][j]);
           if (o == sd) continue;
           const int lo = min(s_lab[sd], s_lab[o]);
           chg |= atomicMin(&s_lab[sd], lo) > lo;
@@ -3378,6 +3530,7 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     }
     for (int i = tid; i < nw; i += T) s_root[i] = s_lab[i];
     __syncthreads();
+    PT_SUB(2);
     for (int rt = w; rt < nw; rt += nwv) {
       if (s_root[rt] != rt) continue;
       int npl = s_npl[rt];
@@ -3402,12 +3555,13 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
       if (!ok && lane == 0) s_bad = 1;
     }
     __syncthreads();
+    PT_SUB(3);
     if (!s_bad) {
-      for (int i = tid; i < d.B; i += T) __hip_atomic_store(&pown[i], INT_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = tid; i < d.B; i += T) pown_st(i, INT_MAX);
       __syncthreads();
       for (int rt = w; rt < nw; rt += nwv)
         if (s_root[rt] == rt)
-          for (int j = lane; j < s_npl[rt]; j += 64) atomicMin(&pown[s_pl[rt][j]], rt);
+          for (int j = lane; j < s_npl[rt]; j += 64) pown_min(s_pl[rt][j], rt);
       __syncthreads();
     }
   }
@@ -3415,14 +3569,9 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     for (int sd = w; sd < nw; sd += nwv)
       if (s_root[sd] == sd)
         for (int j = lane; j < s_npl[sd]; j += 64)
-          if (__hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sd) s_bad = 1;
-#else
-  if (!s_bad)
-    for (int sd = w; sd < nw; sd += nwv)
-      for (int j = lane; j < s_npl[sd]; j += 64)
-        if (__hip_atomic_load(&pown[s_pl[sd][j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sd) s_bad = 1;
-#endif
+          if (pown_ld(s_pl[sd][j]) != sd) s_bad = 1;
   __syncthreads();
+  PT_SUB(4);
   PT_MARK(5, 6);
   if (tid == 0) PP_DIAG(s_bad ? 5 : 6);
   if (s_bad) {  // a closure overflowed, or two groups may meet: the serial pass
@@ -3434,12 +3583,11 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     uint32_t *mine = pend + (size_t)w * NW;
     for (int i = lane; i < NW; i += 64) mine[i] = 0;
     wave_fence();
-#if AIGAR_PP_MERGE
     // group g (the g-th root) runs in wave g % PPG_WAVES, one group after the
-    // other (groups are independent): its seeds' pending bits, its cell table
-    // (every live cell of its closure: one load round), its turns
+    // other (groups are independent): its seeds' pending bits, its table (every
+    // (member, slot) pair's cell state, list entry and activity, and each
+    // member's count and liveness: one load round), its turns
     double rmax = c.rmax_cell;
-    const PPT tab0{t_e[w], t_x[w], t_y[w], t_m[w], t_r[w], t_seq[w], t_al[w], 0};
     int g = 0;  // roots before rt
     for (int rt = 0; rt < nw; rt++) {
       if (s_root[rt] != rt) continue;
@@ -3451,24 +3599,35 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
           const int P = d.work[(size_t)a * d.Wcap + sd];
           mine[P >> 5] |= 1u << (P & 31);
         }
-      PPT tab = tab0;
       const int npl = s_npl[rt];
+      PPT tab{t_e[w], t_x[w], t_y[w], t_m[w], t_r[w], t_seq[w], t_al[w], t_act[w], t_pid[w], t_pn[w], t_pal[w],
+              t_pl[w], t_row[w], 0, npl};
       int nt = 0;
 #pragma unroll
-      for (int kk = 0; kk < 4; kk++) {  // (player j, slot) pairs, four per lane
-        const int pr = lane + 64 * kk, j = pr >> 4;
+      for (int kk = 0; kk < 4; kk++) {  // (member j, slot k) pairs, four per lane
+        const int pr = lane + 64 * kk, j = pr >> 4, k = pr & 15;
         bool keep = false;
         size_t ci = 0;
         double x = 0, y = 0, m = 0, r = 0;
         int64_t sq = 0;
+        int pj = 0, pn = 0, pal = 0;
+        uint8_t act = 0, li = 0;
         if (j < npl) {
-          ci = (size_t)(pr & 15) * d.NP + (size_t)a * d.B + s_pl[rt][j];
+          pj = s_pl[rt][j];
+          const int gpj = a * d.B + pj;
+          ci = (size_t)k * d.NP + gpj;
           keep = (d.c_flags[ci] & F_ALIVE) != 0;
           x = d.c_x[ci];
           y = d.c_y[ci];
           m = d.c_m[ci];
           r = d.c_r[ci];
           sq = d.c_seq[ci];
+          act = d.c_active[ci];
+          li = d.p_list[ci];  // (p_list rows share the cells' (slot, player) layout)
+          if (k == 0) {
+            pn = d.p_ncells[gpj];
+            pal = d.p_alive[gpj];
+          }
         }
         const unsigned long long bal = __ballot(keep);
         const int slot = nt + __popcll(bal & ((1ull << lane) - 1));
@@ -3480,6 +3639,16 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
           tab.r[slot] = r;
           tab.seq[slot] = sq;
           tab.al[slot] = 1;
+          tab.act[slot] = act;
+        }
+        if (j < npl) {
+          tab.pl[pr] = li;
+          tab.row[pr] = (int8_t)(keep && slot < PPT_CAP ? slot : -1);
+          if (k == 0) {
+            tab.pid[j] = pj;
+            tab.pn[j] = (uint8_t)pn;
+            tab.pal[j] = (uint8_t)pal;
+          }
         }
         nt += __popcll(bal);
       }
@@ -3489,26 +3658,16 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
       }
       tab.n = nt;
       wave_fence();
-      pp_turns(d, a, mine, PPL{g_key[w], g_val[w], g_srt[w], g_x[w], g_y[w], g_m[w], g_r[w], PPG_CELLS}, odirty,
-               rmax, scr_k + (size_t)a * d.Wcap, dead0, &tab);
+      pp_group_turns(d, a, mine, g_key[w], g_val[w], g_srt[w], odirty, rmax, d.dead + (size_t)a * d.B + dead0,
+                     scr_k + (size_t)a * d.Wcap, &s_nd, tab);
     }
     if (lane == 0) s_rmax[w] = rmax;
-#else
-    for (int sd = w; sd < nw; sd += PPG_WAVES) {
-      const int P = d.work[(size_t)a * d.Wcap + sd];
-      if (lane == 0) mine[P >> 5] |= 1u << (P & 31);
-    }
-    wave_fence();
-    double rmax = c.rmax_cell;
-    pp_turns(d, a, mine, PPL{g_key[w], g_val[w], g_srt[w], g_x[w], g_y[w], g_m[w], g_r[w], PPG_CELLS}, odirty,
-             rmax, scr_k + (size_t)a * d.Wcap, dead0);
-    if (lane == 0) s_rmax[w] = rmax;
-#endif
   }
   __syncthreads();
+  PT_SUB(5);
   PT_MARK(5, 7);
-  // the pass's deaths (appended by atomics) into turn order: rank by key
-  const int nd = __hip_atomic_load(&c.n_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - dead0;
+  // the pass's deaths (slots taken in completion order) into turn order: rank by key
+  const int nd = s_nd;
   const int64_t *dk = scr_k + (size_t)a * d.Wcap;
   int *dl = d.dead + (size_t)a * d.B + dead0;
   int rk[2], pv[2];
@@ -3531,8 +3690,10 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
     double r = c.rmax_cell;
     for (int k = 0; k < PPG_WAVES; k++) r = fmax(r, s_rmax[k]);
     c.rmax_cell = r;
+    c.n_dead = dead0 + nd;
     c.stat[6] += 1;
   }
+  PT_SUB(6);
 }
 
 // ------------------------------------------------------------ T18 spawn
@@ -3628,6 +3789,7 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
     __syncthreads();
     if (defer) occ_rebuild_dirty(d, a, s_odirty);
     __syncthreads();
+    PT_SUB(7);
   }
   PT_MARK(5, 1);
   ArenaCtl &c = d.ctl[a];
@@ -4368,7 +4530,8 @@ void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
   hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   // playerPlayerOverlap's serial pass + spawnStuff's plan + the end-of-tick virus
   // grid + the closing pellet update's sorted kill / join lists (and the pellet spawns)
-  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024), sizeof(uint32_t) * ((d.B + 31) / 32) * PPG_WAVES, s, d, 0,
+  hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024),
+                     sizeof(uint32_t) * ((d.B + 31) / 32) * PPG_WAVES + (d.B <= PP_LOWN_MAX ? sizeof(int) * d.B : 0), s, d, 0,
                      scr_k, scr_v, 1, 1);  // (pending bitmaps: one per parallel pp group wave)
   // the closing pellet update (survivors U joining staged records -> the new
   // current buffer) + the rest of spawnStuff as extra blocks: player respawns

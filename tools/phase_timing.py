@@ -13,7 +13,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.path.join(ROOT, "aigar_amd", "libaigar_hip_pt.so")
+SO = os.environ.get("AIGAR_PT_SO") or os.path.join(ROOT, "aigar_amd", "libaigar_hip_pt.so")
 KERNELS = {0: ("k_food_prep", ["", "player", "cell", "pellet walk", "blob walk", "select", "reserve"]),
            1: ("k_players", ["", "player loads", "tail loads", "tail done", "update_player", "look-back", "seq + blobs"]),
            2: ("k_players/x", ["", "head+policy+queue", "cell updates", "arena block", "blob block", "last-block grid"]),
@@ -63,6 +63,11 @@ def run(steps, policy="random"):
         pa_cnt = pa_cnt + buf[7, 0, :].astype(np.float64) if "pa_cnt" in dir() else buf[7, 0, :].astype(np.float64)
         pg_acc = pg_acc + buf[6, 1024, :].astype(np.float64) if "pg_acc" in dir() else buf[6, 1024, :].astype(np.float64)
         pg_cnt = pg_cnt + buf[7, 1024, :].astype(np.float64) if "pg_cnt" in dir() else buf[7, 1024, :].astype(np.float64)
+        sub = buf[6, 2048:2048 + 64, :].astype(np.float64)  # pp pass block sub-marks, per arena block
+        sub_ok = sub[:, 6] > 0  # (blocks that ran the parallel pass this step)
+        if sub_ok.any():
+            sb_acc = (sb_acc if "sb_acc" in dir() else 0) + sub[sub_ok].sum(axis=0)
+            sb_n = (sb_n if "sb_n" in dir() else 0) + int(sub_ok.sum())
         for k in KERNELS:
             started = buf[k, :, 0] != 0
             if not started.any():
@@ -111,6 +116,11 @@ def run(steps, policy="random"):
             "%s %.2f us" % (nm, pg_acc[k] * us / steps) for k, nm in enumerate(names)))
         print("pp group waves counts per step: turns %.2f, gathers %.2f, eats %.2f, pc eaten %.2f, candidates %.2f" % tuple(
             pg_cnt[k] / steps for k in (0, 1, 2, 3, 4)))
+    if "sb_acc" in dir():
+        names = ["pown init", "seed closures", "labels", "merged closures", "owner check", "turns", "death sort",
+                 "occ rebuild"]
+        print("pp parallel pass block marks (mean over %d block-steps, us from kernel start): " % sb_n + ", ".join(
+            "%s %.2f" % (nm, sb_acc[k] * us / sb_n) for k, nm in enumerate(names)))
     khz_ = khz.value / 1e3
     for k in KERNELS:
         row = []
