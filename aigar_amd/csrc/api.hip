@@ -160,6 +160,11 @@ struct aigar_handle {
   bool tr_failed = false;
   // aigar_run: one whole env step (policy + Field.update + observation) as a graph
   hipGraphExec_t run_graph = nullptr;
+  hipGraphExec_t run_graph_u = nullptr;  // run_unroll steps in one graph (same key)
+  // AIGAR_RUN_UNROLL (default 4): each graph launch costs an inter-graph gap on
+  // the device that a node boundary inside a graph does not (C3 A/B,
+  // profiles/r05_ab_notes.txt v30: 1 -> 4 steps per graph 42.5 -> 44.4 M env-steps/s)
+  int run_unroll = 4;
   aigar_run_params run_key{};
   void *run_out = nullptr;
   int run_dtype = -1;
@@ -222,6 +227,7 @@ static int obs_len_of(const aigar_config &c) {
 static void free_all(aigar_handle *h) {
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
   if (h->run_graph) (void)hipGraphExecDestroy(h->run_graph);
+  if (h->run_graph_u) (void)hipGraphExecDestroy(h->run_graph_u);
   if (h->env_graph) (void)hipGraphExecDestroy(h->env_graph);
   for (void *p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
@@ -291,6 +297,7 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   aigar_handle *h = new aigar_handle();
   h->cfg = *cfg;
   if (getenv("AIGAR_NO_GRAPH")) h->use_graph = false;
+  if (const char *u = getenv("AIGAR_RUN_UNROLL")) h->run_unroll = std::max(1, std::min(64, atoi(u)));
   if (getenv("AIGAR_TILE_GRAPH")) h->tile_graph = true;
   h->d.pp_par = getenv("AIGAR_PP_SERIAL") ? 0 : 1;
   // tuning knob: a fixed number of reservation rounds for every population
@@ -672,13 +679,26 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
                     h->run_dtype == (obs_out ? dtype : -1);
   if (h->use_graph && !same && n_steps > 0) {
     if (h->run_graph) (void)hipGraphExecDestroy(h->run_graph);
+    if (h->run_graph_u) (void)hipGraphExecDestroy(h->run_graph_u);
     h->run_graph = capture_graph(h, [&](hipStream_t cs) { launch_env_step(h, cs, *p, obs_out, dtype); });
     if (!h->run_graph) return fail("aigar_run: graph capture failed");
+    // (run_unroll > 1: the same step captured that many times in one graph -- one
+    // graph launch, and one inter-graph gap, per run_unroll steps)
+    h->run_graph_u = nullptr;
+    if (h->run_unroll > 1) {
+      h->run_graph_u = capture_graph(h, [&](hipStream_t cs) {
+        for (int k = 0; k < h->run_unroll; k++) launch_env_step(h, cs, *p, obs_out, dtype);
+      });
+      if (!h->run_graph_u) return fail("aigar_run: graph capture failed");
+    }
     h->run_key = *p;
     h->run_out = obs_out;
     h->run_dtype = obs_out ? dtype : -1;
   }
-  for (int t = 0; t < n_steps; t++) {
+  int t = 0;
+  if (h->run_graph_u && !h->profile)
+    for (; t + h->run_unroll <= n_steps; t += h->run_unroll) HIPCHK(hipGraphLaunch(h->run_graph_u, h->stream));
+  for (; t < n_steps; t++) {
     Mark m(h, "run");
     if (h->run_graph) HIPCHK(hipGraphLaunch(h->run_graph, h->stream));
     else launch_env_step(h, h->stream, *p, obs_out, dtype);
