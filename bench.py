@@ -448,7 +448,7 @@ def main():
     start = start_world(stp, name, replicas.rank_seed(args.seed, rank), arenas)
     salt = args.seed + 7919 * rank  # replicas of one snapshot diverge through their policy draws
 
-    def run(n):  # n whole steps (policy + tick + observation), one graph replayed n times
+    def run(n):  # n whole steps (policy + tick + observation): aigar_run replays its step graph (4 steps per launch)
         stp.run(n, args.policy, obs, p_split=ps, p_eject=pe, seed=salt, greedy_split=True)
 
     if args.policy == "random" and name in SNAPSHOTS:
