@@ -56,7 +56,7 @@ def test_run_multi_step_float32_and_recapture():
     fused, sep = _pair(cfg, 4)
     o32 = torch.zeros((fused.NP, fused.obs_len), dtype=torch.float32, device="cuda")
     r32 = torch.zeros_like(o32)
-    fused.run(5, "random", o32, p_split=0.1, p_eject=0.1, seed=8)  # 5 replays of one graph
+    fused.run(5, "random", o32, p_split=0.1, p_eject=0.1, seed=8)  # one 4-step graph replay + one 1-step replay
     for _ in range(5):
         sep.policy_random(0.1, 0.1, 8)
         sep.step(1)
@@ -84,6 +84,31 @@ def test_run_multi_step_float32_and_recapture():
     assert torch.equal(torch.nan_to_num(o32, nan=-7.0), torch.nan_to_num(r32, nan=-7.0))
     fused.close()
     sep.close()
+
+
+@pytest.mark.parametrize("policy", ["random", "greedy"])
+def test_unrolled_run_graph_matches_one_step_graph(policy, monkeypatch):
+    """aigar_run's multi-step graph (AIGAR_RUN_UNROLL copies of the step in one
+    graph, read at aigar_create; default 4) against the one-step graph replayed
+    n times: the same world and rows for step counts below, at and past the
+    unroll (11 = 8 + 3: one unrolled replay and three one-step replays)."""
+    monkeypatch.setenv("AIGAR_RUN_UNROLL", "1")
+    one = _lib.Stepper(_cfg(bots=256))
+    monkeypatch.setenv("AIGAR_RUN_UNROLL", "8")
+    unr = _lib.Stepper(_cfg(bots=256))
+    oa = torch.zeros((one.NP, one.obs_len), dtype=torch.float64, device="cuda")
+    ob = torch.zeros_like(oa)
+    for s in (one, unr):
+        s.set_stream(torch.cuda.current_stream().cuda_stream)
+        s.reset(31)
+    for n in (3, 8, 11):
+        one.run(n, policy, oa, p_split=0.05, p_eject=0.05, seed=6, greedy_split=True)
+        unr.run(n, policy, ob, p_split=0.05, p_eject=0.05, seed=6, greedy_split=True)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.nan_to_num(oa, nan=-7.0), torch.nan_to_num(ob, nan=-7.0)), n
+        assert parity.diff_states(one.get_state(), unr.get_state(), ftol=0.0) == [], n
+    one.close()
+    unr.close()
 
 
 def test_run_rejects_host_buffers_and_bad_policy():
