@@ -3453,6 +3453,8 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   __shared__ int8_t t_row[PPG_WAVES][PPG_PL * kMaxCells];
   ArenaCtl &c = d.ctl[a];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nwv = blockDim.x >> 6, T = blockDim.x;
+  // each wave's first seed, loaded beside the count (in bounds whatever the count)
+  const int p_first = w < d.Wcap ? d.work[(size_t)a * d.Wcap + w] : 0;
   if (tid == 0) {  // (every thread reads the count before it is reset)
     s_nw = min(c.n_pend, d.Wcap);
     s_dead0 = c.n_dead;
@@ -3495,7 +3497,7 @@ __device__ __forceinline__ void pp_pass(const Dev &d, int a, int64_t *scr_k, int
   __syncthreads();
   PT_SUB(0);
   for (int sd = w; sd < nw; sd += nwv) {
-    const int P = d.work[(size_t)a * d.Wcap + sd];
+    const int P = sd == w ? p_first : d.work[(size_t)a * d.Wcap + sd];
     if (lane == 0) s_pl[sd][0] = P;
     int npl = 1;
     const bool ok = pp_closure(d, a, s_pl[sd], npl);
