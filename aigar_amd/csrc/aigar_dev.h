@@ -181,6 +181,7 @@ struct Dev {
   uint32_t obs_ch, obs_ex;
   int flags;
   int pp_par;  // playerPlayerOverlap may run as independent groups (pp_pass; AIGAR_PP_SERIAL=1: never)
+  int share_cells;  // launch choice: k_food_prep / k_pp_active share a block's cells (Greedy populations)
   ArenaCtl *ctl;
   // players [NP]
   int *p_alive, *p_respawn, *p_ncells, *p_split, *p_eject, *p_pend;

@@ -2113,6 +2113,7 @@ constexpr int PREP_WAVES = 1;  // wavefronts per player (wave h takes cells h, h
 // pass once the owners' outcomes arrived).  Cells that cannot touch a held food
 // are skipped.  resume: only cells not yet final (f_done != 1) are prepared.
 __device__ __forceinline__ double tile_rall() { return sqrt(kMaxMass / kPi) * (1 + 1e-9); }  // any cell's radius bound
+template <bool SHARE>
 __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int resume) {
   FLOOR(4);
   TILE_GATE(d);
@@ -2130,22 +2131,46 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wi = xcd_block(blockIdx.x, gridDim.x) * 4 + w, gp = wi / PREP_WAVES,
             h = wi - gp * PREP_WAVES;
+  static_assert(PREP_WAVES == 1, "the block's cell sharing assumes one wave per player");
+  // SHARE (Greedy populations, many multi-cell players): a block's four players
+  // share their further cells -- a wave prepares its player's first cell, then
+  // claims cells 1 .. n-1 of its own player and of the block's other players of
+  // the same arena (q_next: LDS claim counters), so a multi-cell player's cells
+  // run side by side on the waves whose players had one (cells are independent
+  // here: each reserves with its own priority).  A wave that reads a count before
+  // its owner published it skips that player; the owner then claims its cells
+  // itself.  (Under the random population few players have several cells and the
+  // claims cost more than they save: ~1.5 us on this kernel, r05 v41.)
+  __shared__ int q_n[4], q_next[4], q_a[4];
+  if constexpr (SHARE) {
+    if (lane == 0) {
+      q_n[w] = 0;
+      q_next[w] = 1;  // (cell 0: its owner, unclaimed)
+    }
+    __syncthreads();
+  }
   if (gp < d.NP && gp % d.B == 0 && h == 0 && lane == 0) d.ctl[gp / d.B].food_undone[1] = 0;  // round 1's failure count
   if (gp >= d.NP) return;
   // this wave's first list row rides the liveness / count load round (the row
   // exists whatever the count: h < PREP_WAVES <= kMaxCells)
   const int s_first = uni((int)d.p_list[h * d.NP + gp]);
   s_bm[w][lane] = d.bmap[(size_t)(gp / d.B) * 64 + lane];  // (read after the pellet walk: its waits cover it)
-  if (!d.p_alive[gp]) return;  // uniform per wave
-  const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  const bool alive = d.p_alive[gp];
+  const int NP = d.NP, a = gp / d.B;
   Food F(d, a);
   const uint32_t base = d.ctl[a].food_round;
-  int n = uni(d.p_ncells[gp]);  // (wave-uniform values kept in SGPRs: 4 waves per SIMD fit in 128 VGPRs)
+  const int n0 = uni(d.p_ncells[gp]);  // (wave-uniform values kept in SGPRs: 4 waves per SIMD fit in 128 VGPRs)
+  const int n = alive ? n0 : 0;
+  if (SHARE && lane == 0) {
+    q_a[w] = a;
+    __hip_atomic_store(&q_n[w], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   PT_MARK(0, 1);
-  for (int k = h; k < n; k += PREP_WAVES) {
-    size_t ci = (size_t)(k == h ? s_first : uni((int)d.p_list[k * NP + gp])) * NP + gp;
+  // cell k of player gpc (arena a), pool index ci
+  auto prep_cell = [&](const int gpc, const int k, const size_t ci) {
+    const int p = gpc - a * d.B;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
-    if (resume && d.f_done[ci] == 1) continue;  // final (here or by its owner's message)
+    if (resume && d.f_done[ci] == 1) return;  // final (here or by its owner's message)
     double x = uni(d.c_x[ci]), y = uni(d.c_y[ci]), m = uni(d.c_m[ci]), r = uni(d.c_r[ci]);
     int64_t cseq = uni(d.c_seq[ci]);
     PT_MARK(0, 2);
@@ -2155,7 +2180,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
         d.f_cnt[ci] = 0;
         d.f_done[ci] = 2;
       }
-      continue;
+      return;
     }
     int cnt = 0;
     double lsum = 0;
@@ -2239,7 +2264,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
         if (valid && F.alive(j) && F.ej(j) != cseq && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), qm))
           atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
       });
-      continue;
+      return;
     }
     int nsel = 0;
     bool ovf = cnt > PREP_CAND;
@@ -2279,7 +2304,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
         if (valid && F.alive(j) && rect_hit(footprint(F.x(j), F.y(j), F.r(j), d.size), qb))
           atomicMax((unsigned long long *)F.owner(j), (unsigned long long)key);
       });
-      continue;
+      return;
     }
     int *lst = d.f_list + ci * FCAP;
     uint64_t key = food_key(base + 1, prio);
@@ -2299,6 +2324,35 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
     }
     wave_sync_lds();
     PT_MARK(0, 6);
+  };
+  // its own first cell (the slot arrived with the count) unclaimed, then claims of
+  // the block's further cells, its own player's first; one call site (two
+  // inlined copies of the cell spilled VGPRs)
+  if constexpr (!SHARE) {  // the player's cells one after the other
+    for (int k = 0; k < n; k++) prep_cell(gp, k, (size_t)(k == 0 ? s_first : uni((int)d.p_list[k * NP + gp])) * NP + gp);
+    return;
+  }
+  const int g0 = xcd_block(blockIdx.x, gridDim.x) * 4;
+  int gpc = gp, kc = n > 0 ? 0 : -1, sc = s_first;
+  for (int step = 0; step <= 4 * kMaxCells; step++) {
+    if (kc < 0) {  // the next claim: a player of the block (same arena) with a cell left
+      for (int t = 0; t < 4 && kc < 0; t++) {
+        const int w2 = (w + t) & 3;
+        const int n2 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&q_n[w2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (n2 <= 1 || __builtin_amdgcn_readfirstlane(q_a[w2]) != a) continue;
+        const int leader = __ffsll((long long)__ballot(1)) - 1;  // (the claim by the first active lane)
+        int k = 0;
+        if (lane == leader) k = atomicAdd(&q_next[w2], 1);
+        k = __builtin_amdgcn_readlane(k, leader);
+        if (k >= n2) continue;
+        gpc = __builtin_amdgcn_readfirstlane(g0 + w2);
+        kc = k;
+        sc = __builtin_amdgcn_readfirstlane((int)d.p_list[k * NP + gpc]);
+      }
+      if (kc < 0) break;
+    }
+    prep_cell(gpc, kc, (size_t)sc * NP + gpc);
+    kc = -1;
   }
 }
 // one eaten food: the event (in its reference phase), kill, growth
@@ -2789,9 +2843,8 @@ __device__ __forceinline__ void occ_rebuild_dirty(const Dev &d, int a, const uin
 
 // one wavefront per player: cells with an overlapping enemy cell at phase start
 // (+ the player's cells into the spawn occupancy)
-__global__ void __launch_bounds__(256) k_pp_active(Dev d) {
-  FLOOR(6);
-  PT_BEGIN(3);
+// (!SHARE: each wave tests its own player's cells in order)
+__device__ __forceinline__ void pp_active_own(const Dev &d PT_PARAMS) {
   const int lane = threadIdx.x & 63;
   const int gp = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
   // C4, device-bounded eat passes: the tick may go on only if no owned cell is undone
@@ -2832,6 +2885,101 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
     int w = atomicAdd(&d.ctl[a].n_pend, 1);
     if (w < d.Wcap) d.work[(size_t)a * d.Wcap + w] = gp - a * d.B;
     else set_err(d, a, ERR_WORK_CAP);
+  }
+}
+// SHARE (Greedy populations): a block's four players share their cells as in
+// k_food_prep -- a wave tests its own player's first cell, then claims the
+// remaining cells of the block's players of its arena (q_next).  A one-cell
+// player is queued by its own wave; for a player with more cells every tested
+// cell marks q_any and counts in q_done, and the wave that tests the last one
+// queues the player if marked.
+template <bool SHARE>
+__global__ void __launch_bounds__(256) k_pp_active(Dev d) {
+  FLOOR(6);
+  PT_BEGIN(3);
+  if constexpr (!SHARE) {
+    pp_active_own(d PT_ARGS);
+    return;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g0 = xcd_block(blockIdx.x, gridDim.x) * 4, gp = g0 + w;
+  __shared__ int q_n[4], q_next[4], q_done[4], q_any[4], q_a[4];
+  if (lane == 0) {
+    q_n[w] = 0;
+    q_next[w] = 1;  // (cell 0: its owner, unclaimed)
+    q_done[w] = 0;
+    q_any[w] = 0;
+  }
+  __syncthreads();
+  // C4, device-bounded eat passes: the tick may go on only if no owned cell is undone
+  if (d.tiled && gp == 0 && lane == 0 && d.ctl[0].n_undone_glob != 0) atomicOr(&d.ctl[0].err, ERR_TILE_PASSES);
+  if (gp >= d.NP) return;
+  const int s_first = d.p_list[gp];  // (list row 0 rides the liveness / count load round)
+  const bool alive = d.p_alive[gp];
+  const int NP = d.NP, a = gp / d.B;
+  const int *st = d.cstart + (size_t)a * (d.H + 1);
+  const int *it = d.citems + (size_t)a * kMaxCells * d.B;
+  const int E = expand_for(d.ctl[a].rmax_cell);
+  const int n = alive ? d.p_ncells[gp] : 0;
+  if (lane == 0) {
+    q_a[w] = a;
+    __hip_atomic_store(&q_n[w], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  PT_MARK(3, 1);
+  int wc = w, kc = n > 0 ? 0 : -1, nc = n, sc = s_first;
+  for (int step = 0; step <= 4 * kMaxCells; step++) {
+    if (kc < 0) {  // the next claim: a player of the block (same arena) with a cell left
+      for (int t = 0; t < 4 && kc < 0; t++) {
+        const int w2 = (w + t) & 3;
+        const int n2 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&q_n[w2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (n2 <= 1 || __builtin_amdgcn_readfirstlane(q_a[w2]) != a) continue;
+        const int leader = __ffsll((long long)__ballot(1)) - 1;  // (the claim by the first active lane)
+        int k = 0;
+        if (lane == leader) k = atomicAdd(&q_next[w2], 1);
+        k = __builtin_amdgcn_readlane(k, leader);
+        if (k >= n2) continue;
+        wc = w2;
+        kc = k;
+        nc = n2;
+        sc = __builtin_amdgcn_readfirstlane((int)d.p_list[k * NP + g0 + w2]);
+      }
+      if (kc < 0) break;
+    }
+    const int gpc = __builtin_amdgcn_readfirstlane(g0 + wc);
+    const size_t ci = (size_t)sc * NP + gpc;
+    double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
+    PT_MARK(3, 2);
+    Rect q = footprint(x, y, r, d.size);
+    occ_add(d, a, q);
+    bool any = wave_any_in_grid(st, it, d.cols, q, E, [&](int e) {
+      // only the LOWER-index player of a pair is marked: its turn comes first
+      // and resolves the pair ("the one that can eat does", field.py:238-243).
+      // The higher-index side's turn could only see a changed pair, and every
+      // change re-activates it: a growth re-activates the cells overlapping the
+      // grown one; a cell skipped by the live-list quirk re-activates its partners.
+      if (!(d.c_flags[e] & F_ALIVE) || (int)(e % NP) <= gpc) return false;
+      if (!rect_hit(cell_rect(d, e), q)) return false;
+      // a pair where neither side can eat stays inert until one of them grows
+      double me = d.c_m[e];
+      return overlap(x, y, m, r, d.c_x[e], d.c_y[e], me, d.c_r[e]) && (can_eat(m, me) || can_eat(me, m));
+    }, d.cshift_c);
+    const int leader = __ffsll((long long)__ballot(1)) - 1;
+    if (lane == leader) {
+      d.c_active[ci] = any;
+      bool push = any;
+      if (nc > 1) {
+        if (any) atomicOr(&q_any[wc], 1);
+        push = atomicAdd(&q_done[wc], 1) == nc - 1 &&  // (after the mark: LDS atomics of a CU apply in order)
+               __hip_atomic_load(&q_any[wc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+      }
+      if (push) {
+        const int wq = atomicAdd(&d.ctl[a].n_pend, 1);
+        if (wq < d.Wcap) d.work[(size_t)a * d.Wcap + wq] = gpc - a * d.B;
+        else set_err(d, a, ERR_WORK_CAP);
+      }
+    }
+    PT_MARK(3, 3);
+    kc = -1;
   }
 }
 
@@ -4501,8 +4649,12 @@ void launch_pellet_rows(const Dev &d, hipStream_t s) {
 static void launch_food(const Dev &d, hipStream_t s, int rounds, Scratch scr, int resume = 0, int fold = 0) {
   rounds = std::max(rounds, 1);
   const int g = nblk(d.NP, 256);
-  hipLaunchKernelGGL(k_food_prep, dim3(std::max(nblk((long)d.NP * PREP_WAVES, 4), resume ? 0 : d.A)), dim3(256), 0, s, d,
-                     rounds, resume);
+  if (d.share_cells)
+    hipLaunchKernelGGL(k_food_prep<true>, dim3(std::max(nblk((long)d.NP * PREP_WAVES, 4), resume ? 0 : d.A)), dim3(256),
+                       0, s, d, rounds, resume);
+  else
+    hipLaunchKernelGGL(k_food_prep<false>, dim3(std::max(nblk((long)d.NP * PREP_WAVES, 4), resume ? 0 : d.A)), dim3(256),
+                       0, s, d, rounds, resume);
   for (int r = 1; r <= rounds; r++) {
     hipLaunchKernelGGL(k_food_commit, dim3(g), dim3(256), 0, s, d, r, r == rounds ? 1 : 0, scr.k, scr.v, rounds,
                        fold && r == rounds ? 1 : 0, r == 1 && !resume ? 1 : 0);
@@ -4529,7 +4681,8 @@ void launch_tick_pre(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v, co
 }
 // the phases after it: playerPlayerOverlap, spawnStuff, closing rebuild (field.py:233-313)
 void launch_tick_post(const Dev &d, hipStream_t s, int64_t *scr_k, int *scr_v) {
-  hipLaunchKernelGGL(k_pp_active, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
+  if (d.share_cells) hipLaunchKernelGGL(k_pp_active<true>, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
+  else hipLaunchKernelGGL(k_pp_active<false>, dim3(nblk(d.NP, 4)), dim3(256), 0, s, d);
   // playerPlayerOverlap's serial pass + spawnStuff's plan + the end-of-tick virus
   // grid + the closing pellet update's sorted kill / join lists (and the pellet spawns)
   hipLaunchKernelGGL(k_spawn_plan, dim3(d.A), dim3(1024),
