@@ -229,7 +229,11 @@ int aigar_step(aigar_handle *h, int n_ticks);
  * NULL, every bot's getStateRepresentation (bot.py:272-299) into the DEVICE
  * buffer obs_out[A*B][aigar_obs_len()] (dtype as aigar_observe).  The step is
  * captured once as a single hipGraph (re-captured when the parameters or the
- * buffer change) and replayed, so no host round trip separates the phases.
+ * buffer change) and replayed, so no host round trip separates the phases;
+ * a second graph holds AIGAR_RUN_UNROLL copies of the step (environment,
+ * read at aigar_create; default 4) and carries n_steps / 4 of them (the rest
+ * one step per replay) -- the same kernels in the same order, one graph launch
+ * per 4 steps.
  * policy: AIGAR_POLICY_NONE keeps the current commands; RANDOM is
  * aigar_policy_random(p_split, p_eject, seed);
  * GREEDY is aigar_policy_greedy for every player.  With AIGAR_FLAG_EVENTS the
