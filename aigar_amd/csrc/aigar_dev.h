@@ -98,7 +98,8 @@ enum : uint32_t {
   ERR_TILE_OBS = 2048,    // a tile observed a bot whose view reaches beyond its held pellets
   ERR_TILE_PASSES = 4096,  // a device-bounded tiled tick ended with owned cells undone
   ERR_PREDICT = 8192,      // updatePlayers made other counts than k_players' arena block predicted (head_counts)
-  ERR_TILE_HANDOFF = 16384  // more dead bots to hand off in one tick than a message has hand-off slots
+  ERR_TILE_HANDOFF = 16384,  // more dead bots to hand off in one tick than a message has hand-off slots
+  ERR_CLAIM = 32768  // a bounded cell-claim loop (shared-cell kernels) ran out with claims left
 };
 enum : uint32_t { WARN_NEW_VIRUS_EATS = 1, WARN_DEAD_VIRUS = 2, WARN_TILE_OBS = 4 };
 enum : uint32_t { DIRTY_VIRUS = 1, DIRTY_BLOB = 2 };

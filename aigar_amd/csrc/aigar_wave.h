@@ -23,6 +23,9 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
 // a wave-uniform value moved to SGPRs (the compiler keeps a uniform value that
 // came from a vector load in VGPRs; in a register-bound kernel that costs waves)
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// the wave's first active lane: a claim or an error bit written by "lane 0" is lost
+// when lane 0 is inactive (the round-5 hang: a lane-0 atomic that never ran)
+__device__ __forceinline__ int wave_leader() { return __ffsll((long long)__ballot(1)) - 1; }
 __device__ __forceinline__ int64_t uni(int64_t v) {
   const int lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);

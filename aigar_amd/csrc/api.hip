@@ -153,6 +153,7 @@ struct aigar_handle {
   bool rccl_bad = false;  // an all-gather failed while a graph was captured
   bool loopback = false;  // timing rehearsal: the exchange copies this tile's message to its own slot only
   bool cmd_ready = false;  // this tick's Greedy commands were exchanged and applied (aigar_tile_apply_commands)
+  bool cmd_pending = false;  // aigar_tile_policy wrote a command message that was not applied yet
   hipGraphExec_t tr_graph = nullptr;
   aigar_run_params tr_key{};
   void *tr_out = nullptr;
@@ -165,6 +166,7 @@ struct aigar_handle {
   // the device that a node boundary inside a graph does not (C3 A/B,
   // profiles/r05_ab_notes.txt v30: 1 -> 4 steps per graph 42.5 -> 44.4 M env-steps/s)
   int run_unroll = 4;
+  bool run_u_tried = false;  // the unrolled graph of this key was captured (or its capture failed)
   aigar_run_params run_key{};
   void *run_out = nullptr;
   int run_dtype = -1;
@@ -530,7 +532,7 @@ static int check_device_errors(aigar_handle *h) {
                   "16 worklist cap, 32 observation cap, 64 candidate cap, 128 slot, 256 pixel-frame object cap, "
                   "512 tile message cap, 1024 tile record lookup, 2048 tile view beyond the held pellets, "
                   "4096 tiled tick ended with undone cells, 8192 new-cell / blob counts not as predicted, "
-                  "16384 more dead bots to hand off than hand-off slots)",
+                  "16384 more dead bots to hand off than hand-off slots, 32768 cell claims left at the claim bound)",
                   ctl[a].err, a);
   return 0;
 }
@@ -563,6 +565,7 @@ extern "C" int aigar_reset(aigar_handle *h, uint64_t seed) {
   if (d.tiled) {  // every tile's history copy is current (all zero)
     HIPCHK(hipMemsetAsync(d.t_holder, 0xFF, sizeof(int) * NP, h->stream));
     HIPCHK(hipMemsetAsync(d.t_obsby, 0xFF, sizeof(int) * NP, h->stream));
+    HIPCHK(hipMemsetAsync(d.t_hodefer, 0, NP, h->stream));  // (hand-off priorities restart)
   }
   launch_reset(d, h->stream, seed);
   HIPCHK(hipGetLastError());
@@ -624,6 +627,22 @@ __global__ void k_step_begin(Dev d) {
 
 static int food_rounds(const aigar_handle *h) { return h->rounds > 0 ? h->rounds : (h->greedy_seen ? 2 : 1); }
 
+// food_rounds() follows the handle's history: when a Greedy policy first runs, the
+// graphs captured with the old round count are dropped (recaptured at their next
+// call), so a step graph and the tile passes never mix round counts.  (The
+// Field.update graph of aigar_step keeps its own graph_rounds check.)
+static void note_greedy(aigar_handle *h) {
+  if (h->greedy_seen) return;
+  h->greedy_seen = true;
+  if (h->rounds > 0) return;  // (the round count is fixed: nothing changes)
+  (void)hipStreamSynchronize(h->stream);  // (no replay of a graph being destroyed is pending)
+  for (hipGraphExec_t *g : {&h->run_graph, &h->run_graph_u, &h->env_graph, &h->tb_graph, &h->te_graph, &h->tr_graph}) {
+    if (*g) (void)hipGraphExecDestroy(*g);
+    *g = nullptr;
+  }
+  h->run_u_tried = false;
+}
+
 extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
   if (!h) return fail("null handle");
   if (n_ticks < 0) return fail("n_ticks < 0");
@@ -681,7 +700,7 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
   HIPCHK(hipSetDevice(h->cfg.device));
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every call (all n_steps accumulate)
     hipLaunchKernelGGL(k_step_begin, dim3((h->d.A + 63) / 64), dim3(64), 0, h->stream, h->d);
-  if (p->policy == AIGAR_POLICY_GREEDY) h->greedy_seen = true;  // (food_rounds)
+  if (p->policy == AIGAR_POLICY_GREEDY) note_greedy(h);  // (food_rounds)
   const bool same = h->run_graph && memcmp(&h->run_key, p, sizeof *p) == 0 && h->run_out == obs_out &&
                     h->run_dtype == (obs_out ? dtype : -1);
   if (h->use_graph && !same && n_steps > 0) {
@@ -689,18 +708,22 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
     if (h->run_graph_u) (void)hipGraphExecDestroy(h->run_graph_u);
     h->run_graph = capture_graph(h, [&](hipStream_t cs) { launch_env_step(h, cs, *p, obs_out, dtype); });
     if (!h->run_graph) return fail("aigar_run: graph capture failed");
-    // (run_unroll > 1: the same step captured that many times in one graph -- one
-    // graph launch, and one inter-graph gap, per run_unroll steps)
     h->run_graph_u = nullptr;
-    if (h->run_unroll > 1) {
-      h->run_graph_u = capture_graph(h, [&](hipStream_t cs) {
-        for (int k = 0; k < h->run_unroll; k++) launch_env_step(h, cs, *p, obs_out, dtype);
-      });
-      if (!h->run_graph_u) return fail("aigar_run: graph capture failed");
-    }
+    h->run_u_tried = false;
     h->run_key = *p;
     h->run_out = obs_out;
     h->run_dtype = obs_out ? dtype : -1;
+  }
+  // run_unroll > 1: the same step captured that many times in one graph -- one
+  // graph launch, and one inter-graph gap, per run_unroll steps.  Captured at the
+  // first call of the key that can use it; if that capture fails, the one-step
+  // graph serves alone.
+  if (h->run_graph && !h->run_graph_u && !h->run_u_tried && h->run_unroll > 1 && n_steps >= h->run_unroll &&
+      !h->profile) {
+    h->run_u_tried = true;
+    h->run_graph_u = capture_graph(h, [&](hipStream_t cs) {
+      for (int k = 0; k < h->run_unroll; k++) launch_env_step(h, cs, *p, obs_out, dtype);
+    });
   }
   int t = 0;
   if (h->run_graph_u && !h->profile)
@@ -752,23 +775,27 @@ extern "C" int aigar_tile_set_buffers(aigar_handle *h, void *outbox, void *inbox
 extern "C" int aigar_tile_policy(aigar_handle *h, int greedy_split) {
   if (need_tiled(h)) return -1;
   HIPCHK(hipSetDevice(h->cfg.device));
-  h->greedy_seen = true;  // (food_rounds)
+  note_greedy(h);  // (food_rounds)
   {
     Mark m(h, "policy");
     launch_tile_policy(h->d, h->stream, greedy_split ? 1 : 0, h->d_mask, h->box_recs - 1);
   }
   h->pass_recs = h->box_recs;  // (the command message: the whole buffer is exchanged)
   h->cmd_ready = false;
+  h->cmd_pending = true;
   HIPCHK(hipGetLastError());
   return 0;
 }
 extern "C" int aigar_tile_apply_commands(aigar_handle *h) {
   if (need_tiled(h)) return -1;
-  if (h->pass_recs != h->box_recs) return fail("tile_apply_commands: no aigar_tile_policy before it");
+  // (a flag of its own: pass_recs alone can equal box_recs after an eat pass)
+  if (!h->cmd_pending || h->pass_recs != h->box_recs)
+    return fail("tile_apply_commands: no aigar_tile_policy before it");
   HIPCHK(hipSetDevice(h->cfg.device));
   launch_tile_cmd_apply(h->d, h->stream, h->box_recs);
   HIPCHK(hipGetLastError());
   h->pass_recs = 0;
+  h->cmd_pending = false;
   h->cmd_ready = true;
   return 0;
 }
@@ -803,6 +830,7 @@ extern "C" int aigar_tile_begin(aigar_handle *h, const aigar_run_params *p) {
     else issue(h->stream);
   }
   h->pass_recs = 1 + h->d.tcap + h->d.hcap * h->d.hrec;  // (+ the observation-history hand-off slots)
+  h->cmd_pending = false;
   h->first_pass = 1;
   HIPCHK(hipGetLastError());
   return 0;
@@ -830,6 +858,7 @@ extern "C" int aigar_tile_resume(aigar_handle *h) {
   Mark m(h, "tile_resume");
   launch_tile_pass(h->d, h->stream, food_rounds(h), h->scr_k, h->scr_v, 0);
   h->pass_recs = 1 + h->d.tcap + h->d.bm_words / 4;
+  h->cmd_pending = false;
   h->first_pass = 0;
   HIPCHK(hipGetLastError());
   return 0;
@@ -1017,12 +1046,13 @@ extern "C" int aigar_tile_run(aigar_handle *h, int n_steps, const aigar_run_para
   if (!h->rccl_comm && !h->loopback) return fail("tile_run: no RCCL communicator (aigar_tile_comm_init)");
   if (n_steps < 0 || extra_passes < 0 || extra_passes > 64) return fail("tile_run: bad n_steps / extra_passes");
   if (p->policy < AIGAR_POLICY_NONE || p->policy > AIGAR_POLICY_GREEDY) return fail("tile_run: unknown policy %d", p->policy);
-  if (p->policy == AIGAR_POLICY_GREEDY) h->greedy_seen = true;  // (food_rounds)
+  if (p->policy == AIGAR_POLICY_GREEDY) note_greedy(h);  // (food_rounds)
   if (obs_out && dtype != 0 && dtype != 1) return fail("dtype must be 0 (float64) or 1 (float32)");
   HIPCHK(hipSetDevice(h->cfg.device));
   if (h->d.flags & AIGAR_FLAG_EVENTS)  // the event log restarts every call (all n_steps accumulate)
     hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, h->stream, h->d);
   h->pass_recs = 0;  // (the aigar_tile_* call sequence restarts at a tile_begin)
+  h->cmd_pending = false;
   const bool same = h->tr_graph && memcmp(&h->tr_key, p, sizeof *p) == 0 && h->tr_out == obs_out &&
                     h->tr_dtype == (obs_out ? dtype : -1) && h->tr_extra == extra_passes;
   if (h->use_graph && !h->profile && !same && !h->tr_failed && n_steps > 0) {
@@ -1156,7 +1186,7 @@ extern "C" int aigar_set_roles(aigar_handle *h, const uint8_t *roles, int on_dev
   HIPCHK(hipStreamSynchronize(h->stream));
   h->n_greedy = ng;
   h->n_random = nr;
-  if (ng) h->greedy_seen = true;  // (food_rounds)
+  if (ng) note_greedy(h);  // (food_rounds)
   return 0;
 }
 extern "C" int aigar_env_config(aigar_handle *h, const aigar_env_params *p) {
@@ -1726,6 +1756,7 @@ extern "C" int aigar_load_state(aigar_handle *h, int arena, const aigar_state *s
   if (d.tiled) {
     HIPCHK(hipMemsetAsync(d.t_holder, 0xFF, sizeof(int) * d.NP, h->stream));
     HIPCHK(hipMemsetAsync(d.t_obsby, 0xFF, sizeof(int) * d.NP, h->stream));
+    HIPCHK(hipMemsetAsync(d.t_hodefer, 0, d.NP, h->stream));
   }
   launch_player_fov(d, h->stream);  // FOV cache of the loaded players
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1740,7 +1771,7 @@ extern "C" int aigar_policy_greedy(aigar_handle *h, int greedy_split, const uint
     HIPCHK(hipMemcpyAsync(h->d_mask, mask, (size_t)h->d.NP, hipMemcpyHostToDevice, h->stream));
     m = h->d_mask;
   }
-  h->greedy_seen = true;  // (food_rounds)
+  note_greedy(h);  // (food_rounds)
   {
     Mark mk(h, "policy");
     launch_policy_greedy(h->d, h->stream, greedy_split ? 1 : 0, m, -1);

@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // that does not (a halo below the view's reach) is an error, and the pellet
   // channel is NaN
   const bool held = tile_holds_rect(d, rect_grow(Q, 1, d.cols));
-  if (!held && lane == 0) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
+  if (!held && lane == wave_leader()) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
   // owner of cell pool index g = slot * NP + player, without a 64-bit modulo
   const double inv_np = 1.0 / NP;
   auto pool_owner = [&](size_t g) {
@@ -451,10 +451,11 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     // lists and walk again (exact, only slower)
     const int need = (np > OBS_PCAP ? np : 0) + (nc > OBS_CCAP ? nc : 0) + (nv > OBS_VCAP ? nv : 0);
     int b = 0;
-    if (lane == 0) b = obs_claim(d, epoch, need);
-    b = __shfl(b, 0);
+    const int ld = wave_leader();
+    if (lane == ld) b = obs_claim(d, epoch, need);
+    b = __builtin_amdgcn_readlane(b, ld);
     if (b + need > d.OBcap) {
-      if (lane == 0) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
+      if (lane == ld) atomicOr(&d.ctl[a].err, ERR_OBS_CAP);
       np = min(np, OBS_PCAP);
       nc = min(nc, OBS_CCAP);
       nv = min(nv, OBS_VCAP);
@@ -964,7 +965,7 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
   by = __shfl(by, bl);
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
   // C4 (aigar_tile_policy): the tile taking this bot's move must hold every pellet of its view
-  if (d.tiled && !tile_holds_rect(d, rect_grow(Q, 1, d.cols)) && lane == 0) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
+  if (d.tiled && !tile_holds_rect(d, rect_grow(Q, 1, d.cols)) && lane == wave_leader()) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
   double best = -1;
   uint64_t bord = ~0ull;
   double tx = 0, ty = 0;

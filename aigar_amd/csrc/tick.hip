@@ -707,9 +707,11 @@ __device__ void tile_plan_thread(const Dev &d, int gp) {
     d.t_obsby[gp] = -1;
     d.t_holder[gp] = h;
   }
-  if (h != d.tile_id) return;
-  if (d.p_alive[gp]) {
-    if (tile_of(d, d.p_fx[gp], d.p_fy[gp]) == h) return;
+  // (a bot that does not queue for a live hand-off keeps no waiting priority)
+  if (h != d.tile_id || !d.p_alive[gp] || tile_of(d, d.p_fx[gp], d.p_fy[gp]) == h) {
+    if (d.t_hodefer[gp]) d.t_hodefer[gp] = 0;
+    if (h != d.tile_id || d.p_alive[gp]) return;
+  } else {
     const int q = atomicAdd(&c.n_ho_live, 1);
     if (q < d.NP) d.t_holive[q] = gp;
     return;
@@ -2334,7 +2336,8 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   }
   const int g0 = xcd_block(blockIdx.x, gridDim.x) * 4;
   int gpc = gp, kc = n > 0 ? 0 : -1, sc = s_first;
-  for (int step = 0; step <= 4 * kMaxCells; step++) {
+  int step = 0;
+  for (; step <= 4 * kMaxCells; step++) {
     if (kc < 0) {  // the next claim: a player of the block (same arena) with a cell left
       for (int t = 0; t < 4 && kc < 0; t++) {
         const int w2 = (w + t) & 3;
@@ -2354,6 +2357,9 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
     prep_cell(gpc, kc, (size_t)sc * NP + gpc);
     kc = -1;
   }
+  // (a block holds at most 4 x kMaxCells cells: the bound is never reached unless the
+  // claim counters are corrupt -- then cells went unprepared, which must not pass silently)
+  if (step > 4 * kMaxCells && lane == wave_leader()) set_err(d, a, ERR_CLAIM);
 }
 // one eaten food: the event (in its reference phase), kill, growth
 // (eatCell -> adjustCellSize -> grow, field.py:327-344)
@@ -2927,7 +2933,8 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
   }
   PT_MARK(3, 1);
   int wc = w, kc = n > 0 ? 0 : -1, nc = n, sc = s_first;
-  for (int step = 0; step <= 4 * kMaxCells; step++) {
+  int step = 0;
+  for (; step <= 4 * kMaxCells; step++) {
     if (kc < 0) {  // the next claim: a player of the block (same arena) with a cell left
       for (int t = 0; t < 4 && kc < 0; t++) {
         const int w2 = (w + t) & 3;
@@ -2981,6 +2988,7 @@ __global__ void __launch_bounds__(256) k_pp_active(Dev d) {
     PT_MARK(3, 3);
     kc = -1;
   }
+  if (step > 4 * kMaxCells && lane == wave_leader()) set_err(d, a, ERR_CLAIM);  // (as in k_food_prep)
 }
 
 // removes cell e (pool index) from its player's list; returns true if the player died
@@ -3951,8 +3959,15 @@ __global__ void __launch_bounds__(1024) k_spawn_plan(Dev d, int init, int64_t *s
     if (!(dirty & (kind == 0 ? DIRTY_VIRUS : DIRTY_BLOB))) continue;
     // blobs die every tick (stopped ones turn into pellets): the list keeps its
     // holes -- every consumer tests F_ALIVE and orders by seq -- until they are
-    // half of it or it nears its capacity, so most ticks skip this pass
-    if (kind == 1 && c.n_blob < 2 * c.n_blob_live + 256 && c.n_blob < d.Ecap / 2) continue;
+    // half of it or it nears its capacity, so most ticks skip this pass -- but
+    // never when the next tick's ejections could overflow the holes' list: every
+    // player cell may eject once (field.py:134-146), and a split may double the
+    // cells first, so the bound is 2 x this tick's cell-grid total
+    if (kind == 1 && c.n_blob < 2 * c.n_blob_live + 256 && c.n_blob < d.Ecap / 2) {
+      const int cc = cgrid_cols(d);
+      const int ncell = d.cstart[(size_t)a * (d.H + 1) + cc * cc];
+      if (c.n_blob + min(2 * ncell, kMaxCells * d.B) <= d.Ecap) continue;
+    }
     int n = kind == 0 ? c.n_vir : c.n_blob;
     int cap = kind == 0 ? d.Vcap : d.Ecap;
     int out = 0;

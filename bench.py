@@ -131,6 +131,13 @@ def cpu_baseline(name, budget_s=12.0, seed=1, policy="random"):
     o = Oracle(cfg)
     o.reset(seed)
     rng = np.random.default_rng(seed)
+    start = "reset(%d)" % seed
+    snap = SNAPSHOTS.get(name)
+    path = os.path.join(ROOT, "data", "%s.npz" % snap) if snap else None
+    if path and os.path.exists(path) and arenas == 1:  # the GPU line's start world (start_world)
+        z = np.load(path)
+        o.load_state({k: z[k] for k in z.files})
+        start = "data/%s.npz" % snap
 
     def commands():
         st = o.player_stats()
@@ -151,6 +158,11 @@ def cpu_baseline(name, budget_s=12.0, seed=1, policy="random"):
         else:
             o.set_commands(commands())
 
+    if policy == "random" and snap and start != "reset(%d)" % seed:
+        for _ in range(SETTLE_TICKS):  # (untimed, as the GPU line: the random population settles)
+            act()
+            o.step(1)
+        start += " + %d untimed random-policy ticks" % SETTLE_TICKS
     for _ in range(2):  # warm-up
         act()
         o.step(1)
@@ -166,8 +178,8 @@ def cpu_baseline(name, budget_s=12.0, seed=1, policy="random"):
     dt = time.perf_counter() - t0
     o.close()
     return {"value": bots * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%s world, %d steps (%s policy + Field.update + obs for all %d bots) after 2 warm-up "
-                      "steps, oracle/oracle.c single thread, %.1f s" % (name.upper(), n, policy, bots, dt)}
+            "sample": "%s world from %s, %d steps (%s policy + Field.update + obs for all %d bots) after 2 warm-up "
+                      "steps, oracle/oracle.c single thread, %.1f s" % (name.upper(), start, n, policy, bots, dt)}
 
 
 def _c5_arena_worker(args):
@@ -391,9 +403,30 @@ def c4_leg(args, name, rank, world, local, seed, dist, backend):
             "step_graph": graphed,
             "exchange": {"collective": "ncclAllGather inside the step graph (RCCL, xGMI)" if rccl else
                          "all_gather_into_tensor (%s, staged through host memory)" % backend,
+                         "rccl_ranks": info["ntiles"] if rccl else 0,  # (the communicator: one rank per tile)
+                         "process_group_ranks": world,
                          "bytes_per_rank_first_pass": (1 + info["tcap"]) * 32 + info.get("handoff_bytes", 0),
                          "avg_ms": ex_ms},
             "per_tile": tiles_all}
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` (N > 1) outside torch.distributed.run: start the
+    N ranks (one process per GPU) the way the driver does, as a CHILD process --
+    this process has not touched the GPU and never execs -- with the same
+    arguments; rank 0's JSON line reaches stdout through the inherited pipe, and
+    the child's exit code is returned (the reference's own multi-process launch is
+    an mp.Pool of workers, aigar.py:549-554)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.stdout.flush()
+    return subprocess.call(cmd, cwd=ROOT)
 
 
 def main():
@@ -420,6 +453,8 @@ def main():
                          "(bot.py:579-633, ENABLE_GREEDY_SPLIT) on the device")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     rank, world, local = replicas.world_from_env()
     if args.gpus != world:

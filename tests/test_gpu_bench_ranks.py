@@ -25,13 +25,21 @@ def _free_port():
 
 
 @pytest.mark.gpu
-def test_two_rank_bench_line():
+@pytest.mark.parametrize("launch", ["torchrun", "plain"])
+def test_two_rank_bench_line(launch):
+    """`torchrun`: the driver's launch; `plain`: `python bench.py --gpus 2`, which
+    starts torch.distributed.run itself as a child process."""
     steps = 10
     env = dict(os.environ, AIGAR_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", str(steps), "--warmup", "3", "--no-cpu-baseline", "--no-pixels",
-           "--batched-arenas", "0"]
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    tail = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", "3",
+            "--no-cpu-baseline", "--no-pixels", "--batched-arenas", "0"]
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + tail
+    else:
+        cmd = [sys.executable] + tail
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -49,6 +57,7 @@ def test_two_rank_bench_line():
     assert c4["scaling"] == "strong" and "tiled 2x1" in c4["workload"]
     assert c4["eat_passes_per_tick"] >= 1 and c4["exchange"]["bytes_per_rank_first_pass"] > 0
     assert c4["value"] > 0 and c4["exchange"]["avg_ms"] > 0
+    assert c4["exchange"]["process_group_ranks"] == 2 and c4["exchange"]["rccl_ranks"] == 0  # (gloo: no RCCL)
     # the observation is divided: each tile observed part of the bots, together all the live ones
     obs = [t["bots_observed"] for t in c4["per_tile"]]
     assert len(obs) == 2 and min(obs) > 0 and 4000 < sum(obs) <= 4096, obs

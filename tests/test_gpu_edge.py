@@ -87,6 +87,31 @@ def test_mass_cap_and_virus_explosion():
     assert most == 16  # the explosion fills the player up to the 16-cell cap (field.py:354)
 
 
+def test_eject_burst_near_blob_capacity():
+    """the blob list keeps its holes between compactions
+    (k_spawn_plan); a tick on which every cell ejects (field.py:134-146) must
+    still find room when the live blobs plus its ejections fit the capacity.
+    40 players split to 16 cells each, a trickle of ejections leaves holes, then
+    every player ejects from all of its cells at once (~640 blobs, capacity 1024)."""
+    B, size = 40, 600
+    cfg = make_config(bots=B, field_size=size, max_pellets=300.0, channels=CH & ~_abi.OBS_VIRUS, extras=0x1F,
+                      blob_cap=1024)
+    g, o = _pair(cfg, 35)
+    d = dict(o.get_state())
+    cf = d["cells_f"].copy()
+    cf[:, 2] = 1500.0
+    cf[:, 3] = math.sqrt(1500.0 / math.pi)
+    d["cells_f"] = cf
+    _load_both(g, o, d)
+    _run(g, o, 5, B, size, 1.0, 0.0, 35)  # every player splits up to the 16-cell cap
+    assert int(np.min(g.get_state()["players_i"][:, 4])) >= 8
+    _run(g, o, 24, B, size, 0.0, 0.04, 36)  # a trickle: blobs die after 15 ticks and leave holes
+    _run(g, o, 1, B, size, 0.0, 1.0, 37)  # the burst
+    assert g.get_state()["n_blobs"] >= 300
+    _run(g, o, 12, B, size, 0.0, 0.04, 38)
+    g.sync()  # no ERR_BLOB_CAP
+
+
 def test_refill_of_a_depleted_world_in_one_tick():
     """a tick whose spawns put more joining records into one bucket row
     than the closing update's LDS list holds (512; field 1000 = 50 rows, 40,000
