@@ -77,7 +77,9 @@ def test_random_population(bots, ticks, seed, kw):
 @pytest.mark.parametrize("name", ["stress_virus", "crowd32", "merge8", "virus_feed", "greedy16_virus_split",
                                   "greedy16", "random64",
                                   # BASELINE configs[1] and [2] at full size (reference-generated fixtures)
-                                  "c2_greedy256", "c3_4096", "c3_4096_t600"])
+                                  "c2_greedy256", "c3_4096", "c3_4096_t600",
+                                  # the C3 world with every event kind; the C3 start with reference Greedy bots
+                                  "c3_4096_virus", "c3_greedy4096"])
 def test_reference_states(name):
     """Start both from the reference's own initial world (tests/golden), replay its commands."""
     z = parity.load_golden(name)

@@ -22,7 +22,10 @@ SCENARIOS = ["c1_greedy", "greedy16", "greedy16_virus_split", "stress_virus", "c
              "simple16", "cnn42", "cnn84",
              # BASELINE.json configs[1] (256 Greedy bots, 10k pellets) and configs[2] (the headline C3 world:
              # 4096 bots, 100k pellets, 1152 viruses, split + eject) from the bench's matured worlds
-             "c2_greedy256", "c3_4096", "c3_4096_t600"]
+             "c2_greedy256", "c3_4096", "c3_4096_t600",
+             # the C3 world with every event kind (virus eats, explosions, virus splits, merges) and the C3
+             # start world with the reference's own Greedy bots
+             "c3_4096_virus", "c3_greedy4096"]
 
 
 def _same(a, b):
@@ -85,3 +88,15 @@ def test_golden_covers_every_event_kind(golden_dir):
         z = np.load(os.path.join(golden_dir, name + ".npz"))
         seen |= set(np.unique(z["events"][:, 0]).tolist()) if len(z["events"]) else set()
     assert seen == set(range(1, 11))
+
+
+def test_headline_fixtures_hold_every_event_kind(golden_dir):
+    """at the headline size (4096 bots, 100k pellets, 1152 viruses) the reference's
+    own runs pin every event kind -- merges, virus eats and splits, cell eats of viruses,
+    explosions, pellet / blob / cell eats, deaths and respawns (field.py:183-370)."""
+    kinds = set()
+    for name in ("c3_4096", "c3_4096_t600", "c3_4096_virus", "c3_greedy4096"):
+        z = np.load(os.path.join(golden_dir, name + ".npz"))
+        assert int(z["n_players"]) == 4096 and float(z["max_pellets"]) == 100000.0
+        kinds |= set(z["events"][:, 0].tolist())
+    assert kinds == set(range(1, 11)), sorted(kinds)

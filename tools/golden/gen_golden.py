@@ -328,14 +328,60 @@ SCENARIOS = {
     # eject p = 1e-2 per bot-tick.  Every bot is observed every tick (its last-frame
     # grids evolve as in the device / oracle runs); the full 854-value rows are kept at the last tick.
     "c3_4096": dict(n=4096, driver="bench", load="data/c3_t50.npz", virus=True, split=True, eject=True,
-                    p_split=2.5e-3, p_eject=1e-2, ticks=4, ck_every=4, obs=True, obs_init_stored=False, seed=12),
+                    p_split=2.5e-3, p_eject=1e-2, ticks=10, ck_every=5, obs=True, obs_init_stored=False, seed=12),
     # the same world size from the late matured world (data/c3_t600.npz: 6233 cells, 580 past mass 125,
     # 673 multi-cell players) with more splits and ejections, so that the headline size also pins
     # splits, ejected blobs, virus eating and explosions
     "c3_4096_t600": dict(n=4096, driver="bench", load="data/c3_t600.npz", virus=True, split=True, eject=True,
                          p_split=0.03, p_eject=0.05, ticks=4, ck_every=4, obs=True, obs_init_stored=False,
                          seed=13),
+    # the headline world with every event kind: the tick-600 world with a few players set up
+    # next to viruses -- 400-mass cells on 100-mass viruses (playerVirusOverlap + the explosion,
+    # field.py:225-231, 350-370), 150-mass cells ejecting at 195-mass viruses (virusBlobOverlap + the
+    # virus split, field.py:246-253, 315-324), multi-cell players whose merge timers ran out steered to
+    # their centre (mergePlayerCells) -- everyone else on bench.py's policy
+    "c3_4096_virus": dict(n=4096, driver="bench", load="data/c3_t600.npz", virus=True, split=True, eject=True,
+                          p_split=2.5e-3, p_eject=1e-2, ticks=16, ck_every=8, obs=True, obs_init_stored=False,
+                          seed=14, setup="virus_events"),
+    # the headline start world with the reference's own Greedy bots (bot.py:579-633, ENABLE_GREEDY_SPLIT)
+    "c3_greedy4096": dict(n=4096, driver="greedy", load="data/c3_t50.npz", virus=True, split=True, eject=True,
+                          greedy_split=True, ticks=4, ck_every=4, obs=True, obs_init_stored=False, seed=15),
 }
+
+
+def setup_virus_events(field):
+    """c3_4096_virus: mutate the loaded world before tick 1 (the snapshot "init/" is taken after it,
+    so the fixture's start world holds the mutations); returns per-player command overrides
+    [(player, (x, y), eject)] applied on top of the bench policy every tick."""
+    size = field.size
+    vir = [v for v in field.viruses if 80 < v.x < size - 80 and 80 < v.y < size - 80]
+    singles = [i for i, p in enumerate(field.players) if p.getIsAlive() and len(p.cells) == 1]
+    multis = [i for i, p in enumerate(field.players) if p.getIsAlive() and len(p.cells) >= 3]
+    # spread the picks over the lists (neighbouring indices are unrelated places on the field)
+    pick = lambda lst, k, n: lst[(k * len(lst)) // n]
+    over = []
+    for k in range(6):  # eaters: overlap (cell.py:143-152) and mass > 1.25 x virus mass at tick 1
+        v, i = vir[k * 7], pick(singles, k, 12)
+        c = field.players[i].cells[0]
+        c.setMass(400.0)
+        c.setPos([float(v.x) + 4.0, float(v.y) - 3.0])
+        over.append((i, (float(v.x), float(v.y)), False))
+    for k in range(6, 12):  # feeders: one 14.4-mass blob takes a 195-mass virus past 200.8
+        v, i = vir[k * 7], pick(singles, k, 12)
+        v.setMass(195.0)
+        c = field.players[i].cells[0]
+        c.setMass(150.0)
+        c.setPos([float(v.x) - 20.0, float(v.y)])
+        over.append((i, (float(v.x), float(v.y)), True))
+    for k in range(8):  # mergers
+        i = pick(multis, k, 8)
+        cells = field.players[i].cells
+        for c in cells:
+            c.mergeTime = 0.0
+        cx = sum(float(c.x) for c in cells) / len(cells)
+        cy = sum(float(c.y) for c in cells) / len(cells)
+        over.append((i, (cx, cy), False))
+    return over
 OBS_SIMPLE = 0x400  # include/aigar.h AIGAR_OBS_SIMPLE
 
 
@@ -510,6 +556,9 @@ def run_scenario(ref, rec, name, sc):
                                   min(field.size, max(0, c0.y + 6 * math.sin(ang))), 40.0 + 5 * k, p)
                 c.mergeTime = float(k)
                 p.addCell(c)
+    overrides = []
+    if sc.get("setup") == "virus_events":
+        overrides = setup_virus_events(field)
     if driver == "feed":
         v = field.viruses[0]
         big = field.players[0].cells[0]
@@ -568,6 +617,10 @@ def run_scenario(ref, rec, name, sc):
             model.takeBotActions()
         elif driver == "bench":
             bench_commands(field, obs_bots, rng, sc)
+            for i, (x, y), e in overrides:
+                p = field.players[i]
+                if p.getIsAlive():
+                    p.setCommands(x, y, False, e)
         else:
             cmds = scripted_commands(field, rng, sc) if driver == "scripted" else feed_commands(field, rng, t)
             for p, (x, y, s, e) in zip(field.players, cmds):
