@@ -68,6 +68,41 @@ __device__ __forceinline__ int64_t readlane_i64(int64_t v, int k) {
   return (int64_t)(((unsigned long long)hi << 32) | lo);
 }
 
+// getAdditionalFeatures (bot.py:302-323) in two halves.  extra_load, with the
+// kernel's first load round: lane k loads input k (0 lastFovSize, 1 total mass,
+// 2-5 the last action, 6-9 the one before) -- loaded at the end, lane 0's loads
+// waited behind the wave's row stores (vmcnt counts stores too on gfx9) and added
+// a dependent memory round to every wave's tail.  extra_store, at the end: each
+// lane writes its own feature (lane 10 the current fov size, which it records as
+// the next lastFovSize).
+__device__ __forceinline__ double extra_load(const Dev &d, int gp, int lane) {
+  const uint32_t ex = d.obs_ex;
+  const double *src = nullptr;
+  if (lane == 0 && (ex & AIGAR_EX_LAST_FOV)) src = d.o_lastfov + gp;
+  else if (lane == 1 && (ex & AIGAR_EX_MASS)) src = d.p_mass + gp;
+  else if (lane >= 2 && lane < 6 && (ex & AIGAR_EX_LAST_ACT)) src = d.o_act_cur + (size_t)gp * 4 + (lane - 2);
+  else if (lane >= 6 && lane < 10 && (ex & AIGAR_EX_2LAST_ACT)) src = d.o_act_prev + (size_t)gp * 4 + (lane - 6);
+  return src ? *src : 0.0;
+}
+template <typename OutT>
+__device__ __forceinline__ void extra_store(const Dev &d, int gp, int lane, OutT *row, int off, double fs, double xin) {
+  const uint32_t ex = d.obs_ex;
+  const int lf = (ex & AIGAR_EX_LAST_FOV) ? 1 : 0, fv = (ex & AIGAR_EX_FOV) ? 1 : 0;
+  const int ms = (ex & AIGAR_EX_MASS) ? 1 : 0, la = (ex & AIGAR_EX_LAST_ACT) ? 4 : 0;
+  int o = -1;
+  double v = xin;
+  if (lane == 0 && lf) o = off;
+  else if (lane == 1 && ms) o = off + lf + fv;
+  else if (lane >= 2 && lane < 6 && la) o = off + lf + fv + ms + (lane - 2);
+  else if (lane >= 6 && lane < 10 && (ex & AIGAR_EX_2LAST_ACT)) o = off + lf + fv + ms + la + (lane - 6);
+  else if (lane == 10 && fv) {
+    o = off + lf;
+    v = fs;
+    d.o_lastfov[gp] = fs;
+  }
+  if (o >= 0) row[o] = (OutT)v;
+}
+
 // One list of visible objects (structure of arrays).  Lives in LDS; when a
 // bot sees more objects than the LDS list holds, the same scan is repeated
 // into a slice of the global overflow pool (exact, only slower).
@@ -311,6 +346,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const int oslot = lane < kMaxCells ? (int)d.p_list[lane * NP + gp] : 0;
   const ArenaCtl &ctl = d.ctl[a];
   const double rmax_c = ctl.rmax_cell, rmax_v = ctl.rmax_virus;  // (the walk's grid expansions)
+  const double xin = extra_load(d, gp, lane);
   if (!alive) {  // getStateRepresentation returns None for dead players
     for (int i = lane; i < L; i += 64) row_st(0, i, (OutT)__builtin_nan(""));
     return;
@@ -891,20 +927,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
 #ifdef AIGAR_OBS_TIMING
   if (lane < OBS_TS && gp < 65536) g_obs_ts[(size_t)gp * OBS_TS + lane] = obs_ts_l[lane];
 #endif
-  if (lane == 0) {  // getAdditionalFeatures (bot.py:302-323)
-    const uint32_t ex = d.obs_ex;
-    int o = off;
-    if (ex & AIGAR_EX_LAST_FOV) row[o++] = (OutT)d.o_lastfov[gp];
-    if (ex & AIGAR_EX_FOV) {
-      d.o_lastfov[gp] = fs;
-      row[o++] = (OutT)fs;
-    }
-    if (ex & AIGAR_EX_MASS) row[o++] = (OutT)d.p_mass[gp];
-    if (ex & AIGAR_EX_LAST_ACT)
-      for (int k = 0; k < 4; k++) row[o++] = (OutT)d.o_act_cur[(size_t)gp * 4 + k];
-    if (ex & AIGAR_EX_2LAST_ACT)
-      for (int k = 0; k < 4; k++) row[o++] = (OutT)d.o_act_prev[(size_t)gp * 4 + k];
-  }
+  extra_store(d, gp, lane, row, off, fs, xin);  // getAdditionalFeatures (bot.py:302-323)
 }
 
 // Python round(v, 5) (getRelativeCellPos, bot.py:16-21): round-half-even of
