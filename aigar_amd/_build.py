@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 SO = os.path.join(HERE, "libaigar_hip.so")
 SOURCES = ["tick.hip", "obs.hip", "api.hip"]
 HEADERS = ["aigar_sem.h", "aigar_dev.h", "aigar_math.h", "aigar_trig.h", "aigar_wave.h", "aigar_glibc_pow_tables.h",
-           "aigar_trig_tables.h", "pixels.inc", "obs_wide.inc", os.path.join("..", "..", "include", "aigar.h")]
+           "aigar_trig_tables.h", "aigar_glibc_trig.h", "aigar_glibc_trig_tables.h", "pixels.inc", "obs_wide.inc", os.path.join("..", "..", "include", "aigar.h")]
 ARCH = os.environ.get("AIGAR_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no FMA contraction, every fp64 operation rounds like the
 # reference's Python floats.

@@ -95,6 +95,7 @@ def load(build_if_missing=False):
         "aigar_profile": [vp, i32],
         "aigar_kernel_time": [vp, C.c_char_p, dp, C.POINTER(i32)],
         "aigar_selftest_pow": [dp, dp, dp, i32],
+        "aigar_selftest_trig": [dp, dp, dp, i32],
         "aigar_counters": [vp, i32, C.POINTER(C.c_int64), i32],
         "aigar_policy_greedy": [vp, i32, vp, i32],
         "aigar_apply_actions": [vp, vp, i32, i32, i32, i32, i32],
@@ -506,6 +507,19 @@ def tile_exchange_local(steppers):
     arr = (C.c_void_p * len(steppers))(*[s.h.value for s in steppers])
     if L.aigar_tile_exchange_local(arr, len(steppers)) < 0:
         raise RuntimeError("aigar: " + L.aigar_last_error().decode())
+
+
+def selftest_trig(y, x):
+    """Device atan2(y, x), sin(x), cos(x) (glibc's, restated in aigar_glibc_trig.h) for host arrays."""
+    L = load()
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.zeros(3 * len(x))
+    dp = C.POINTER(C.c_double)
+    if L.aigar_selftest_trig(y.ctypes.data_as(dp), x.ctypes.data_as(dp), out.ctypes.data_as(dp), len(x)) < 0:
+        raise RuntimeError("aigar: " + L.aigar_last_error().decode())
+    n = len(x)
+    return out[:n], out[n:2 * n], out[2 * n:]
 
 
 def selftest_pow(x, y):

@@ -7,7 +7,7 @@
 #include <stdint.h>
 
 #include "aigar_math.h"
-#include "aigar_trig.h"
+#include "aigar_glibc_trig.h"
 
 #define AIGAR_D __device__ __forceinline__
 
@@ -117,7 +117,7 @@ AIGAR_D void set_move_direction(double x, double y, double m, double r, double c
   double xd = cpx - x, yd = cpy - y;
   double hyp = xd * xd + yd * yd, r2 = r * r;
   double mod = hyp >= r2 ? 1.0 : hyp / r2;  // min(hyp, r2) / r2 (r2 / r2 is exactly 1: no division then)
-  double ang = aigar_math::trig_atan2(yd, xd);  // correctly rounded (aigar_trig.h)
+  double ang = aigar_math::trig_atan2(yd, xd);  // glibc's atan2, bit for bit (aigar_glibc_trig.h)
   double sp = kMoveSpeed * aigar_math::pow_glibc(m, -0.35);  // glibc pow, bit for bit (aigar_math.h)
   aigar_math::trig_sincos(ang, s, c);
   vx = sp * mod * c;

@@ -156,20 +156,4 @@ AIGAR_HD double atan2_cr(double y, double x) {
   return yneg ? -v : v;
 }
 
-// the stepper's trig entry points (AIGAR_LIBM_TRIG: OCML instead, A/B builds only)
-AIGAR_HD double trig_atan2(double y, double x) {
-#ifdef AIGAR_LIBM_TRIG
-  return atan2(y, x);
-#else
-  return atan2_cr(y, x);
-#endif
-}
-AIGAR_HD void trig_sincos(double a, double &s, double &c) {
-#ifdef AIGAR_LIBM_TRIG
-  s = sin(a);
-  c = cos(a);
-#else
-  sincos_cr(a, s, c);
-#endif
-}
 }  // namespace aigar_math

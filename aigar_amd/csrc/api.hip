@@ -1906,3 +1906,33 @@ extern "C" int aigar_selftest_pow(const double *x, const double *y, double *out,
   (void)hipFree(dz);
   return 0;
 }
+
+// out[0, n): atan2(y, x); out[n, 2n): sin(x); out[2n, 3n): cos(x) -- the stepper's trig
+// entry points (aigar_glibc_trig.h), one thread per element
+__global__ void k_selftest_trig(const double *y, const double *x, double *out, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = aigar_math::trig_atan2(y[i], x[i]);
+  double s, c;
+  aigar_math::trig_sincos(x[i], s, c);
+  out[n + i] = s;
+  out[2 * (size_t)n + i] = c;
+}
+
+extern "C" int aigar_selftest_trig(const double *y, const double *x, double *out, int n) {
+  if (!x || !y || !out || n < 0) return fail("null argument");
+  double *dx = nullptr, *dy = nullptr, *dz = nullptr;
+  const size_t b = sizeof(double) * (size_t)(n > 0 ? n : 1);
+  HIPCHK(hipMalloc(&dx, b));
+  HIPCHK(hipMalloc(&dy, b));
+  HIPCHK(hipMalloc(&dz, 3 * b));
+  HIPCHK(hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy, y, sizeof(double) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_selftest_trig, dim3((n + 255) / 256), dim3(256), 0, 0, dy, dx, dz, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dz, 3 * sizeof(double) * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dz);
+  return 0;
+}

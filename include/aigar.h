@@ -436,6 +436,11 @@ int aigar_counters(aigar_handle *h, int arena, int64_t *out, int n);
  * for bit) on host arrays of n (x, y) pairs -- used by the parity tests. */
 int aigar_selftest_pow(const double *x, const double *y, double *out, int n);
 
+/* Diagnostics: evaluate the device's trig (aigar_glibc_trig.h: glibc 2.35's
+ * __ieee754_atan2_fma / __sin_fma / __cos_fma, bit for bit) on host arrays:
+ * out[0, n) = atan2(y, x), out[n, 2n) = sin(x), out[2n, 3n) = cos(x). */
+int aigar_selftest_trig(const double *y, const double *x, double *out, int n);
+
 #ifdef __cplusplus
 }
 #endif

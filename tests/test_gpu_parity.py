@@ -45,6 +45,30 @@ def test_device_pow_is_glibc_pow():
     assert np.array_equal(dev, glibc), np.argwhere(dev != glibc)[:5]  # bit for bit (aigar_math.h)
 
 
+def test_device_trig_is_glibc_trig():
+    """The device's atan2 / sin / cos (aigar_glibc_trig.h) equal the C library's -- what the
+    reference's math.atan2 / math.sin / math.cos call (cell.py:47-103, field.py:363-365) -- bit
+    for bit: move directions from coordinate differences, the angles atan2 returns, integer
+    degrees, and the s_sin.c / e_atan2.c range seams."""
+    rng = np.random.default_rng(1)
+    n = 100000
+    x = np.concatenate([rng.uniform(-4800, 4800, n), rng.uniform(-1e-3, 1e-3, n),
+                        np.ldexp(rng.uniform(-1, 1, n), rng.integers(-40, 40, n)), [0.0, -0.0, 0.0, -0.0, 5.0]])
+    y = np.concatenate([rng.uniform(-4800, 4800, n), rng.uniform(-1e-3, 1e-3, n),
+                        np.ldexp(rng.uniform(-1, 1, n), rng.integers(-40, 40, n)), [0.0, 0.0, -0.0, -0.0, 0.0]])
+    at, _, _ = _lib.selftest_trig(y, x)
+    ref = np.array([math.atan2(b, a) for b, a in zip(y, x)])
+    assert np.array_equal(at.view(np.int64), ref.view(np.int64)), np.argwhere(at != ref)[:5]
+    seams = np.concatenate([b * (1 + np.arange(-200, 201) * 2.0 ** -52)
+                            for b in (2.0 ** -26, 0.126, 0.855469, 2.426265, math.pi, 2 * math.pi)])
+    a = np.concatenate([ref, np.deg2rad(np.arange(360)), rng.uniform(-7, 7, n), seams, -seams])
+    _, s, c = _lib.selftest_trig(np.zeros_like(a), a)
+    rs = np.array([math.sin(v) for v in a])
+    rc = np.array([math.cos(v) for v in a])
+    assert np.array_equal(s.view(np.int64), rs.view(np.int64)), np.argwhere(s != rs)[:5]
+    assert np.array_equal(c.view(np.int64), rc.view(np.int64)), np.argwhere(c != rc)[:5]
+
+
 def test_reset_is_identical():
     cfg = make_config(bots=64, virus=True, max_viruses=20, channels=FULL_CH, extras=0x1F)
     g, o = pair(cfg, 11)

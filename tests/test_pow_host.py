@@ -58,3 +58,25 @@ def test_pellet_radius_constants():
     assert sorted(consts) == ["1", "2", "3"]
     for m, c in consts.items():
         assert float.fromhex(c) == math.sqrt(int(m) / math.pi), m
+
+
+def test_glibc_trig_matches_libm(tmp_path):
+    """aigar_glibc_trig.h sin / cos / atan2 == the C library's (which the reference's math
+    module calls) on ~11 M inputs shaped like the path's (host build); where the static libm
+    is present, also == its FMA variants __sin_fma / __cos_fma / __ieee754_atan2_fma, linked
+    directly.  -fno-builtin-*: gcc would otherwise fuse sin(a), cos(a) into sincos(), a
+    different glibc routine (oracle/Makefile does the same)."""
+    exe = str(tmp_path / "check_glibc_trig")
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-builtin-sin", "-fno-builtin-cos",
+           "-fno-builtin-atan2", "-I", os.path.join(ROOT, "aigar_amd", "csrc"),
+           os.path.join(ROOT, "tools", "gen", "check_glibc_trig.cpp"), "-o", exe]
+    libm_a = "/usr/lib/x86_64-linux-gnu/libm-2.35.a"
+    if os.path.exists(libm_a):
+        objs = ["s_sin-fma.o", "e_atan2-fma.o", "sincostab.o", "branred.o"]
+        subprocess.check_call(["ar", "x", libm_a] + objs, cwd=str(tmp_path))
+        cmd[1:1] = ["-DAIGAR_LINK_FMA_VARIANTS"]
+        cmd += [str(tmp_path / o) for o in objs]
+    subprocess.check_call(cmd)
+    out = subprocess.run([exe, "5000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout, out.stdout
