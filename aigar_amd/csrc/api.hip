@@ -27,7 +27,8 @@ void launch_pel_gather(const Dev &d, hipStream_t s, int a);
 void launch_tile_apply(const Dev &d, hipStream_t s, int box_recs, int first);
 void launch_reset(const Dev &d, hipStream_t s, uint64_t seed);
 void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch,
-                    const uint8_t *mask = nullptr);
+                    const uint8_t *mask = nullptr, int greedy_next = -1);
+bool observe_fuses_greedy(const Dev &d);
 void launch_policy_refrandom(const Dev &d, hipStream_t s, int skip_rate, int enable_split, int enable_eject,
                              uint64_t salt);
 int launch_observe_pixels(const Dev &d, hipStream_t s, void *out, int dtype, int side, uint64_t seed, uint8_t *ovf);
@@ -673,7 +674,11 @@ extern "C" int aigar_step(aigar_handle *h, int n_ticks) {
 // bot's getStateRepresentation (model.py:100-112, bot.py:272-299) -- captured
 // once as a single hipGraph and replayed n_steps times: no host round trip
 // between the policy, the tick's ~25 kernels and the observation.
-static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_params &p, void *out, int dtype) {
+// policy_done: this step's Greedy moves were picked by the previous step's
+// observation (fuse_next there); fuse_next: this step's observation also picks the
+// next step's Greedy moves (observe_fuses_greedy) -- one launch fewer per step
+static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_params &p, void *out, int dtype,
+                            bool policy_done = false, bool fuse_next = false) {
   // the random population's policy runs inside the tick's first kernel (same draws as aigar_policy_random)
 #ifdef AIGAR_NO_POLICY_FOLD  // (diagnostics build: the policy as its own launch)
   const RandomPolicy rp{0, 0, 0, 0};
@@ -681,7 +686,7 @@ static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_para
 #else
   const RandomPolicy rp{p.policy == AIGAR_POLICY_RANDOM, p.p_split, p.p_eject, p.seed};
 #endif
-  if (p.policy == AIGAR_POLICY_GREEDY) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr, -1);
+  if (p.policy == AIGAR_POLICY_GREEDY && !policy_done) launch_policy_greedy(h->d, s, p.greedy_split ? 1 : 0, nullptr, -1);
   // a Greedy population splits by choice: many players hold several cells, and the
   // eat-phase preparation and the pp activity test share a block's cells among its
   // waves (r05 v41: greedy 16.9 -> 18.2 M env-steps/s; the random population keeps
@@ -689,7 +694,12 @@ static void launch_env_step(aigar_handle *h, hipStream_t s, const aigar_run_para
   Dev dt = h->d;
   dt.share_cells = p.policy == AIGAR_POLICY_GREEDY ? 1 : 0;
   launch_tick(dt, s, food_rounds(h), h->scr_k, h->scr_v, &rp);
-  if (out) launch_observe(h->d, s, out, dtype, 0);  // epoch 0: the device-side epoch
+  if (out) launch_observe(h->d, s, out, dtype, 0, nullptr, fuse_next ? (p.greedy_split ? 1 : 0) : -1);  // epoch 0: the device-side epoch
+}
+// aigar_run's unrolled graph may carry each step's Greedy moves in the step before
+static bool run_fuses_greedy(const aigar_handle *h, const aigar_run_params &p, const void *out) {
+  return p.policy == AIGAR_POLICY_GREEDY && out && observe_fuses_greedy(h->d) &&
+         !getenv("AIGAR_NO_GREEDY_FUSE");
 }
 
 extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p, void *obs_out, int dtype) {
@@ -721,8 +731,12 @@ extern "C" int aigar_run(aigar_handle *h, int n_steps, const aigar_run_params *p
   if (h->run_graph && !h->run_graph_u && !h->run_u_tried && h->run_unroll > 1 && n_steps >= h->run_unroll &&
       !h->profile) {
     h->run_u_tried = true;
+    // (the Greedy population: steps 1.. of the graph take the moves their previous
+    // step's observation picked -- the first step, and the one-step graph, run the policy)
+    const bool fuse = run_fuses_greedy(h, *p, obs_out);
     h->run_graph_u = capture_graph(h, [&](hipStream_t cs) {
-      for (int k = 0; k < h->run_unroll; k++) launch_env_step(h, cs, *p, obs_out, dtype);
+      for (int k = 0; k < h->run_unroll; k++)
+        launch_env_step(h, cs, *p, obs_out, dtype, fuse && k > 0, fuse && k + 1 < h->run_unroll);
     });
   }
   int t = 0;

@@ -103,6 +103,118 @@ __device__ __forceinline__ void extra_store(const Dev &d, int gp, int lane, OutT
   if (o >= 0) row[o] = (OutT)v;
 }
 
+// Python round(v, 5) (getRelativeCellPos, bot.py:16-21): round-half-even of
+// the exact binary value to a multiple of 1e-5, as the double nearest k/1e5
+__device__ __forceinline__ double py_round5(double v) {
+  double p = v * 100000.0;
+  double e = fma(v, 100000.0, -p);  // p + e == 1e5 * v exactly
+  double k0 = floor(p), f, dd;
+  if (p == k0 && e < 0) {
+    f = k0 - 1;
+    dd = 1.0;
+  } else {
+    f = k0;
+    dd = p - k0;
+  }
+  double g = dd - 0.5;
+  int sgn = (g != 0) ? (g > 0 ? 1 : -1) : (e > 0 ? 1 : (e < 0 ? -1 : 0));
+  double k = (sgn > 0) ? f + 1 : (sgn < 0) ? f : ((fmod(f, 2.0) == 0.0) ? f : f + 1);
+  double r = k / 100000.0;
+  if (r == 0.0) r = copysign(0.0, v);
+  return r;
+}
+
+// make_greedy_bot_move (bot.py:579-633) in three parts, shared by k_policy_greedy
+// and the observation that computes the next tick's Greedy moves on its own walk
+// (k_observe<..., GREEDY>: aigar_run with the Greedy population).
+// (1) the biggest own cell: max(playerCells, key=mass) keeps the first maximum;
+// lane k holds cell k's (mass, x, y) (mass -1 past the list), all lanes get the winner
+__device__ __forceinline__ void greedy_own_best(double &bm, double &bx, double &by) {
+  const int lane = threadIdx.x & 63;
+  int bl = lane;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double om = __shfl_xor(bm, off);
+    int ol = __shfl_xor(bl, off);
+    if (om > bm || (om == bm && ol < bl)) {
+      bm = om;
+      bl = ol;
+    }
+  }
+  bx = __shfl(bx, bl);
+  by = __shfl(by, bl);
+}
+// (2) per lane: the best mass / distance^2 candidate seen, ties to the first in list
+// order (pellets, enemy cells, viruses, each by creation sequence); a candidate has
+// passed the liveness, own-cell and isInFov tests
+struct GreedyAcc {
+  double best = -1;
+  uint64_t bord = ~0ull;
+  double tx = 0, ty = 0;
+  __device__ __forceinline__ void consider(int kd, double x, double y, double m, int64_t seq, double bm, double bx,
+                                           double by) {
+    if (kd != 0 && !(bm > 1.25 * m)) return;  // the biggest own cell must be able to eat it
+    const double sd = (x - bx) * (x - bx) + (y - by) * (y - by);
+    const double k = m / (sd != 0 ? sd : 1);
+    const uint64_t ord = ((uint64_t)kd << 56) | (uint64_t)seq;
+    if (k > best || (k == best && ord < bord)) {
+      best = k;
+      bord = ord;
+      tx = x;
+      ty = y;
+    }
+  }
+};
+// (3) the wave's best, then set_command_point (bot.py:550-577) by lane 0
+__device__ __forceinline__ void greedy_commit(const Dev &d, int gp, GreedyAcc acc, double fx, double fy, double fs,
+                                              int greedy_split) {
+  const int lane = threadIdx.x & 63, a = gp / d.B, p = gp - a * d.B;
+  double best = acc.best, tx = acc.tx, ty = acc.ty;
+  uint64_t bord = acc.bord;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double ok = __shfl_xor(best, off);
+    uint64_t oo = __shfl_xor(bord, off);
+    double ox = __shfl_xor(tx, off), oy = __shfl_xor(ty, off);
+    if (ok > best || (ok == best && oo < bord)) {
+      best = ok;
+      bord = oo;
+      tx = ox;
+      ty = oy;
+    }
+  }
+  if (lane != 0) return;
+  const ArenaCtl &ctl = d.ctl[a];
+  const int64_t ix = (int64_t)fx, iy = (int64_t)fy;
+  const int64_t left = ix - (int64_t)(fs / 2), top = iy - (int64_t)(fs / 2);
+  uint64_t u[4];
+  philox((uint64_t)p, ST_GREEDY, (uint64_t)ctl.tick, 0, ctl.key0, ctl.key1, u);
+  double a0, a1;
+  if (bord != ~0ull) {  // getRelativeCellPos(bestCell, left, top, size)
+    a0 = py_round5((tx - (double)left) / fs);
+    a1 = py_round5((ty - (double)top) / fs);
+  } else {
+    a0 = u01(u[0]);
+    a1 = u01(u[1]);
+  }
+  int split = 0, eject = 0;
+  if (greedy_split) {  // ENABLE_GREEDY_SPLIT: randint(0, 10000) > splitLikelihood
+    int lh = d.p_split_lh[gp];
+    if (lh <= 0) {
+      uint64_t v[4];
+      philox((uint64_t)p, ST_GREEDY_LH, 0, 0, ctl.key0, ctl.key1, v);
+      lh = (int)ph_randint(v[0], 9950, 10000);
+    }
+    split = ph_randint(u[2], 0, 10000) > lh;
+    eject = ph_randint(u[3], 0, 10000) > 100000;  // ejectLikelihood (bot.py:94)
+  }
+  const int64_t isz = (int64_t)fs;  // set_command_point: left + action * int(size)
+  d.p_cmdx[gp] = (double)left + a0 * (double)isz;
+  d.p_cmdy[gp] = (double)top + a1 * (double)isz;
+  d.p_split[gp] = split;
+  d.p_eject[gp] = eject;
+}
+
 // One list of visible objects (structure of arrays).  Lives in LDS; when a
 // bot sees more objects than the LDS list holds, the same scan is repeated
 // into a slice of the global overflow pool (exact, only slower).
@@ -271,8 +383,13 @@ __device__ __forceinline__ void wave_fov_walk(const Dev &d, int a, Rect Q, doubl
 #endif
 // WT: the store policy of the row and the history (below), chosen per launch by
 // the number of bots (launch_observe)
-template <typename OutT, bool WT>
-__global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch, const uint8_t *mask) {
+// GREEDY (aigar_run with the Greedy population): the walk also picks every bot's
+// next Greedy move (make_greedy_bot_move, bot.py:579-633: it reads the world this
+// observation reads -- nothing changes before the next tick's policy), so that
+// tick needs no k_policy_greedy launch; greedy_split as for k_policy_greedy
+template <typename OutT, bool WT, bool GREEDY>
+__global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint32_t epoch, const uint8_t *mask,
+                                                         int greedy_split) {
   FLOOR(9);
   // p_seq / p_perm are reused, once the pellets are ranked, for the masses and
   // masks in creation order (no indirection in the per-square sums)
@@ -366,6 +483,11 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     orad = d.c_r[ci];
     omass = d.c_m[ci];
   }
+  // GREEDY: the biggest own cell (greedy_own_best) from the same loads
+  double g_bm = lane < ncell ? omass : -1.0, g_bx = ox, g_by = oy;
+  if constexpr (GREEDY) greedy_own_best(g_bm, g_bx, g_by);
+  GreedyAcc gacc_best;
+  bool gacc = GREEDY;  // (the first walk only: an overflow walk sees the same candidates again)
   const double left = fx - fs / 2, top = fy - fs / 2, gs = fs / G, inv_gs = 1.0 / gs;
   const int cols = (int)ceil(fs / gs);
   const double lim = fs - 1;
@@ -433,7 +555,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       const double *Y = kd == 0 ? &PR->y : (kd == 1 ? d.c_y : d.v_y);
       const double *M = kd == 0 ? &PR->m : (kd == 1 ? d.c_m : d.v_m);
       const double *RR = kd == 1 ? d.c_r : d.v_r;
-      const int64_t *S = kd == 0 ? &PR->seq : d.v_seq;
+      const int64_t *S = kd == 0 ? &PR->seq : (kd == 1 ? d.c_seq : d.v_seq);
       const uint32_t *FL = kd == 1 ? d.c_flags : d.v_flags;
       const size_t gr = kd == 0 ? g * kPelStride : g;
       bool ok = false;
@@ -444,12 +566,14 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
         y = Y[gr];
         m = M[gr];
         r = kd == 0 ? 0.0 : RR[g];
-        sq = kd == 1 ? 0 : S[gr];
+        sq = (kd == 1 && !GREEDY) ? 0 : S[gr];
         uint32_t fl = kd == 0 ? (F_ALIVE | F_INHASH) : FL[g];
         if (kd == 0) r = pellet_radius(m);
         // (the hash query's footprint test is implied by isInFov: aigar_sem.h in_fov)
         ok = (fl & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) && !(kd == 1 && pool_owner(g) == gp) &&
              in_fov(x, y, r, fx, fy, fs);
+        if constexpr (GREEDY)  // (k_policy_greedy's filter exactly: liveness, not its own cell, isInFov)
+          if (gacc && ok) gacc_best.consider(kd, x, y, m, sq, g_bm, g_bx, g_by);
       }
       uint32_t msk = 0;
       if (ok) {
@@ -473,6 +597,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     ObjList C0{nullptr, c_mass, nullptr, c_mask, c_own, nullptr};
     ObjList V0{v_seqs, v_mass, v_rad, v_mask, nullptr, nullptr};
     walk(P0, OBS_PCAP, C0, OBS_CCAP, V0, OBS_VCAP, np, nc, nv);
+  }
+  if constexpr (GREEDY) {
+    greedy_commit(d, gp, gacc_best, fx, fy, fs, greedy_split);
+    gacc = false;
   }
   OBS_STAMP(2);
 #if defined(AIGAR_OBS_STOP) && AIGAR_OBS_STOP == 2
@@ -934,26 +1062,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   extra_store(d, gp, lane, row, off, fs, xin);  // getAdditionalFeatures (bot.py:302-323)
 }
 
-// Python round(v, 5) (getRelativeCellPos, bot.py:16-21): round-half-even of
-// the exact binary value to a multiple of 1e-5, as the double nearest k/1e5
-__device__ __forceinline__ double py_round5(double v) {
-  double p = v * 100000.0;
-  double e = fma(v, 100000.0, -p);  // p + e == 1e5 * v exactly
-  double k0 = floor(p), f, dd;
-  if (p == k0 && e < 0) {
-    f = k0 - 1;
-    dd = 1.0;
-  } else {
-    f = k0;
-    dd = p - k0;
-  }
-  double g = dd - 0.5;
-  int sgn = (g != 0) ? (g > 0 ? 1 : -1) : (e > 0 ? 1 : (e < 0 ? -1 : 0));
-  double k = (sgn > 0) ? f + 1 : (sgn < 0) ? f : ((fmod(f, 2.0) == 0.0) ? f : f + 1);
-  double r = k / 100000.0;
-  if (r == 0.0) r = copysign(0.0, v);
-  return r;
-}
 
 // Model.takeBotActions for Greedy bots (bot.py:252-269): make_greedy_bot_move
 // (bot.py:579-633) then set_command_point (bot.py:550-577).  One wavefront per
@@ -963,12 +1071,10 @@ __device__ __forceinline__ double py_round5(double v) {
 // each by creation sequence).  mask (optional): which players are Greedy bots.
 // mask: NULL = every player; want < 0: players with mask != 0; else mask == want
 __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, const uint8_t *mask, int want) {
-  const int gp = xcd_block(blockIdx.x, gridDim.x), lane = threadIdx.x, NP = d.NP, a = gp / d.B, p = gp - a * d.B;
+  const int gp = xcd_block(blockIdx.x, gridDim.x), lane = threadIdx.x, NP = d.NP, a = gp / d.B;
   if (!d.p_alive[gp] || (mask && (want < 0 ? !mask[gp] : mask[gp] != want))) return;  // (dead players keep their command)
   const ArenaCtl &ctl = d.ctl[a];
   const double fx = d.p_fx[gp], fy = d.p_fy[gp], fs = d.p_fs[gp];
-  const int64_t ix = (int64_t)fx, iy = (int64_t)fy;
-  const int64_t left = ix - (int64_t)(fs / 2), top = iy - (int64_t)(fs / 2);
   // biggest own cell: max(playerCells, key=mass) keeps the first maximum
   const int ncell = d.p_ncells[gp];
   double bm = -1, bx = 0, by = 0;
@@ -978,24 +1084,11 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
     bx = d.c_x[ci];
     by = d.c_y[ci];
   }
-  int bl = lane;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double om = __shfl_xor(bm, off);
-    int ol = __shfl_xor(bl, off);
-    if (om > bm || (om == bm && ol < bl)) {
-      bm = om;
-      bl = ol;
-    }
-  }
-  bx = __shfl(bx, bl);
-  by = __shfl(by, bl);
+  greedy_own_best(bm, bx, by);
   const Rect Q = footprint(fx, fy, fs / 2, d.size);
   // C4 (aigar_tile_policy): the tile taking this bot's move must hold every pellet of its view
   if (d.tiled && !tile_holds_rect(d, rect_grow(Q, 1, d.cols)) && lane == wave_leader()) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
-  double best = -1;
-  uint64_t bord = ~0ull;
-  double tx = 0, ty = 0;
+  GreedyAcc acc;
   wave_fov_walk(d, a, Q, fx, fy, fs, ctl.rmax_cell, ctl.rmax_virus, true, d.virus_enabled, [] {},
                 [&](bool valid, int kd, size_t g) {
     if (!valid) return;
@@ -1013,56 +1106,9 @@ __global__ void __launch_bounds__(64) k_policy_greedy(Dev d, int greedy_split, c
     if ((fl & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
     if (kd == 1 && (int)(g % NP) == gp) return;
     if (!in_fov(x, y, r, fx, fy, fs)) return;  // (implies the hash query's footprint test: aigar_sem.h)
-    if (kd != 0 && !(bm > 1.25 * m)) return;  // the biggest own cell must be able to eat it
-    const double sd = (x - bx) * (x - bx) + (y - by) * (y - by);
-    const double k = m / (sd != 0 ? sd : 1);
-    const uint64_t ord = ((uint64_t)kd << 56) | (uint64_t)S[gr];
-    if (k > best || (k == best && ord < bord)) {
-      best = k;
-      bord = ord;
-      tx = x;
-      ty = y;
-    }
+    acc.consider(kd, x, y, m, S[gr], bm, bx, by);
   });
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double ok = __shfl_xor(best, off);
-    uint64_t oo = __shfl_xor(bord, off);
-    double ox = __shfl_xor(tx, off), oy = __shfl_xor(ty, off);
-    if (ok > best || (ok == best && oo < bord)) {
-      best = ok;
-      bord = oo;
-      tx = ox;
-      ty = oy;
-    }
-  }
-  if (lane != 0) return;
-  uint64_t u[4];
-  philox((uint64_t)p, ST_GREEDY, (uint64_t)ctl.tick, 0, ctl.key0, ctl.key1, u);
-  double a0, a1;
-  if (bord != ~0ull) {  // getRelativeCellPos(bestCell, left, top, size)
-    a0 = py_round5((tx - (double)left) / fs);
-    a1 = py_round5((ty - (double)top) / fs);
-  } else {
-    a0 = u01(u[0]);
-    a1 = u01(u[1]);
-  }
-  int split = 0, eject = 0;
-  if (greedy_split) {  // ENABLE_GREEDY_SPLIT: randint(0, 10000) > splitLikelihood
-    int lh = d.p_split_lh[gp];
-    if (lh <= 0) {
-      uint64_t v[4];
-      philox((uint64_t)p, ST_GREEDY_LH, 0, 0, ctl.key0, ctl.key1, v);
-      lh = (int)ph_randint(v[0], 9950, 10000);
-    }
-    split = ph_randint(u[2], 0, 10000) > lh;
-    eject = ph_randint(u[3], 0, 10000) > 100000;  // ejectLikelihood (bot.py:94)
-  }
-  const int64_t isz = (int64_t)fs;  // set_command_point: left + action * int(size)
-  d.p_cmdx[gp] = (double)left + a0 * (double)isz;
-  d.p_cmdy[gp] = (double)top + a1 * (double)isz;
-  d.p_split[gp] = split;
-  d.p_eject[gp] = eject;
+  greedy_commit(d, gp, acc, fx, fy, fs, greedy_split);
 }
 void launch_policy_greedy(const Dev &d, hipStream_t s, int greedy_split, const uint8_t *mask, int want) {
   hipLaunchKernelGGL(k_policy_greedy, dim3(d.NP), dim3(64), 0, s, d, greedy_split, mask, want);
@@ -1233,7 +1279,27 @@ constexpr int kObsWtBots = 16384;  // k_observe's store policy switch (bots per 
 // the state representation the configuration asks for (bot.py:272-299): the
 // default grid (<= 16 squares per side), the wide grid (CNN grid view), or the
 // simple representation (GRID_VIEW_ENABLED = False)
-void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch, const uint8_t *mask) {
+// whether the observation can also pick the next tick's Greedy moves (k_observe's
+// GREEDY mode: the grid observation with its pellet channel, which walks every
+// candidate the Greedy policy reads)
+bool observe_fuses_greedy(const Dev &d) {
+  return !(d.obs_ch & AIGAR_OBS_SIMPLE) && d.G <= 16 && (d.obs_ch & AIGAR_OBS_PELLET) && !d.tiled;
+}
+// greedy_next >= 0 (observe_fuses_greedy): also the next tick's Greedy moves, with greedy_split = greedy_next
+void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t epoch, const uint8_t *mask,
+                    int greedy_next) {
+  if (greedy_next >= 0 && observe_fuses_greedy(d) && !mask) {
+    const bool wt = d.NP <= kObsWtBots;
+    if (dtype == 0) {
+      if (wt) hipLaunchKernelGGL((k_observe<double, true, true>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask, greedy_next);
+      else hipLaunchKernelGGL((k_observe<double, false, true>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask, greedy_next);
+    } else {
+      if (wt) hipLaunchKernelGGL((k_observe<float, true, true>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask, greedy_next);
+      else hipLaunchKernelGGL((k_observe<float, false, true>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask, greedy_next);
+    }
+    return;
+  }
+  if (greedy_next >= 0) launch_policy_greedy(d, s, greedy_next, nullptr, -1);  // (cannot fuse: its own launch, first)
   if (d.obs_ch & AIGAR_OBS_SIMPLE) {
     if (dtype == 0) hipLaunchKernelGGL(k_observe_simple<double>, dim3(d.NP), dim3(64), 0, s, d, (double *)out, mask);
     else hipLaunchKernelGGL(k_observe_simple<float>, dim3(d.NP), dim3(64), 0, s, d, (float *)out, mask);
@@ -1245,11 +1311,11 @@ void launch_observe(const Dev &d, hipStream_t s, void *out, int dtype, uint32_t 
     // launch), non-temporal beyond (a streaming one); see k_observe
     const bool wt = d.NP <= kObsWtBots;
     if (dtype == 0) {
-      if (wt) hipLaunchKernelGGL((k_observe<double, true>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
-      else hipLaunchKernelGGL((k_observe<double, false>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask);
+      if (wt) hipLaunchKernelGGL((k_observe<double, true, false>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask, 0);
+      else hipLaunchKernelGGL((k_observe<double, false, false>), dim3(d.NP), dim3(64), 0, s, d, (double *)out, epoch, mask, 0);
     } else {
-      if (wt) hipLaunchKernelGGL((k_observe<float, true>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
-      else hipLaunchKernelGGL((k_observe<float, false>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask);
+      if (wt) hipLaunchKernelGGL((k_observe<float, true, false>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask, 0);
+      else hipLaunchKernelGGL((k_observe<float, false, false>), dim3(d.NP), dim3(64), 0, s, d, (float *)out, epoch, mask, 0);
     }
   }
 }
