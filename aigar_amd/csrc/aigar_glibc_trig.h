@@ -158,6 +158,75 @@ AIGAR_HD double cos_glibc(double x) {
   return x - x;
 }
 
+// sin and cos of one angle, shaped for a wavefront: the same operations as
+// sin_glibc / cos_glibc, but every lane runs ONE do_sin and ONE do_cos whose
+// inputs the range selects (|x| < 0.855469: (x, 0) both; < 2.426265: the
+// hp0 - |x| forms; else reduce_sincos's (a, da) and the quadrant picks which
+// core is which), the Taylor / table choice of do_sin a select, and both
+// sincostab rows loaded in one round.  Branching per lane -- the stepper's
+// angles span every range in one wave -- serialised the paths and their table
+// loads (measured: 44.6 -> 31.8 M env-steps/s at C3).  Results are identical
+// (tools/gen/check_glibc_trig.cpp checks both shapes against libm).
+namespace gsin {
+AIGAR_HD int row_of(double u) { const uint32_t k = lo32(u); return (int)(k < 109u ? k : 109u) << 2; }  // (109: the last row; NaN / inf lanes)
+}  // namespace gsin
+AIGAR_HD void sincos_glibc(double x, double &sv, double &cv) {
+  using namespace gsin;
+  const uint32_t k = hi32(x) & 0x7fffffffu;
+  const double ax = fabs(x);
+  const double y = hp0 - ax, am = y + hp1, dam = (y - am) + hp1;  // (2.426265 range)
+  double ar, dar;
+  const int n = reduce(x, ar, dar);  // (105414350 range)
+  const bool r1 = k < 0x3feb6000u, r2 = !r1 && k < 0x400368fdu;
+  const double XS = r1 ? x : (r2 ? am : ar), DXS0 = r1 ? 0.0 : (r2 ? dam : dar);
+  const double XC = r1 ? x : (r2 ? y : ar), DXC0 = r1 ? 0.0 : (r2 ? hp1 : dar);
+  // the two table rows (one load round)
+  const double uS = big + fabs(XS), uC = big + fabs(XC);
+  const int kS = row_of(uS), kC = row_of(uC);
+  const double snS = gsct(kS), ssnS = gsct(kS + 1), csS = gsct(kS + 2), ccsS = gsct(kS + 3);
+  const double snC = gsct(kC), ssnC = gsct(kC + 1), csC = gsct(kC + 2), ccsC = gsct(kC + 3);
+  // do_sin (XS, DXS0): TAYLOR_SIN below 0.126, else the table form
+  double S;
+  {
+    const double xx = XS * XS;
+    const double p = fma(fma(fma(fma(s5, xx, s4), xx, s3), xx, s2), xx, s1);
+    const double St = XS + fma(xx, fma(p, XS, -(0.5 * DXS0)), DXS0);
+    const double dx = XS <= 0 ? -DXS0 : DXS0;
+    const double xr = fabs(XS) - (uS - big), x2 = xr * xr;
+    const double ss = xr + fma(xr * x2, fma(x2, sn5, sn3), dx);
+    const double cc = fma(xr, dx, x2 * fma(fma(x2, cs6, cs4), x2, cs2));
+    const double cor = fma(ss, csS, fma(-cc, snS, fma(ss, ccsS, ssnS)));
+    S = fabs(XS) < t126 ? St : copysign(snS + cor, XS);
+  }
+  // do_cos (XC, DXC0)
+  double C;
+  {
+    const double dx = XC < 0 ? -DXC0 : DXC0;
+    const double xr = (fabs(XC) - (uC - big)) + dx, x2 = xr * xr;
+    const double ss = fma(xr * x2, fma(x2, sn5, sn3), xr);
+    const double cc = x2 * fma(fma(x2, cs6, cs4), x2, cs2);
+    const double cor = fma(-ss, snC, fma(-cc, csC, fma(-ss, ssnC, ccsC)));
+    C = csC + cor;
+  }
+  if (r1) {
+    sv = S;
+    cv = C;
+  } else if (r2) {
+    sv = copysign(C, x);
+    cv = S;
+  } else {  // do_sincos (a, da, n) and (a, da, n + 1)
+    const double s0 = (n & 1) ? C : S, c0 = (n & 1) ? S : C;
+    sv = (n & 2) ? -s0 : s0;
+    cv = ((n + 1) & 2) ? -c0 : c0;
+  }
+  if (k < 0x3e500000u) sv = x;    // |x| < 2^-26
+  if (k < 0x3e400000u) cv = 1.0;  // |x| < 2^-27
+  if (k >= 0x419921fbu) {         // (__branred range: not on the path) and inf / nan
+    sv = k < 0x7ff00000u ? sin_cr(x) : x - x;
+    cv = k < 0x7ff00000u ? cos_cr(x) : x - x;
+  }
+}
+
 namespace gatan {
 constexpr double hpi = 0x1.921fb54442d18p+0, hpi1 = 0x1.1a62633145c07p-54;
 constexpr double opi = 0x1.921fb54442d18p+1, opi1 = 0x1.1a62633145c07p-53;
@@ -298,6 +367,70 @@ AIGAR_HD double atan2_glibc(double y, double x) {
   return copysign(z, y);  // signArctan2
 }
 
+// atan2 shaped for a wavefront, as sincos_glibc: the four quadrant cases share
+// their forms (ii)-(iv) are K + s u with K = pi/2 or pi and s = +-1, whose
+// ESUB / EADD corrections take their first branch since |u| < 1/16 < K), the
+// Taylor and table forms are both evaluated and selected, and the cij row is
+// loaded in one round; the special operands replace the result at the end, in
+// e_atan2.c's order.  Identical results to atan2_glibc.
+AIGAR_HD double atan2_glibc_flat(double y, double x) {
+  using namespace gatan;
+  const uint64_t bx = as_u64(x), by = as_u64(y);
+  const uint32_t ux = (uint32_t)(bx >> 32), dx = (uint32_t)bx, uy = (uint32_t)(by >> 32), dy = (uint32_t)by;
+  const double ax0 = x < 0 ? -x : x, ay0 = y < 0 ? -y : y;
+  const int de = (int)(uy & 0x7ff00000u) - (int)(ux & 0x7ff00000u);
+  // the regular path
+  const bool sml = ax0 < twom500 || ay0 < twom500;
+  double ax = ax0 * (sml ? two500 : 1.0), ay = ay0 * (sml ? two500 : 1.0);
+  const bool lrg = ax > two500 || ay > two500;
+  ax *= lrg ? twom500 : 1.0;
+  ay *= lrg ? twom500 : 1.0;
+  const bool yx = ay < ax, xpos = x > 0, c1 = xpos && yx, c3 = !xpos && ax < ay;
+  const double num = yx ? ay : ax, den = yx ? ax : ay;
+  const double u = num / den;
+  const double v0 = den * u, vv = fma(den, u, -v0);  // EMULV
+  const double du = ((num - v0) - vv) / den;
+  const bool c4 = !xpos && !c3;
+  const double K = c4 ? opi : hpi, K1 = c4 ? opi1 : hpi1, sg = c3 ? 1.0 : -1.0;
+  // the cij row (its load first)
+  double ri = fma(u, two8, two52) - two52;
+  ri = (ri >= 16.0 && ri <= 256.0) ? ri : 16.0;  // (u < 1/16, nan: a row that is not used)
+  const int i = (int)ri - 16;
+  const double cj0 = gcij(i, 0), cj1 = gcij(i, 1), cj2 = gcij(i, 2), cj3 = gcij(i, 3), cj4 = gcij(i, 4),
+               cj5 = gcij(i, 5), cj6 = gcij(i, 6);
+  // Taylor, u < 1/16
+  const double v = u * u, pd = poly_d(v);
+  const double zTi = u + fma(u * v, pd, du);
+  const double zz = (u * v) * pd;
+  const double t2 = K + sg * u;
+  const double cor = (K - t2) + sg * u;
+  const double zTr = (((cor + K1) + sg * du) + sg * zz) + t2;
+  // table
+  const double t3 = u - cj0, vi = t3 + du;
+  const double dvi = fabs(t3) > fabs(du) ? (t3 - vi) + du : (du - vi) + t3;
+  const double p4 = fma(vi, fma(vi, fma(vi, cj6, cj5), cj4), cj3);
+  const double zBi = fma(vi, cj2, fma(dvi, cj2, (vi * vi) * p4)) + cj1;
+  const double pc = fma(vi, fma(vi, fma(vi, fma(vi, cj6, cj5), cj4), cj3), cj2);
+  const double zBr = (K + sg * cj1) + fma(sg * vi, pc, K1);
+  const double z = u < inv16 ? (c1 ? zTi : zTr) : (c1 ? zBi : zBr);
+  double res = copysign(z, y);
+  // e_atan2.c's special operands, last-checked first
+  if (de <= em) res = x > 0 ? copysign(ay0 / ax0, y) : (y > 0 ? opi : -opi);
+  if (de >= ep) res = y > 0 ? hpi : -hpi;
+  if (uy == 0xfff00000u && dy == 0) res = -hpi;
+  if (uy == 0x7ff00000u && dy == 0) res = hpi;
+  if (ux == 0xfff00000u && dx == 0)
+    res = (uy == 0x7ff00000u && dy == 0) ? tqpi : (uy == 0xfff00000u && dy == 0) ? -tqpi : ((uy & 0x80000000u) == 0 ? opi : -opi);
+  if (ux == 0x7ff00000u && dx == 0)
+    res = (uy == 0x7ff00000u && dy == 0) ? qpi : (uy == 0xfff00000u && dy == 0) ? -qpi : ((uy & 0x80000000u) == 0 ? 0.0 : -0.0);
+  if (x == 0) res = (uy & 0x80000000u) == 0 ? hpi : -hpi;
+  if (uy == 0x80000000u && dy == 0) res = (ux & 0x80000000u) == 0 ? -0.0 : -opi;
+  if (uy == 0x00000000u && dy == 0) res = (ux & 0x80000000u) == 0 ? 0.0 : opi;
+  if ((uy & 0x7ff00000u) == 0x7ff00000u && (((uy & 0x000fffffu) | dy) != 0)) res = y + y;
+  if ((ux & 0x7ff00000u) == 0x7ff00000u && (((ux & 0x000fffffu) | dx) != 0)) res = x + y;
+  return res;
+}
+
 // the stepper's trig entry points: glibc's functions (AIGAR_CR_TRIG: the
 // correctly rounded aigar_trig.h versions, AIGAR_LIBM_TRIG: OCML -- A/B builds only)
 AIGAR_HD double trig_atan2(double y, double x) {
@@ -306,7 +439,7 @@ AIGAR_HD double trig_atan2(double y, double x) {
 #elif defined(AIGAR_CR_TRIG)
   return atan2_cr(y, x);
 #else
-  return atan2_glibc(y, x);
+  return atan2_glibc_flat(y, x);
 #endif
 }
 AIGAR_HD void trig_sincos(double a, double &s, double &c) {
@@ -316,8 +449,7 @@ AIGAR_HD void trig_sincos(double a, double &s, double &c) {
 #elif defined(AIGAR_CR_TRIG)
   sincos_cr(a, s, c);
 #else
-  s = sin_glibc(a);
-  c = cos_glibc(a);
+  sincos_glibc(a, s, c);
 #endif
 }
 

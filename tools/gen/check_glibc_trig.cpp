@@ -34,7 +34,12 @@ static long bad = 0, total = 0;
 
 static void check_sc(double a) {
   const double s = sin_glibc(a), c = cos_glibc(a);
+  double fs, fc;
+  sincos_glibc(a, fs, fc);  // (the wavefront-shaped form the device runs)
   total++;
+  if (!same(s, fs) || !same(c, fc)) {
+    if (++bad < 12) printf("sincos_glibc(%a): %a %a vs sin/cos_glibc %a %a\n", a, fs, fc, s, c);
+  }
   if (!same(s, sin(a)) || !same(c, cos(a))) {
     if (++bad < 12) printf("sin/cos(%a): %a %a vs libm %a %a\n", a, s, c, sin(a), cos(a));
   }
@@ -48,6 +53,9 @@ static void check_sc(double a) {
 static void check_at(double y, double x) {
   const double r = atan2_glibc(y, x);
   total++;
+  if (!same(r, atan2_glibc_flat(y, x))) {
+    if (++bad < 12) printf("atan2_glibc_flat(%a, %a): %a vs atan2_glibc %a\n", y, x, atan2_glibc_flat(y, x), r);
+  }
   if (!same(r, atan2(y, x))) {
     if (++bad < 12) printf("atan2(%a, %a): %a vs libm %a\n", y, x, r, atan2(y, x));
   }
