@@ -663,15 +663,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     pint = __ballot(bad) == 0;
   }
 #endif
-  // Otherwise (a blob conversion's 14.4 in view), when the grid is small: each
-  // square collects its pellets' list indices (at most kSqSlots; more: the scan
-  // below) and sums them in creation order itself -- a sort of <= 4 entries per
-  // square instead of ranking the list and scanning it per square (pord)
-  const bool pord_try = !pint && in_lds && GG <= 128 && G <= 16;
   // rank pellets by creation sequence (the sum order of the reference)
   const double *sm = nullptr;
   const uint32_t *smk = nullptr;
-  auto rank_pellets = [&]() {  // np <= OBS_PCAP = 4 x 64: keep (rank, m, mask) in registers, then store in order
+  if (in_lds && !pint) {  // np <= OBS_PCAP = 4 x 64: keep (rank, m, mask) in registers, then store in order
     int rk4[OBS_PCAP / 64];
     double m4[OBS_PCAP / 64];
     uint32_t k4[OBS_PCAP / 64];
@@ -697,9 +692,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       }
     sm = &p_sx[0].m;
     smk = &p_px[0].mask;
-  };
-  if (in_lds && !pint && !pord_try) {
-    rank_pellets();
   } else if (!in_lds) {
     for (int i = lane; i < np; i += 64) {
       int64_t sq = PL.seq[i];
@@ -789,69 +781,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     }
     wave_fence();
   }
-  constexpr int kSqSlots = 4;
-  int *const s_sqn = &p_px[0].perm;                                // [128] pellets per square
-  uint8_t *const s_sqe = reinterpret_cast<uint8_t *>(&p_px[128]);  // [128][kSqSlots] their list indices
-  bool pord = false;
-  if (pord_try) {
-    for (int t = lane; t < 128; t += 64) s_sqn[t] = 0;
-    wave_fence();
-    for (int i = lane; i < np; i += 64) {  // (the same squares as the whole-unit scatter)
-      const uint32_t mk = p_mask[i];
-      for (uint32_t X = mk & 0xFFFFu; X; X &= X - 1) {
-        const int ix = __ffs(X) - 1;
-        if (ix >= cols) break;
-        for (uint32_t Y = mk >> 16; Y; Y &= Y - 1) {
-          const int t = (__ffs(Y) - 1) * cols + ix;
-          if (t >= GG) break;
-          const int c = sdiv(t, Mg), r = t - c * G;
-          if ((in_col >> r) & (in_row >> c) & 1) {
-            const int k = atomicAdd(&s_sqn[t], 1);
-            if (k < kSqSlots) s_sqe[t * kSqSlots + k] = (uint8_t)i;
-          }
-        }
-      }
-    }
-    wave_fence();
-    bool over = false;
-    for (int t = lane; t < GG; t += 64) over |= s_sqn[t] > kSqSlots;
-    pord = __ballot(over) == 0;
-    if (!pord) {  // (a crowded square: the creation-order ranking and the scan)
-      rank_pellets();
-      wave_fence();
-    }
-  }
-  // square t's pellet sum in creation order (pord): its <= kSqSlots entries sorted by sequence
-  auto ord_sum = [&](int t) -> double {
-    const int n = s_sqn[t];
-    if (n == 0) return 0.0;
-    int e[kSqSlots];
-    int64_t q[kSqSlots];
-#pragma unroll
-    for (int k = 0; k < kSqSlots; k++) {
-      e[k] = k < n ? (int)s_sqe[t * kSqSlots + k] : 0;
-      q[k] = k < n ? p_sx[e[k]].seq : INT64_MAX;
-    }
-    auto cs = [&](int a, int b) {  // compare-exchange (a sorting network of 4)
-      const bool sw = q[b] < q[a];
-      const int64_t qa = q[a];
-      const int ea = e[a];
-      q[a] = sw ? q[b] : q[a];
-      e[a] = sw ? e[b] : e[a];
-      q[b] = sw ? qa : q[b];
-      e[b] = sw ? ea : e[b];
-    };
-    cs(0, 1);
-    cs(2, 3);
-    cs(0, 2);
-    cs(1, 3);
-    cs(1, 2);
-    double sum = 0;
-#pragma unroll
-    for (int k = 0; k < kSqSlots; k++)
-      if (k < n) sum = sum + p_m[e[k]];
-    return sum;
-  };
   // instantiated twice: with the LDS lists themselves (ds_read, no wait on the
   // row stores in flight) and with generic pointers (a list in the overflow pool)
   // The per-square scans read list entry k through accessors: PEL(k) -> (mass,
@@ -892,8 +821,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     } else if (within && ix < 16) {
       if (pint) {
         vp = (double)s_pcnt[t];
-      } else if (pord) {
-        vp = ord_sum(t);
       } else {
         double s = 0;
         bool anyp = false;
@@ -996,10 +923,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   }
   };
   const bool all_lds = in_lds && CL.mask == c_mask && VL.mask == v_mask;
-  if (all_lds && (pint || pord || np <= 64) && nc <= 64 && nv <= 64 && GG <= 128) {
+  if (all_lds && (pint || np <= 64) && nc <= 64 && nv <= 64 && GG <= 128) {
     // common case: entry k of every list sits in lane k's registers and is read
     // with v_readlane into scalar registers (no LDS round trip per entry)
-    const bool rp = !pint && !pord && lane < np;
+    const bool rp = !pint && lane < np;
     const double rpm = rp ? sm[lane] : 0.0, rcm = lane < nc ? c_mass[lane] : 0.0;
     const uint32_t rpk = rp ? smk[lane] : 0u, rck = lane < nc ? c_mask[lane] : 0u;
     const int rco = lane < nc ? c_own[lane] : 0;
@@ -1023,9 +950,6 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       if (pint) {  // (GG <= 128 here; the counts of squares outside the field or past ix 15 stayed 0)
         vp0 = (double)s_pcnt[lane];
         vp1 = lane + 64 < GG ? (double)s_pcnt[lane + 64] : 0.0;
-      } else if (pord) {  // (likewise: such squares collected no entry)
-        vp0 = ord_sum(lane);
-        vp1 = lane + 64 < GG ? ord_sum(lane + 64) : 0.0;
       } else {
         double s0 = 0, s1 = 0;
         bool a0 = false, a1 = false;
