@@ -15,7 +15,7 @@ import csv, sys, collections
 v = collections.defaultdict(lambda: collections.defaultdict(float))
 n = collections.Counter()
 for r in csv.DictReader(open(sys.argv[1])):
-    if "k_observe<double, true>" not in r["Kernel_Name"]:
+    if "k_observe<double, true" not in r["Kernel_Name"]:
         continue
     v[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
 tot = collections.defaultdict(float)
