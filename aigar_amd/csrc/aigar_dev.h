@@ -179,11 +179,6 @@ struct Dev {
   int virus_enabled;
   double max_pellets, max_viruses;
   int G, L;
-  // the observation's per-handle constants (k_observe computed them per wave: two
-  // integer and three fp64 divisions of VALU work): 1 / NP, 1 / G, and for the
-  // grid's cols = G or G + 1 (the cols == 12 quirk) 1 / cols and ceil(2^16 / n)
-  double inv_np, inv_G, inv_cols[2];
-  int Mg, Mc[2];
   uint32_t obs_ch, obs_ex;
   int flags;
   int pp_par;  // playerPlayerOverlap may run as independent groups (pp_pass; AIGAR_PP_SERIAL=1: never)

@@ -336,13 +336,6 @@ extern "C" int aigar_create(const aigar_config *cfg, aigar_handle **out) {
   d.EVcap = cfg->event_cap > 0 ? cfg->event_cap : 65536;
   d.G = G;
   d.L = obs_len_of(*cfg);
-  d.inv_np = 1.0 / d.NP;
-  d.inv_G = 1.0 / G;
-  for (int k = 0; k < 2; k++) {
-    d.inv_cols[k] = 1.0 / (G + k);
-    d.Mc[k] = (65536 + (G + k) - 1) / (G + k);
-  }
-  d.Mg = (65536 + G - 1) / G;
   d.obs_ch = cfg->obs_channels;
   d.obs_ex = cfg->obs_extras;
   d.flags = cfg->flags;

@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const bool held = tile_holds_rect(d, rect_grow(Q, 1, d.cols));
   if (!held && lane == wave_leader()) atomicOr(&d.ctl[a].err, ERR_TILE_OBS);
   // owner of cell pool index g = slot * NP + player, without a 64-bit modulo
-  const double inv_np = d.inv_np;
+  const double inv_np = 1.0 / NP;
   auto pool_owner = [&](size_t g) {
     const int gi = (int)g;
     int o = gi - (int)((double)gi * inv_np) * NP;
@@ -745,8 +745,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   const double hrow = py_max(py_min(rowy + gs / 2, fieldSize), 0.0) - py_min(py_max(rowy - gs / 2, 0.0), fieldSize);
   const unsigned long long in_col = __ballot(!(colx + gs / 2 < 0 || colx - gs / 2 > fieldSize));
   const unsigned long long in_row = __ballot(!(rowy + gs / 2 < 0 || rowy - gs / 2 > fieldSize));
-  // (cols = ceil(fs / (fs / G)) is G or G + 1: the quotient is within an ulp of G)
-  const double inv_G = d.inv_G, inv_cols = d.inv_cols[cols == G ? 0 : 1];
+  const double inv_G = 1.0 / G, inv_cols = 1.0 / cols;
   // t / n for 0 <= t, n < 2^20: double reciprocal, then one correction step
   auto idiv = [](int t, int n, double inv_n) {
     int q = (int)((double)t * inv_n);
@@ -757,7 +756,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // t / n for 0 <= t < 512, 1 <= n <= 128: (t * ceil(2^16 / n)) >> 16 is exact
   // (checked for every such pair) -- a 24-bit multiply and a shift
   const bool small = GG <= 512 && G <= 127;  // (wave-uniform; cols <= G + 1)
-  const int Mg = d.Mg, Mc = d.Mc[cols == G ? 0 : 1];
+  const int Mg = (65536 + G - 1) / G, Mc = (65536 + cols - 1) / cols;
   auto sdiv = [](int t, int M) { return (int)(((unsigned)t * (unsigned)M) >> 16); };
   // the whole-unit pellets' sums (pint): square t = iy * cols + ix of every
   // (column bit ix, row bit iy) of a pellet's mask -- the squares whose `need`
