@@ -4276,6 +4276,45 @@ __device__ __forceinline__ int block_excl1(int v, int *wsum, int &total) {
   __syncthreads();
   return before + inc - v;
 }
+// two exclusive block scans in one pass (one barrier): a, one value per thread
+// in thread order, and p[0..3], four per thread (thread t holds items 4t .. 4t+3);
+// tp = p's total.  wsum: 8 entries.
+__device__ __forceinline__ void block_scan_pair(int &a, int64_t *p, int64_t *wsum, int64_t &tp) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int sa = a;
+  const int64_t sp = p[0] + p[1] + p[2] + p[3];
+  int ia = sa;
+  int64_t ip = sp;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int ya = __shfl_up(ia, off);
+    const int64_t yp = __shfl_up(ip, off);
+    if (lane >= off) {
+      ia += ya;
+      ip += yp;
+    }
+  }
+  if (lane == 63) {
+    wsum[w] = ia;
+    wsum[4 + w] = ip;
+  }
+  __syncthreads();
+  int64_t ba = 0, bp = 0;
+  tp = 0;
+  for (int k = 0; k < nw; k++) {
+    ba += k < w ? wsum[k] : 0;
+    bp += k < w ? wsum[4 + k] : 0;
+    tp += wsum[4 + k];
+  }
+  a = (int)ba + ia - sa;
+  int64_t run = bp + ip - sp;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int64_t x = p[k];
+    p[k] = run;
+    run += x;
+  }
+}
 constexpr int PU_JREC = 64;  // joining records per row kept whole in LDS (beyond: loaded again)
 constexpr int PU_LDS = 512;  // row slots whose records the update parks in LDS (longer rows: two rounds)
 constexpr int PU_K = PU_LDS / 256;  // consecutive slots per thread
@@ -4287,11 +4326,12 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
   __shared__ int s_jcol[PU_JREC];
   __shared__ PelRec s_rec[PU_LDS];
   __shared__ int s_rcol[PU_LDS];
-  __shared__ uint8_t s_rdead[PU_LDS];
   __shared__ int s_ost[kPelRowCols + 1];  // the row's old bucket starts (absolute slots)
   __shared__ int s_live[kPelRowCols], s_stc[kPelRowCols];  // per bucket: survivors, joining records
   __shared__ int s_lpre[kPelRowCols], s_nofs[kPelRowCols];  // survivors before the bucket; its new start - row base
   __shared__ int wsum[4];
+  __shared__ int64_t wsum2[8];
+  __shared__ short s_slotb[PU_LDS];  // a parked suffix slot's old bucket
   const int tid = threadIdx.x, C = d.cols;
   ArenaCtl &c = d.ctl[a];
   const int nconv = c.pu_nconv, nst = nconv + c.pu_nsp, spec = c.pu_spec;
@@ -4395,9 +4435,6 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
   // written; else the whole row into its other home
   const bool inplace = hi - f <= PU_LDS;
   const int home = C * d.PR, nb = inplace ? lo : lo >= home ? lo - home : lo + home;
-  for (int bx = tid; bx < C; bx += blockDim.x)
-    s_live[bx] = inplace ? max(0, min(s_ost[bx + 1], f) - s_ost[bx]) : 0;  // (slots before f: all live)
-  __syncthreads();
   auto bucket_of = [&](int i) {  // old bucket of slot i: s_ost[bx] <= i < s_ost[bx + 1]
     int l = 0, h = C;  // invariant: s_ost[l] <= i < s_ost[h]
     while (h - l > 1) {
@@ -4432,36 +4469,64 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
   };
   int total;
   if (inplace) {
-    // round 2: the suffix's liveness, records and colours in ONE round of loads,
-    // parked in LDS until their new positions are known (registers: the launch
-    // spilled) -- and before any of the suffix is overwritten
-    for (int i = f + tid; i < hi; i += blockDim.x) {
-      const bool dead = d.pel_dead[D0 + i];
-      s_rec[i - f] = d.pel[S0 + i];
-      s_rcol[i - f] = d.pel_col[S0 + i];
-      s_rdead[i - f] = dead ? 1 : 0;
-    }
-    __syncthreads();
-    // each thread's PU_K consecutive suffix slots: bucket, survivor count
+    // round 2: thread t's PU_K consecutive suffix slots -- liveness, records,
+    // colours in ONE round of loads, parked in LDS (the suffix is rewritten in
+    // place: every record is read before any is written)
     const int i0 = f + PU_K * tid;
     uint32_t livem = 0;
-    int b0 = i0 < hi ? bucket_of(i0) : 0, bk[PU_K];
 #pragma unroll
     for (int k = 0; k < PU_K; k++) {
       const int i = i0 + k;
-      if (i >= hi) continue;
-      while (s_ost[b0 + 1] <= i) b0++;  // (consecutive slots: the next bucket is near)
-      bk[k] = b0;
-      if (!s_rdead[i - f]) {
-        livem |= 1u << k;
-        atomicAdd(&s_live[b0], 1);
-      } else {
-        d.pel_dead[D0 + i] = 0;  // eaten: dropped, and its flag clean for whatever lands on the slot
+      if (i < hi) {
+        livem |= d.pel_dead[D0 + i] ? 0u : 1u << k;
+        s_rec[i - f] = d.pel[S0 + i];
+        s_rcol[i - f] = d.pel_col[S0 + i];
       }
     }
-    int tot;
-    int ex = (f - lo) + block_excl1(__popc(livem), wsum, tot);  // (its barriers complete the bucket counts)
-    total = bucket_scans();
+    // meanwhile, with LDS alone: every suffix slot's old bucket (scattered by
+    // bucket: buckets are a few slots long), the survivors before f
+    for (int bx = tid; bx < C; bx += blockDim.x) {
+      const int s0 = s_ost[bx], s1 = s_ost[bx + 1];
+      for (int i = max(s0, f); i < s1; i++) s_slotb[i - f] = (short)bx;
+      s_live[bx] = max(0, min(s1, f) - s0);
+    }
+    __syncthreads();
+    int bk[PU_K];
+#pragma unroll
+    for (int k = 0; k < PU_K; k++) {
+      const int i = i0 + k;
+      bk[k] = 0;
+      if (i >= hi) continue;
+      bk[k] = s_slotb[i - f];
+      if ((livem >> k) & 1) atomicAdd(&s_live[bk[k]], 1);
+      else d.pel_dead[D0 + i] = 0;  // eaten: dropped, and its flag clean for whatever lands on the slot
+    }
+    __syncthreads();
+    // ONE pass of scans: the survivors' order over the suffix, the new bucket starts
+    int pk[4];
+    int64_t pb[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int bx = tid * 4 + k;
+      pk[k] = bx < C ? s_live[bx] : 0;
+      pb[k] = bx < C ? ((int64_t)s_stc[bx] << 32) | (uint32_t)pk[k] : 0;
+    }
+    int ex = __popc(livem);
+    int64_t tb;
+    block_scan_pair(ex, pb, wsum2, tb);
+    ex += f - lo;
+    total = (int)(tb >> 32) + (int)(uint32_t)tb;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int bx = tid * 4 + k;
+      if (bx < C) {
+        const int lp = (int)(uint32_t)pb[k];
+        s_nofs[bx] = lp + (int)(pb[k] >> 32);
+        s_lpre[bx] = lp;
+      }
+    }
+    if (total > d.PR && tid == 0) set_err(d, a, ERR_PELLET_CAP);
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < PU_K; k++)
       if ((livem >> k) & 1) {
@@ -4473,6 +4538,8 @@ __device__ void pel_row_update(const Dev &d, int a, int r PT_PARAMS) {
         }
       }
   } else {  // (longer rows: the same in chunks of 256 slots, the records loaded after the count)
+    for (int bx = tid; bx < C; bx += blockDim.x) s_live[bx] = 0;
+    __syncthreads();
     for (int i = lo + tid; i < hi; i += blockDim.x)
       if (!d.pel_dead[D0 + i]) atomicAdd(&s_live[bucket_of(i)], 1);
     __syncthreads();

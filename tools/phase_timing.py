@@ -20,7 +20,7 @@ KERNELS = {0: ("k_food_prep", ["", "player", "cell", "pellet walk", "blob walk",
            3: ("k_pp_active", ["", "player", "cell", "grid test"]),
            4: ("k_food_commit", ["", "round 1", "round 2", "round 3", "round 4", "round 5", "round 6", "round 7+"]),
            5: ("k_spawn_plan", ["", "pp serial", "compaction", "virus grid", "spawn counts", "pellet close", "pp closures", "pp turns"]),
-           8: ("k_pel_update", ["", "first loads", "kill / join lists", "pellets + buckets", "fov cache", "virus spawns"])}
+           8: ("k_pel_update", ["", "first loads", "kill / join lists", "pellets + buckets", "fov cache", "virus spawns", "suffix loaded", "scans done"])}
 
 
 def build():
