@@ -77,6 +77,13 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
     if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[k][pt_w_][m] = (unsigned)(wall_clock64() - pt0_); \
   } while (0)
 #define PT_PARAMS , unsigned long long pt0_, int pt_w_
+// a mark in divergent code: recorded by the first active lane (the latest pass wins)
+#define PT_MARKW(k, m)                                                                              \
+  do {                                                                                              \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                     \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1 && pt_w_ < kPtWaves)         \
+      g_ptw[k][pt_w_][m] = (unsigned)(wall_clock64() - pt0_);                                       \
+  } while (0)
 // accumulating buckets for a serial loop (g_ptw[6][a][k]: wall-clock ticks, [7][a][k]: counts)
 #define PA_DECL                                   \
   unsigned long long pa_t_ = wall_clock64();      \
@@ -115,6 +122,7 @@ __device__ __forceinline__ void pt_ids(unsigned *o) {
 #define PT_SUB(k)
 #define PT_BEGIN(k)
 #define PT_MARK(k, m)
+#define PT_MARKW(k, m)
 #define PT_PARAMS
 #define PT_ARGS
 #define PA_DECL
@@ -2172,6 +2180,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
   auto prep_cell = [&](const int gpc, const int k, const size_t ci) {
     const int p = gpc - a * d.B;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
+    const size_t kc = (size_t)k * NP + gpc;  // (food counts and lists by list position: see food_commit_player)
     if (resume && d.f_done[ci] == 1) return;  // final (here or by its owner's message)
     double x = uni(d.c_x[ci]), y = uni(d.c_y[ci]), m = uni(d.c_m[ci]), r = uni(d.c_r[ci]);
     int64_t cseq = uni(d.c_seq[ci]);
@@ -2179,7 +2188,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
     Rect q = uni(footprint(x, y, r, d.size));
     if (d.tiled && !tile_near_rect(d, rect_grow(footprint(x, y, fmax(r, tile_rall()), d.size), 1, d.cols), 2)) {
       if (lane == 0) {  // cannot compete for any held food: its owner decides it
-        d.f_cnt[ci] = 0;
+        d.f_cnt[kc] = 0;
         d.f_done[ci] = 2;
       }
       return;
@@ -2255,7 +2264,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
       const uint64_t key = food_key(base + rounds + 2, prio);  // excluded: dominates overflow keys too
       const Rect qm = footprint(x, y, fmax(r, tile_rall()), d.size);
       if (lane == 0) {
-        d.f_cnt[ci] = kOverflow;
+        d.f_cnt[kc] = kOverflow;
         d.f_done[ci] = 2;
       }
       F.walk_pellets(q, [&](bool valid, int j) {
@@ -2288,7 +2297,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
     if (ovf) {  // reserve everything the cell may touch, resolved serially in priority order
       uint64_t key = food_key(base + rounds + 1, prio);
       if (lane == 0) {
-        d.f_cnt[ci] = kOverflow;
+        d.f_cnt[kc] = kOverflow;
         d.f_done[ci] = 0;
         int wi = atomicAdd(&d.ctl[a].n_pend, 1);  // straight to the serial pass
         if (wi < d.Wcap) {
@@ -2308,7 +2317,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
       });
       return;
     }
-    int *lst = d.f_list + ci * FCAP;
+    int *lst = d.f_list + kc * FCAP;
     uint64_t key = food_key(base + 1, prio);
     for (int i0 = 0; i0 < cnt; i0 += 64) {
       int i = i0 + lane;
@@ -2321,7 +2330,7 @@ __global__ void __launch_bounds__(256, 4) k_food_prep(Dev d, int rounds, int res
       }
     }
     if (lane == 0) {
-      d.f_cnt[ci] = (uint8_t)nsel;
+      d.f_cnt[kc] = (uint8_t)nsel;
       d.f_done[ci] = (nsel == 0);
     }
     wave_sync_lds();
@@ -2406,10 +2415,15 @@ struct FoodBatch {
   }
 };
 // returns the cell's radius if it ate, else 0
-__device__ double food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, uint32_t prio, const int *lst,
-                                int cnt, FoodBatch &fb) {
-  double x = d.c_x[ci], y = d.c_y[ci], m = d.c_m[ci], r = d.c_r[ci];
-  int64_t cseq = d.c_seq[ci];
+struct EaterIn {  // a committing cell's state, loaded with its reservation keys
+  double x, y, m, r;
+  int64_t seq;
+};
+__device__ double food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, const EaterIn &cell, uint32_t prio,
+                                const int *lst, int cnt, FoodBatch &fb) {
+  const double x = cell.x, y = cell.y;
+  double m = cell.m, r = cell.r;
+  const int64_t cseq = cell.seq;
   const bool own = tile_owns(d, x, y);
   int eaten = 0;
   bool blobs = false, ate = false;
@@ -2475,15 +2489,22 @@ __device__ double food_eat_loop(const Dev &d, const Food &F, int a, size_t ci, u
 }
 // one player's cells in reservation round `round`; returns the largest radius
 // of its cells that ate (0: none) -- the player-cell grid's radius bound
-__device__ double food_commit_player(const Dev &d, int gp, int round, int last, int place) {
+__device__ double food_commit_player(const Dev &d, int gp, int round, int last, int place PT_PARAMS) {
   const int NP = d.NP, a = gp / d.B, p = gp - a * d.B;
   ArenaCtl &c = d.ctl[a];
   // round r reads how many cells failed round r-1 (nothing left: skip), counts
-  // its own failures, and clears the counter round r+1 will use
-  // liveness, count and the list's first row with the round counter: one load round
+  // its own failures, and clears the counter round r+1 will use.
+  // ONE load round: liveness, cell count, the list's first row, and the first
+  // cell's food count and list -- k_food_prep keeps those by list position
+  // (k * NP + gp), so they need no slot first (FCAP slots exist; entries past
+  // the count are never used)
   const bool alive = d.p_alive[gp];
   const int n = d.p_ncells[gp];
   const int s_first = d.p_list[gp];
+  const int cnt_first = d.f_cnt[gp];
+  int l4_first[kTailRegs];
+#pragma unroll
+  for (int t = 0; t < kTailRegs; t++) l4_first[t] = d.f_list[(size_t)gp * FCAP + t];
   if (place && alive) cgrid_place_player(d, gp, n);  // (independent of the eats: its loads overlap theirs)
   if (round > 1 && c.food_undone[(round - 1) % 3] == 0) return 0;
   if (p == 0) c.food_undone[(round + 1) % 3] = 0;
@@ -2491,22 +2512,34 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last, 
   double rgrow = 0;
   Food F(d, a);
   for (int k = 0; k < n; k++) {
-    size_t ci = (size_t)(k == 0 ? s_first : d.p_list[k * NP + gp]) * NP + gp;
-    const int *lst = d.f_list + ci * FCAP;
-    // the food list's first entries ride the done / count loads (FCAP slots
-    // exist; entries past the count are never used)
-    int l4[kTailRegs];
+    const size_t kc = (size_t)k * NP + gp;
+    const int *lst = d.f_list + kc * FCAP;
+    int slot = s_first, cnt = cnt_first, l4[kTailRegs];
 #pragma unroll
-    for (int t = 0; t < kTailRegs; t++) l4[t] = lst[t];
-    const bool done = d.f_done[ci];
-    int cnt = d.f_cnt[ci];
-    if (done) continue;
+    for (int t = 0; t < kTailRegs; t++) l4[t] = l4_first[t];
+    if (k > 0) {  // (a further cell: its slot, count and list in one round)
+      slot = d.p_list[kc];
+      cnt = d.f_cnt[kc];
+#pragma unroll
+      for (int t = 0; t < kTailRegs; t++) l4[t] = lst[t];
+    }
+    PT_MARKW(4, 2);
+    if (cnt == 0 || cnt == kOverflow) continue;  // nothing to eat / already in the serial work list (k_food_prep)
+    const size_t ci = (size_t)slot * NP + gp;
     uint32_t prio = (uint32_t)p * kMaxCells + k;
-    if (cnt == kOverflow) continue;  // already in the serial work list (k_food_prep)
     bool own = true;
     FoodBatch fb;
-    {  // every reservation key of the list at once (one load round for the first
-       // entries) -- with the first entries' records, which the eats use if it won
+    EaterIn cell;
+    bool done;
+    {  // ONE round: the cell's done flag and state, every reservation key of the
+       // list (the first entries) and the first entries' records, which the eats
+       // use if it won
+      done = d.f_done[ci];
+      cell.x = d.c_x[ci];
+      cell.y = d.c_y[ci];
+      cell.m = d.c_m[ci];
+      cell.r = d.c_r[ci];
+      cell.seq = d.c_seq[ci];
       uint64_t key = food_key(d.ctl[a].food_round + round, prio);
       uint64_t kw[kTailRegs];
 #pragma unroll
@@ -2514,11 +2547,14 @@ __device__ double food_commit_player(const Dev &d, int gp, int round, int last, 
       fb.load(d, F, l4, cnt);
 #pragma unroll
       for (int t = 0; t < kTailRegs; t++) own &= kw[t] == key;
+      if (done) continue;  // (an earlier round's, or a tile's final cell)
       for (int t = kTailRegs; t < cnt && own; t++) own = (*F.owner(lst[t]) == key);
     }
+    PT_MARKW(4, 3);
     if (own) {
-      rgrow = fmax(rgrow, food_eat_loop(d, F, a, ci, prio, lst, cnt, fb));
+      rgrow = fmax(rgrow, food_eat_loop(d, F, a, ci, cell, prio, lst, cnt, fb));
       d.f_done[ci] = 1;
+      PT_MARKW(4, 4);
     } else if (!last) {
       // reserve for the next round right away.  Safe without a separate pass: a
       // cell that still has to wait for a lower-priority neighbour made its
@@ -2551,11 +2587,14 @@ __global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last,
   const int ncommit = (d.NP + 255) / 256;
   PT_BEGIN(4);
   const int gp = GTID;
-  const double rg = gp < d.NP ? food_commit_player(d, gp, round, last, place) : 0.0;
+  const double rg = gp < d.NP ? food_commit_player(d, gp, round, last, place PT_ARGS) : 0.0;
   PT_MARK(4, round < 7 ? round : 7);
   wave_atomic_max_pos(&d.ctl[min(gp, d.NP - 1) / d.B].rmax_cell, rg);
-  if (fold && last_block(d.ticket + 1, ncommit) && threadIdx.x < 64)
+  PT_MARK(4, 5);
+  if (fold && last_block(d.ticket + 1, ncommit) && threadIdx.x < 64) {
     for (int a = 0; a < d.A; a++) food_serial_body(d, a, scr_k, scr_v, rounds);
+    PT_MARK(4, 6);
+  }
 }
 // Cells the reservation rounds could not settle, in priority order (player,
 // list position), one wavefront per arena.  The sequential eat loop runs on

@@ -9,4 +9,4 @@ bash tools/abn.sh $T 3 ab/base.so || exit 1
 export AIGAR_PT_SO=$PWD/ab/pt.so
 timeout -k 10 150 python tools/phase_timing.py run 40 random > gpurun_out/${T}_pt_random.txt 2>&1 || exit 1
 timeout -k 10 150 python tools/phase_timing.py run 40 greedy > gpurun_out/${T}_pt_greedy.txt 2>&1 || exit 1
-grep k_pel_update gpurun_out/${T}_pt_random.txt gpurun_out/${T}_pt_greedy.txt | grep -v skew
+grep -E "k_pel_update|k_food_commit" gpurun_out/${T}_pt_random.txt gpurun_out/${T}_pt_greedy.txt | grep -v -E "skew|per CU"

@@ -18,7 +18,7 @@ KERNELS = {0: ("k_food_prep", ["", "player", "cell", "pellet walk", "blob walk",
            1: ("k_players", ["", "player loads", "tail loads", "tail done", "update_player", "look-back", "seq + blobs"]),
            2: ("k_players/x", ["", "head+policy+queue", "cell updates", "arena block", "blob block", "last-block grid"]),
            3: ("k_pp_active", ["", "player", "cell", "grid test"]),
-           4: ("k_food_commit", ["", "round 1", "round 2", "round 3", "round 4", "round 5", "round 6", "round 7+"]),
+           4: ("k_food_commit", ["", "round 1", "r2 | cell list", "r3 | keys+recs", "r4 | eat loop", "rmax atomic", "serial (fold)", "round 7+"]),
            5: ("k_spawn_plan", ["", "pp serial", "compaction", "virus grid", "spawn counts", "pellet close", "pp closures", "pp turns"]),
            8: ("k_pel_update", ["", "first loads", "kill / join lists", "pellets + buckets", "fov cache", "virus spawns", "suffix loaded", "scans done"])}
 
