@@ -164,6 +164,23 @@ __device__ bool last_block(int *ticket, int nblocks) {
   __syncthreads();
   return s_last;
 }
+// The same without the fences (each ~0.7 us on the kernel's tail, A/B r06):
+// for a last block that reads only words the other blocks stored or added with
+// agent-scope atomics (sc1), loading them with agent-scope atomic loads -- the
+// ticket's add comes after every storing wave's vmcnt(0), so the last block's
+// loads after its add returned see them (MI355X_MICROARCH.md, hand-off table)
+__device__ bool last_block_relaxed(int *ticket, int nblocks) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == nblocks - 1;
+    if (t == nblocks - 1) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last;
+}
 // The same for a wide grid: the tickets are sharded by blockIdx % 8 (tk[0..7]),
 // the last block of each shard takes a ticket of tk[8], so no counter sees more
 // than ~nblocks / 8 arrivals (one device-scope counter serialises them at
@@ -891,10 +908,12 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   // every block of the arena draws a ticket; the last one bumps the look-back
   // epoch and sets the blob count
   auto finish = [&]() __attribute__((always_inline)) {
-    if (last_block(&c.pl_ticket, (int)gridDim.x) && tid == 0) {
+    // (the last block reads only the two blob words, stored atomically below)
+    if (last_block_relaxed(&c.pl_ticket, (int)gridDim.x) && tid == 0) {
       __hip_atomic_fetch_add(&c.pl_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // the blob count moves only now: the blob blocks bound their slots by it
-      const int nb = c.n_blob_base + c.n_blob_add;
+      const int nb = __hip_atomic_load(&c.n_blob_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                     __hip_atomic_load(&c.n_blob_add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (nb > d.Ecap) set_err(d, a, ERR_BLOB_CAP);
       c.n_blob = min(nb, d.Ecap);
     }
@@ -1091,8 +1110,8 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
     const int tot = s_ps + s_ts, totb = s_pb + s_tb;
     c.seq_base_upd = seq0;
     c.seq_next = seq0 + tot;
-    c.n_blob_base = blob0;
-    c.n_blob_add = totb;  // (n_blob moves in the last block)
+    __hip_atomic_store(&c.n_blob_base, blob0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&c.n_blob_add, totb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (n_blob moves in the last block)
   }
   // the seq pass: a register-tail player's flags are final already and its list
   // is in flst (fn cells): only its new cells (the last nn) are numbered here
