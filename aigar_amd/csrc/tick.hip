@@ -146,7 +146,9 @@ __device__ __forceinline__ void grid_small_build(const Dev &d, int a, int *cnt, 
 // draws the last one returns true in all its threads and, after its acquire,
 // sees every participant's writes.  The last block resets the counter, so it is
 // 0 between launches (dalloc zeroes it).  Correct for any block placement.
-__device__ bool last_block(int *ticket, int nblocks) {
+// (acquire false: the caller acquires itself, and only when it reads other
+// blocks' plain stores -- agent_acquire_block below)
+__device__ bool last_block(int *ticket, int nblocks, bool acquire = true) {
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -157,12 +159,28 @@ __device__ bool last_block(int *ticket, int nblocks) {
     s_last = t == nblocks - 1;
     if (t == nblocks - 1) {
       __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (acquire) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
   }
   __syncthreads();
   return s_last;
+}
+// the last block's deferred acquire (every thread of the block calls it; `need`
+// block-uniform): one lane's agent-scope acquire, its wait, then the barrier
+__device__ void agent_acquire_block(bool need) {
+  if (!need) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+// a work counter other blocks raise with atomics, read without an acquire
+__device__ __forceinline__ int agent_load(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The same without the fences (each ~0.7 us on the kernel's tail, A/B r06):
 // for a last block that reads only words the other blocks stored or added with
@@ -1613,7 +1631,7 @@ __device__ void blob_grid_place(const Dev &d, int a, int *cnt) {
 __device__ bool vb_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
   if ((threadIdx.x & 63) != 0) return false;
   ArenaCtl &c = d.ctl[a];
-  int nw = min(c.n_pend, d.Wcap);
+  int nw = min(agent_load(&c.n_pend), d.Wcap);
   c.n_pend = 0;
   c.stat[0] += nw;
   int *w = d.work + (size_t)a * d.Wcap;
@@ -1885,17 +1903,28 @@ __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *sc
     if (threadIdx.x == 0) d.ctl[a].n_vir_start = d.ctl[a].n_vir;  // (splits append past it)
     blob_grid_place(d, a, g_cnt);
   }
-  if (last_block(d.ticket + 0, gridDim.x))
+  // the serial passes read the other blocks' plain stores only when they have
+  // work: the last block acquires only then (random C3: ~1 tick in 100)
+  if (last_block(d.ticket + 0, gridDim.x, false)) {
+    __shared__ int s_work;
+    if (threadIdx.x == 0) {
+      int w = 0;
+      for (int a = 0; a < d.A; a++) w |= agent_load(&d.ctl[a].n_pend) | agent_load(&d.ctl[a].n_pend2);
+      s_work = w;
+    }
+    __syncthreads();
+    agent_acquire_block(s_work != 0);
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) {
       const bool vb = vb_serial_body(d, a, scr_k, scr_v);
       if (__shfl(vb ? 1 : 0, 0)) pv_redo(d, a);
       pv_serial_body(d, a, scr_k, scr_v);
     }
+  }
 }
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
   if ((threadIdx.x & 63) != 0) return;
   ArenaCtl &c = d.ctl[a];
-  int nw = min(c.n_pend2, d.Wcap);
+  int nw = min(agent_load(&c.n_pend2), d.Wcap);
   c.n_pend2 = 0;
   c.stat[1] += nw;
   if (nw == 0) return;
@@ -2610,8 +2639,17 @@ __global__ void __launch_bounds__(256) k_food_commit(Dev d, int round, int last,
   PT_MARK(4, round < 7 ? round : 7);
   wave_atomic_max_pos(&d.ctl[min(gp, d.NP - 1) / d.B].rmax_cell, rg);
   PT_MARK(4, 5);
-  if (fold && last_block(d.ticket + 1, ncommit) && threadIdx.x < 64) {
-    for (int a = 0; a < d.A; a++) food_serial_body(d, a, scr_k, scr_v, rounds);
+  if (fold && last_block(d.ticket + 1, ncommit, false)) {  // (acquires only when a cell waits: as k_merge_pv)
+    __shared__ int s_work;
+    if (threadIdx.x == 0) {
+      int w = 0;
+      for (int a = 0; a < d.A; a++) w |= agent_load(&d.ctl[a].n_pend);
+      s_work = w;
+    }
+    __syncthreads();
+    agent_acquire_block(s_work != 0);
+    if (threadIdx.x < 64)
+      for (int a = 0; a < d.A; a++) food_serial_body(d, a, scr_k, scr_v, rounds);
     PT_MARK(4, 6);
   }
 }
@@ -2626,7 +2664,7 @@ __device__ void food_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v
   __shared__ double s_x[FS_CAP], s_y[FS_CAP], s_m[FS_CAP], s_r[FS_CAP];
   const int lane = threadIdx.x & 63;
   ArenaCtl &c = d.ctl[a];
-  const int nw = min(c.n_pend, d.Wcap);
+  const int nw = min(agent_load(&c.n_pend), d.Wcap);
   const uint32_t excl_round = c.food_round + rounds + 2;  // tiles: excluded / tainted keys (k_food_prep)
   wave_fence();
   if (lane == 0) {
