@@ -15,6 +15,7 @@
 // build against libm's pow on 10^7 inputs; tests/test_gpu_parity.py the device.
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
@@ -42,6 +43,32 @@ AIGAR_HD double mod_pos(double a, double b, double inv_b) {
     r = fma(-(q + 1), b, a);
   }
   return r == 0 ? 0.0 : r;
+}
+
+// int(x / b) for x >= 0, b > 0 (inv_b = 1 / b), exactly, without the division
+// (an fp64 divide is ~10 VALU with a transcendental rcp in its chain; the
+// observation's mask loops ran one per candidate and axis: 2.5 of k_observe's
+// 19 us in round 6).  n = the integer nearest x * inv_b is within a few ulps of
+// x / b, so int(x / b) is n or n - 1: fl(x / b) >= n iff x / b lies above the
+// midpoint between n and its predecessor, i.e. iff D = x - n * b >= -t with
+// t = b * (n - pred(n)) / 2 (exact: a power-of-two scaling of b).  fma gives
+// fl(D); rounding is monotone and -t is a double, so fl(D) > -t implies D > -t
+// and fl(D) < -t implies D < -t; fl(D) == -t (D on or next to the midpoint,
+// where ties-to-even decides) takes the division itself.  x / b < 2^31.
+// (tools/gen/check_trunc_div.cpp, tests/test_pow_host.py)
+AIGAR_HD int trunc_div_pos(double x, double b, double inv_b) {
+  const double n = rint(x * inv_b);
+  if (n <= 0.0) return 0;
+  int64_t bits;
+  memcpy(&bits, &n, sizeof bits);
+  bits -= 1;
+  double below;
+  memcpy(&below, &bits, sizeof below);
+  const double t = (n - below) * 0.5 * b;
+  const double d = fma(-n, b, x);
+  if (d > -t) return (int)n;
+  if (d < -t) return (int)n - 1;
+  return (int)(x / b);
 }
 
 // double-double helpers (aigar_trig.h)

@@ -51,7 +51,7 @@ __device__ __forceinline__ uint32_t axis_mask(double p, double r, double gs, dou
   double bl = cl - aigar_math::mod_pos(cl, gs, inv_gs);  // (cl >= 0, gs > 0)
   double lx = py_min(lim, p + r);
   uint32_t m = 0;
-  for (double x = bl; x <= lx; x += gs) m |= 1u << min(31, (int)(x / gs));
+  for (double x = bl; x <= lx; x += gs) m |= 1u << min(31, aigar_math::trunc_div_pos(x, gs, inv_gs));
   return m;
 }
 
@@ -765,6 +765,9 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   if (pint) {
     for (int t = lane; t < GG; t += 64) s_pcnt[t] = 0;
     wave_fence();
+#ifdef AIGAR_OBS_DIAG_NOPINT  // (cost diagnostics only, results invalid)
+    if (np > 0 && p_m[0] == -1.2345)
+#endif
     for (int i = lane; i < np; i += 64) {
       const uint32_t mk = p_mask[i];
       const int mi = (int)p_m[i];
@@ -922,6 +925,10 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
     }
   }
   };
+#ifdef AIGAR_OBS_DIAG_NOCV  // (cost diagnostics only, results invalid: no cell / virus scans)
+  nc = 0;
+  nv = 0;
+#endif
   const bool all_lds = in_lds && CL.mask == c_mask && VL.mask == v_mask;
   if (all_lds && (pint || np <= 64) && nc <= 64 && nv <= 64 && GG <= 128) {
     // common case: entry k of every list sits in lane k's registers and is read

@@ -32,6 +32,19 @@ def test_mod_pos_matches_python_float_mod(tmp_path):
     assert "mismatches=0" in out.stdout, out.stdout
 
 
+def test_trunc_div_pos_matches_division(tmp_path):
+    """aigar_math::trunc_div_pos (nearest integer of x * (1 / b) + an exact fma
+    residual test) == int(x / b) on the observation's mask-loop operands and next
+    to every k * b (host build; the device runs the same header)."""
+    exe = str(tmp_path / "check_trunc_div")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I",
+                           os.path.join(ROOT, "aigar_amd", "csrc"),
+                           os.path.join(ROOT, "tools", "gen", "check_trunc_div.cpp"), "-o", exe])
+    out = subprocess.run([exe, "300000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout, out.stdout
+
+
 def test_trig_is_correctly_rounded(tmp_path):
     """aigar_trig.h sin_cr / cos_cr / atan2_cr == the quad-precision value
     rounded to double on the stepper's input shapes (host build).  glibc, which
