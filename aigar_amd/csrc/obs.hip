@@ -652,13 +652,24 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   // order, so each pellet adds its mass into the squares it covers (LDS integer
   // atomics below) -- no ranking by creation sequence, no per-square scan over
   // the list.  Otherwise the reference's creation-order sums.
+  // A list in the overflow pool takes the same order-free sums (np * 65536 stays
+  // below 2^31): its creation-order scan reads the pool per square, and its
+  // ranking is quadratic -- the crowded Greedy worlds' wide views spent most of
+  // the launch there (tools/clustered.py).
   bool pint = false;
 #ifndef AIGAR_OBS_ORDERED_ONLY  // (A/B builds: the creation-order scan for every bot)
-  if (in_lds && GG <= OBS_PCAP && G <= 16) {
+  if (GG <= OBS_PCAP && G <= 16 && np <= 32767) {
     bool bad = false;
-    for (int i = lane; i < np; i += 64) {
-      const double m = p_m[i];
-      bad |= !(m >= 1.0 && m <= 65536.0 && m == floor(m));
+    if (in_lds) {
+      for (int i = lane; i < np; i += 64) {
+        const double m = p_m[i];
+        bad |= !(m >= 1.0 && m <= 65536.0 && m == floor(m));
+      }
+    } else {
+      for (int i = lane; i < np; i += 64) {
+        const double m = PL.m[i];
+        bad |= !(m >= 1.0 && m <= 65536.0 && m == floor(m));
+      }
     }
     pint = __ballot(bad) == 0;
   }
@@ -692,7 +703,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
       }
     sm = &p_sx[0].m;
     smk = &p_px[0].mask;
-  } else if (!in_lds) {
+  } else if (!in_lds && !pint) {
     for (int i = lane; i < np; i += 64) {
       int64_t sq = PL.seq[i];
       int rk = 0;
@@ -765,22 +776,28 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   if (pint) {
     for (int t = lane; t < GG; t += 64) s_pcnt[t] = 0;
     wave_fence();
+    auto scatter = [&](const uint32_t *pmk, const double *pmm) __attribute__((always_inline)) {
+      for (int i = lane; i < np; i += 64) {
+        const uint32_t mk = pmk[i];
+        const int mi = (int)pmm[i];
+        for (uint32_t X = mk & 0xFFFFu; X; X &= X - 1) {
+          const int ix = __ffs(X) - 1;
+          if (ix >= cols) break;  // (bits ascend)
+          for (uint32_t Y = mk >> 16; Y; Y &= Y - 1) {
+            const int t = (__ffs(Y) - 1) * cols + ix;
+            if (t >= GG) break;
+            const int c = sdiv(t, Mg), r = t - c * G;  // (GG <= 256 here)
+            if ((in_col >> r) & (in_row >> c) & 1) atomicAdd(&s_pcnt[t], mi);
+          }
+        }
+      }
+    };
 #ifdef AIGAR_OBS_DIAG_NOPINT  // (cost diagnostics only, results invalid)
     if (np > 0 && p_m[0] == -1.2345)
 #endif
-    for (int i = lane; i < np; i += 64) {
-      const uint32_t mk = p_mask[i];
-      const int mi = (int)p_m[i];
-      for (uint32_t X = mk & 0xFFFFu; X; X &= X - 1) {
-        const int ix = __ffs(X) - 1;
-        if (ix >= cols) break;  // (bits ascend)
-        for (uint32_t Y = mk >> 16; Y; Y &= Y - 1) {
-          const int t = (__ffs(Y) - 1) * cols + ix;
-          if (t >= GG) break;
-          const int c = sdiv(t, Mg), r = t - c * G;  // (GG <= 256 here)
-          if ((in_col >> r) & (in_row >> c) & 1) atomicAdd(&s_pcnt[t], mi);
-        }
-      }
+    {
+      if (in_lds) scatter(p_mask, p_m);  // (LDS addresses: ds_read)
+      else scatter(PL.mask, PL.m);       // (the overflow pool)
     }
     wave_fence();
   }
@@ -929,7 +946,7 @@ __global__ void __launch_bounds__(64) OBS_ATTR k_observe(Dev d, OutT *out, uint3
   nc = 0;
   nv = 0;
 #endif
-  const bool all_lds = in_lds && CL.mask == c_mask && VL.mask == v_mask;
+  const bool all_lds = (in_lds || pint) && CL.mask == c_mask && VL.mask == v_mask;  // (pint: no pellet list read)
   if (all_lds && (pint || np <= 64) && nc <= 64 && nv <= 64 && GG <= 128) {
     // common case: entry k of every list sits in lane k's registers and is read
     // with v_readlane into scalar registers (no LDS round trip per entry)

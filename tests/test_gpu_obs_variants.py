@@ -109,6 +109,48 @@ def test_wide_grid_overflow_pool_and_big_views():
     o.close()
 
 
+@pytest.mark.parametrize("converted", [False, True])
+def test_default_grid_overflow_pool(converted):
+    """k_observe at the default 11 squares with views of over a thousand pellets
+    (the lists leave LDS for the overflow pool): whole-unit pellets take the
+    order-free sums from the pool, a view holding a blob-made pellet the ranked
+    creation-order scan.  Pellet channel EXACT, the rest within 1e-5."""
+    ch = _abi.OBS_PELLET | _abi.OBS_SELF | _abi.OBS_ENEMY | _abi.OBS_WALL | _abi.OBS_SELF_LF | _abi.OBS_ENEMY_LF
+    cfg = make_config(bots=16, field_size=400, max_pellets=4000.0, channels=ch, extras=_abi.EX_FOV | _abi.EX_MASS)
+    g, o = _lib.Stepper(cfg), Oracle(cfg)
+    o.reset(41)
+    st = o.get_state()
+    cf = np.array(st["cells_f"], copy=True)
+    cf[:4, 2] = [9000.0, 4000.0, 2500.0, 1200.0]
+    cf[:4, 3] = np.sqrt(cf[:4, 2] / np.pi)
+    st["cells_f"] = cf
+    if converted:
+        pf = np.array(st["pellets_f"], copy=True)
+        sel = np.arange(len(pf)) % 7 == 0
+        pf[sel, 2] = 18 * 0.8
+        pf[sel, 3] = np.sqrt(pf[sel, 2] / np.pi)
+        st["pellets_f"] = pf
+    o.load_state(st)
+    g.load_state(st)
+    rng = np.random.default_rng(41)
+    big = 0
+    for t in range(5):
+        og, oo = g.observe(), o.observe()
+        assert np.array_equal(np.isnan(og), np.isnan(oo))
+        pg, po = np.nan_to_num(og[:, :121]), np.nan_to_num(oo[:, :121])
+        assert np.array_equal(pg, po), "tick %d: pellet channel differs (max %g)" % (t, np.abs(pg - po).max())
+        assert parity.obs_close(og, oo), "tick %d" % t
+        big += int((po.sum(axis=1) > 300).sum())  # (views over the LDS list's 256 pellets)
+        cmd = parity.synthetic_commands(rng, None, 16, 400, 0.0, 0.0)
+        g.set_commands(cmd)
+        o.set_commands(cmd)
+        g.step(1)
+        o.step(1)
+    assert big > 0
+    g.close()
+    o.close()
+
+
 def test_pellet_sums_whole_units_and_converted():
     """k_observe's pellet channel takes two paths: when every pellet a bot sees
     weighs whole units (spawns, 1-3) the sums are scattered into the squares in

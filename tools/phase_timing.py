@@ -5,7 +5,7 @@ the time from the wave's first instruction to each mark.  Runs the bench's C3
 step (matured start, graph replays) and prints mean / max per mark in us.
 
   python tools/phase_timing.py build          # here: hipcc the diagnostics .so
-  python tools/phase_timing.py run [steps] [random|greedy]   # GPU box
+  python tools/phase_timing.py run [steps] [random|greedy]   # GPU box (AIGAR_PT_START=world.npz: that start)
 """
 import ctypes as C
 import os
@@ -41,7 +41,15 @@ def run(steps, policy="random"):
     bots, field, pellets, virus, ps, pe, ch, ex, arenas = bench.WORKLOADS[name]
     stp = _lib.Stepper(bench.make_cfg(name, device=0, arenas=arenas))
     obs = torch.empty((bots, stp.obs_len), dtype=torch.float64, device="cuda")
-    print(bench.start_world(stp, name, 1234, arenas))
+    start = os.environ.get("AIGAR_PT_START")  # (a saved world instead, e.g. data/c3_greedy_late.npz)
+    if start:
+        import numpy as np
+        z = np.load(start)
+        stp.reset(1234)
+        stp.load_state({k: z[k] for k in z.files}, 0)
+        print(start)
+    else:
+        print(bench.start_world(stp, name, 1234, arenas))
     stp.run(20, policy, obs, p_split=ps, p_eject=pe, seed=1234, greedy_split=True)
     stp.sync()
     import numpy as np
