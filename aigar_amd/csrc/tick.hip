@@ -685,6 +685,205 @@ __device__ __forceinline__ void update_player(const Dev &d, int gp, const Player
   nb_out = nb;
 }
 
+// lane k's double / int, k wave-uniform
+__device__ __forceinline__ double lane_d(double v, int k) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, k), hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int lane_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+// update_player for a player that has more than kTailRegs cells after its split,
+// on one wavefront (k_players' helper waves): lane k holds list row k's cell in
+// registers, so the phases run without the memory version's reload per cell and
+// pair (a 16-cell player's handlePlayerCollisions was 256 dependent pairs of
+// global loads -- ~270 us per crowded Greedy tick, profiles/r06_clustered.txt).
+// The same phases in the same order as update_player:
+//  * Player.split: the stable sort by mass (descending) as a rank per lane, the
+//    snapshot's qualifying cells in sorted order take the lowest free slots;
+//  * the eject flags, updateCellsMovement (independent per cell);
+//  * performEjections in list order (a ballot prefix numbers the blobs);
+//  * handlePlayerCollisions: for each i in list order, the lanes j test the pair
+//    (i, j) together and the first hit at or after the last one is adjusted --
+//    an adjustment moves only i and j, so the later pairs of the same i need
+//    only i's new position: the serial loop's outcome exactly.
+// Results: the cells (flags final), the list and count, the blob staging rows;
+// the list also into LDS (hl, hn: the seq pass numbers the new cells from it).
+// cnt = pn | pb << 8: the predicted counts, checked (ERR_PREDICT).
+__device__ void player_wave(const Dev &d, int a, int gp, double cpx, double cpy, bool split, bool eject, int cnt,
+                            uint8_t *hl, uint8_t *hn) {
+  const int lane = threadIdx.x & 63, NP = d.NP;
+  const unsigned long long lt = (1ull << lane) - 1;
+  const double W = (double)d.size;
+  const int n0 = uni(d.p_ncells[gp]);
+  int slot = 0, svc = 0;
+  uint32_t fl = 0;
+  double x = 0, y = 0, vx = 0, vy = 0, svx = 0, svy = 0, m = 0, r = 0, mt = 0, spr = 0, spsvx = 0, spsvy = 0;
+  if (lane < n0) {
+    slot = d.p_list[lane * NP + gp];
+    const size_t ci = (size_t)slot * NP + gp;
+    x = d.c_x[ci];
+    y = d.c_y[ci];
+    vx = d.c_vx[ci];
+    vy = d.c_vy[ci];
+    svx = d.c_svx[ci];
+    svy = d.c_svy[ci];
+    m = d.c_m[ci];
+    r = d.c_r[ci];
+    mt = d.c_mt[ci];
+    svc = d.c_svc[ci];
+    fl = d.c_flags[ci];
+    if (split) {  // (update_cell's split geometry; read only for the cells that split)
+      spr = d.sp_r[ci];
+      spsvx = d.sp_svx[ci];
+      spsvy = d.sp_svy[ci];
+    }
+  }
+  int n = n0, n_new = 0;
+  bool touched = false;  // mass / radius / fresh fields changed (stored below)
+  if (split) {  // Player.split (player.py:46-52)
+    int rk = 0;
+    for (int j = 0; j < n0; j++) {
+      const double mj = lane_d(m, j);
+      rk += (mj > m || (mj == m && j < lane)) ? 1 : 0;
+    }
+    int src = lane;
+    for (int k = 0; k < n0; k++)
+      if (lane_i(rk, k) == lane) src = k;
+    slot = __shfl(slot, src);
+    x = __shfl(x, src);
+    y = __shfl(y, src);
+    vx = __shfl(vx, src);
+    vy = __shfl(vy, src);
+    svx = __shfl(svx, src);
+    svy = __shfl(svy, src);
+    m = __shfl(m, src);
+    r = __shfl(r, src);
+    mt = __shfl(mt, src);
+    svc = __shfl(svc, src);
+    fl = (uint32_t)__shfl((int)fl, src);
+    spr = __shfl(spr, src);
+    spsvx = __shfl(spsvx, src);
+    spsvy = __shfl(spsvy, src);
+    uint32_t used = 0;
+    for (int j = 0; j < n0; j++) used |= 1u << lane_i(slot, j);
+    const unsigned long long qb = __ballot(lane < n0 && m > 36);
+    n_new = min(__popcll(qb), kMaxCells - n0);
+    // new cell t (lane n0 + t): the t-th qualifying cell's other half, the t-th free slot
+    int par = lane;
+    uint32_t u = used;
+    for (int t = 0; t < n_new; t++) {
+      const int s = __ffs(~u) - 1;
+      u |= 1u << s;
+      if (lane == n0 + t) slot = s;
+    }
+    for (int k = 0; k < n0; k++) {
+      if (!((qb >> k) & 1)) continue;
+      const int t = __popcll(qb & ((1ull << k) - 1));
+      if (t < n_new && lane == n0 + t) par = k;
+    }
+    const double px = __shfl(x, par), py = __shfl(y, par), pm = __shfl(m, par);
+    const double pr = __shfl(spr, par), psx = __shfl(spsvx, par), psy = __shfl(spsvy, par);
+    const bool is_par = ((qb >> lane) & 1) && __popcll(qb & lt) < n_new;
+    const bool is_new = lane >= n0 && lane < n0 + n_new;
+    if (is_par) {  // Cell.split: the parent keeps the other half (same mass and radius)
+      m = m / 2;
+      r = spr;
+    }
+    if (is_new) {
+      x = px;
+      y = py;
+      m = pm / 2;
+      r = pr;
+      vx = vy = 0;
+      svx = psx;
+      svy = psy;
+      svc = 15;
+      mt = merge_time_for(1, m);
+      fl = F_ALIVE | F_NEW;
+    }
+    touched = is_par || is_new;
+    n = n0 + n_new;
+  }
+  const bool fresh = lane >= n0 && lane < n;
+  if (eject && lane < n && m >= 35) fl |= F_EJECT;  // Player.eject (player.py:54-58)
+  const bool ej = lane < n && (fl & F_EJECT);
+  if (lane < n) update_pos(x, y, vx, vy, svx, svy, svc, W, W);  // updateCellsMovement
+  const unsigned long long eb = __ballot(ej);  // performEjections (field.py:134-146), list order
+  if (ej) {
+    m = m - kEjectMass;  // Cell.eject: radius stays stale (cell.py:90-94)
+    double bsvx, bsvy;
+    int bsvc;
+    add_momentum(x, y, cpx, cpy, W, W, r, bsvx, bsvy, bsvc);
+    const size_t si = (size_t)__popcll(eb & lt) * NP + gp;
+    d.sb_x[si] = x;
+    d.sb_y[si] = y;
+    d.sb_svx[si] = bsvx;
+    d.sb_svy[si] = bsvy;
+    d.sb_slot[si] = (uint8_t)slot;
+  }
+  const int nb = __popcll(eb);
+  for (int i = 0; i < n; i++) {  // handlePlayerCollisions (field.py:149-159)
+    if (lane_i(svc, i) > 0) continue;
+    const double mti = lane_d(mt, i), mi = lane_d(m, i), ri = lane_d(r, i);
+    const bool cand = lane < n && lane != i && svc <= 0 && !(mti <= 0 && mt <= 0);
+    int j0 = 0;
+    for (;;) {
+      const double xi = lane_d(x, i), yi = lane_d(y, i);
+      double dist = 0, sr = 0;
+      bool hit = false;
+      if (cand && lane >= j0) {
+        dist = sqrt((xi - x) * (xi - x) + (yi - y) * (yi - y));
+        sr = ri + r;
+        hit = dist < sr && dist != 0;
+      }
+      const unsigned long long hb = __ballot(hit);
+      if (!hb) break;
+      const int j = __ffsll((long long)hb) - 1;
+      double bx = xi, by = yi, sx = lane_d(x, j), sy = lane_d(y, j);
+      const double mj = lane_d(m, j), dj = lane_d(dist, j), sj = lane_d(sr, j);
+      if (mi > mj) {  // adjustCellPositions (field.py:161-181), the bigger first
+        adjust_pair(bx, by, mi, sx, sy, mj, dj, sj, W);
+      } else {
+        adjust_pair(sx, sy, mj, bx, by, mi, dj, sj, W);
+      }
+      if (lane == i) {
+        x = bx;
+        y = by;
+      }
+      if (lane == j) {
+        x = sx;
+        y = sy;
+      }
+      j0 = j + 1;
+    }
+  }
+  if (lane < n) {
+    const size_t ci = (size_t)slot * NP + gp;
+    d.c_x[ci] = x;
+    d.c_y[ci] = y;
+    d.c_svx[ci] = svx;
+    d.c_svy[ci] = svy;
+    if (ej || touched) d.c_m[ci] = m;
+    if (touched) d.c_r[ci] = r;
+    if (fresh) {
+      d.c_vx[ci] = 0;
+      d.c_vy[ci] = 0;
+      d.c_svc[ci] = svc;
+      d.c_mt[ci] = mt;
+    }
+    // the flags as k_players leaves them (player_tail_regs)
+    d.c_flags[ci] = (fl & ~(F_EJECT | F_NEW)) | F_INHASH;
+    d.p_list[lane * NP + gp] = (uint8_t)slot;
+    hl[lane] = (uint8_t)slot;
+  }
+  if (lane == 0) {
+    d.p_ncells[gp] = n;
+    *hn = (uint8_t)n;
+    if (n_new != (cnt & 0xFF) || nb != (cnt >> 8)) set_err(d, a, ERR_PREDICT);
+  }
+}
+
 // updateViruses + updateBlobs + the per-cell part of updatePlayers in one
 // launch: thread ranges [cell slots | viruses | blobs] (independent, field.py:94-119)
 // the first kSpawnAhead pellet spawns of this tick, drawn now: their counter
@@ -916,6 +1115,10 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   __shared__ double s_cx[256], s_cy[256];
   __shared__ uint8_t s_csp[256];
   __shared__ uint16_t s_q[256 * (kMaxCells - 1)];  // the tile's queued cells: local player << 4 | slot
+  // players of more than kTailRegs cells after the split: queued for the helper
+  // waves (player_wave); entry = local player | predicted counts << 8
+  __shared__ int s_nh, s_hq[256];
+  __shared__ uint8_t s_cej[256], s_hn[256], s_hl[256][kMaxCells];
   PT_BEGIN(1);
 #ifdef AIGAR_PHASE_TIMING  // (the cell phase and the extra blocks mark under slot 2)
   if ((threadIdx.x & 63) == 0 && pt_w_ < kPtWaves) g_ptw[2][pt_w_][0] = (unsigned)pt0_;
@@ -970,7 +1173,7 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   CellIn own{};
   size_t own_ci = 0;
   bool own_ok = false;
-  if (tid == 0) s_nq = 0;
+  if (tid == 0) s_nq = s_nh = 0;
   if (tid < 256) s_heavy[tid] = 0;
   __syncthreads();
   if (tid < 256 && p < d.B) {
@@ -994,6 +1197,7 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
       s_cx[tid] = ph.cpx;
       s_cy[tid] = ph.cpy;
       s_csp[tid] = ph.split ? 1 : 0;
+      s_cej[tid] = ph.eject ? 1 : 0;
       if (ph.n > 1) {
         const int q = atomicAdd(&s_nq, ph.n - 1);
         for (int k = 1; k < ph.n; k++)
@@ -1014,9 +1218,16 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   }
   __syncthreads();
   PT_MARK(2, 2);
-  if (tid >= 256) {  // (the helpers join the player part's three barriers and the last-block ticket only)
+  if (tid >= 256) {  // (the helpers join the player part's three barriers and the last-block ticket)
     __syncthreads();
     __syncthreads();
+    // the queued many-cell players, one per helper wave, beside the player
+    // threads' chains and look-back (their results are read after the third barrier)
+    for (int h = (tid - 256) >> 6; h < s_nh; h += (kPlT - 256) / 64) {
+      const int e = s_hq[h], lp = e & 0xFF;
+      player_wave(d, a, a * d.B + tile * 256 + lp, s_cx[lp], s_cy[lp], s_csp[lp] != 0, s_cej[lp] != 0, e >> 8,
+                  s_hl[h], &s_hn[h]);
+    }
     __syncthreads();
     finish();
     return;
@@ -1036,6 +1247,11 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   // them finds every predecessor's aggregate instead of waiting for the slowest tile
   int pn = 0, pb = 0;
   if (p < d.B && ph.alive) predicted_counts(s_heavy[tid], ph.n, ph.split, ph.eject, pn, pb);
+  int hslot = -1;  // (queued for a helper wave: its list in s_hl[hslot])
+  if (p < d.B && ph.alive && ph.n + pn > kTailRegs) {
+    hslot = atomicAdd(&s_nh, 1);
+    s_hq[hslot] = tid | pn << 8 | pb << 16;
+  }
   const int vs = pn + pb, vb = pb;
   int is = vs, ib = vb;
 #pragma unroll
@@ -1077,7 +1293,10 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   int nn = 0, nb = 0, fn = 0;
   bool fast = false;
   uint8_t flst[kTailRegs];
-  if (p < d.B) {
+  if (hslot >= 0) {  // (player_wave checks its counts)
+    nn = pn;
+    nb = pb;
+  } else if (p < d.B) {
     update_player(d, gp, ph, nn, nb, fast, flst, fn PT_ARGS);  // (its counts from registers, not re-loaded)
     if (nn != pn || nb != pb) set_err(d, a, ERR_PREDICT);
   }
@@ -1133,10 +1352,13 @@ __global__ void __launch_bounds__(512) k_players(Dev d, RandomPolicy rp) {
   }
   // the seq pass: a register-tail player's flags are final already and its list
   // is in flst (fn cells): only its new cells (the last nn) are numbered here
-  if (p < d.B && (fast ? nb > 0 || nn > 0 : d.p_alive[gp] != 0)) {
+  if (p < d.B && (fast || hslot >= 0 ? nb > 0 || nn > 0 : d.p_alive[gp] != 0)) {
     const int64_t s0 = seq0 + s_ps + ws[w] + (is - vs);
     const int boff = s_pb + wb[w] + (ib - vb);
-    if (fast) {
+    if (hslot >= 0) {  // (player_wave: flags final, the list in LDS)
+      const int n = s_hn[hslot];
+      for (int k = n - nn; k < n; k++) d.c_seq[(size_t)s_hl[hslot][k] * NP + gp] = s0 + (k - (n - nn));
+    } else if (fast) {
 #pragma unroll
       for (int k = 0; k < kTailRegs; k++)
         if (k >= fn - nn && k < fn) d.c_seq[(size_t)flst[k] * NP + gp] = s0 + (k - (fn - nn));
