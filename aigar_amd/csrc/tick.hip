@@ -3436,16 +3436,39 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
     const int s_first = d.p_list[gp];
     const int n_first = d.p_ncells[gp];
     if (!d.p_alive[gp]) continue;
-    for (int i = 0;;) {  // for playerCell in player.getCells(): live list
-      if (i >= (i == 0 ? n_first : d.p_ncells[gp])) break;
-      const size_t pc = (size_t)(i == 0 ? s_first : d.p_list[i * NP + gp]) * NP + gp;
-      i++;
-      // the turn cell's state rides the activity load (nothing changes it before
-      // its eat loop: the candidate walk only reads)
-      const double px = d.c_x[pc], py = d.c_y[pc];
-      const int64_t pseq = d.c_seq[pc];
-      double pm = d.c_m[pc], pr = d.c_r[pc];
-      if (!active_ld(d, pc)) continue;
+    // every cell of the turn, one lane each (lane = the row at the turn's start):
+    // its list row, then its state and activity in one round (two rounds per turn,
+    // not two per cell).  A turn cell eats only other players' cells, and the
+    // re-activation after its eat skips the eater's owner, so the player's own
+    // cells and activity change only when the turn cell is eaten: the list then
+    // closes up (the cell that moves into its row is skipped, player.py:97 -- the
+    // next lane but one), and the eater's re-activation may wake own cells (their
+    // activity is loaded again).
+    const int kslot = lane == 0 ? s_first : (lane < n_first ? (int)d.p_list[lane * NP + gp] : 0);
+    double kx = 0, ky = 0, km = 0, kr = 0;
+    int64_t kseq = 0;
+    bool kact = false;
+    if (lane < n_first) {
+      const size_t kc = (size_t)kslot * NP + gp;
+      kx = d.c_x[kc];
+      ky = d.c_y[kc];
+      kseq = d.c_seq[kc];
+      km = d.c_m[kc];
+      kr = d.c_r[kc];
+      kact = active_ld(d, kc) != 0;
+    }
+    unsigned long long amask = __ballot(kact);
+    int nrem = 0;  // own cells removed this turn (rows closed up)
+    for (int kn = 0;;) {  // for playerCell in player.getCells(): live list (its active cells)
+      const unsigned long long rest = kn < 64 ? amask & (~0ull << kn) : 0;
+      if (!rest) break;
+      const int kl = __ffsll((long long)rest) - 1;
+      kn = kl + 1;
+      const int i = kl - nrem + 1;  // (the list row after pc's, as the reference's loop counts)
+      const size_t pc = (size_t)lane_i(kslot, kl) * NP + gp;
+      const double px = lane_d(kx, kl), py = lane_d(ky, kl);
+      const int64_t pseq = (int64_t)__double_as_longlong(lane_d(__longlong_as_double(kseq), kl));
+      double pm = lane_d(km, kl), pr = lane_d(kr, kl);
       active_st(d, pc, 0);
       const Rect q0 = footprint(px, py, pr, d.size);  // (cell_rect)
       PA_T(1);
@@ -3560,6 +3583,10 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
           }
           PA_T(6);
           PA_C(3);
+          nrem++;
+          kn = kl + 2;  // (the skipped row's cell)
+          bool re = lane >= kn && lane < n_first && active_ld(d, (size_t)kslot * NP + gp) != 0;
+          amask = __ballot(re);
           break;
         }
       }
