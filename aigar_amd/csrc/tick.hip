@@ -2113,7 +2113,9 @@ __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *sc
     const int gi = GTID;
     double rg = 0;
     if (gi < d.NP) {
+#ifndef AIGAR_DIAG_NO_MERGE  // (cost diagnostics only, results invalid)
       merge_player(d, gi);
+#endif
       rg = pv_player(d, gi);
     }
     // the player-cell grid's radius bound (pre-eat radii; eaters report their growth)
@@ -2139,7 +2141,9 @@ __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *sc
     for (int a = threadIdx.x >> 6; a < d.A; a += blockDim.x >> 6) {
       const bool vb = vb_serial_body(d, a, scr_k, scr_v);
       if (__shfl(vb ? 1 : 0, 0)) pv_redo(d, a);
+#ifndef AIGAR_DIAG_NO_PV_SERIAL  // (cost diagnostics only, results invalid)
       pv_serial_body(d, a, scr_k, scr_v);
+#endif
     }
   }
 }
@@ -3433,7 +3437,8 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
     uint64_t order = (uint64_t)P << 32;  // this turn's event / death keys
     PA_C(0);
     // liveness, count and the list's first row in one load round
-    const int s_first = d.p_list[gp];
+    // (the list's rows ride the same round: all kMaxCells rows exist)
+    const int kslot = lane < kMaxCells ? (int)d.p_list[lane * NP + gp] : 0;
     const int n_first = d.p_ncells[gp];
     if (!d.p_alive[gp]) continue;
     // every cell of the turn, one lane each (lane = the row at the turn's start):
@@ -3444,7 +3449,6 @@ __device__ __forceinline__ void pp_turns(const Dev &d, int a, uint32_t *pend, co
     // closes up (the cell that moves into its row is skipped, player.py:97 -- the
     // next lane but one), and the eater's re-activation may wake own cells (their
     // activity is loaded again).
-    const int kslot = lane == 0 ? s_first : (lane < n_first ? (int)d.p_list[lane * NP + gp] : 0);
     double kx = 0, ky = 0, km = 0, kr = 0;
     int64_t kseq = 0;
     bool kact = false;
