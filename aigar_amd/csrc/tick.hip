@@ -2147,12 +2147,21 @@ __global__ void __launch_bounds__(256) k_merge_pv(Dev d, int64_t *scr_k, int *sc
     }
   }
 }
+// playerVirusOverlap's serial pass, one wavefront per arena: every lane runs
+// the same serial code (the same loads and plain stores, in program order, as
+// pp_turns), the atomics and the event log on lane 0, and each active cell's
+// virus candidates are gathered by the lanes together (wave_grid_for; the list
+// is then sorted by creation sequence as before, so its order is the same)
 __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) {
-  if ((threadIdx.x & 63) != 0) return;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1;
   ArenaCtl &c = d.ctl[a];
   int nw = min(agent_load(&c.n_pend2), d.Wcap);
-  c.n_pend2 = 0;
-  c.stat[1] += nw;
+  wave_fence();
+  if (lane == 0) {
+    c.n_pend2 = 0;
+    c.stat[1] += nw;
+  }
   if (nw == 0) return;
   const int NP = d.NP;
   int *w = d.work2 + (size_t)a * d.Wcap;
@@ -2174,16 +2183,25 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
       int E = expand_for(c.rmax_virus);
       Rect q = footprint(d.c_x[ci], d.c_y[ci], d.c_r[ci], d.size);
       int nc = 0;
-      grid_visit(st, it, d.cols, q, E, [&](int j) {
-        size_t g = (size_t)a * d.Vcap + j;
-        if ((d.v_flags[g] & (F_ALIVE | F_INHASH)) != (F_ALIVE | F_INHASH)) return;
-        if (!rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q)) return;
-        if (nc < d.Wcap) {
-          ck[nc] = d.v_seq[g];
-          cv[nc] = j;
-          nc++;
+      wave_grid_for(st, it, d.cols, q, E, [&](bool valid, int j) {
+        bool keep = false;
+        int64_t sq = 0;
+        if (valid) {
+          const size_t g = (size_t)a * d.Vcap + j;
+          keep = (d.v_flags[g] & (F_ALIVE | F_INHASH)) == (F_ALIVE | F_INHASH) &&
+                 rect_hit(footprint(d.v_x[g], d.v_y[g], d.v_r[g], d.size), q);
+          if (keep) sq = d.v_seq[g];
         }
+        const unsigned long long bal = __ballot(keep);
+        const int slot = nc + __popcll(bal & lt);
+        if (keep && slot < d.Wcap) {
+          ck[slot] = sq;
+          cv[slot] = j;
+        }
+        nc += __popcll(bal);
       }, d.cshift);
+      nc = min(nc, d.Wcap);
+      wave_fence();  // (the lanes' candidates -> every lane's sort)
       isort_kv(ck, cv, nc);
       for (int t = 0; t < nc; t++) {
         size_t g = (size_t)a * d.Vcap + cv[t];
@@ -2193,17 +2211,21 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
               cm > 1.25 * d.v_m[g]))
           continue;
         // eatVirus -> eatCell(..., isVirus=True) (field.py:333-344)
-        ev_push(d, a, PH_PV, order++, 4, d.c_seq[ci], d.v_seq[g]);
+        if (lane == 0) ev_push(d, a, PH_PV, order, 4, d.c_seq[ci], d.v_seq[g]);
+        order++;
         double m = grow_mass(cm, d.v_m[g] * kVirusEatFactor);
         d.c_m[ci] = m;
         d.c_r[ci] = radius_of(m);
-        atomic_max_pos(&c.rmax_cell, d.c_r[ci]);  // (the player-cell grid's radius bound)
+        if (lane == 0) {
+          atomic_max_pos(&c.rmax_cell, d.c_r[ci]);  // (the player-cell grid's radius bound)
+          atomicOr(&d.ctl[a].dirty, DIRTY_VIRUS);
+        }
         d.v_flags[g] = 0;
-        atomicOr(&d.ctl[a].dirty, DIRTY_VIRUS);
         // playerCellAteVirus (field.py:350-370)
         int ncur = d.p_ncells[gp];
         int n_new = kMaxCells - ncur;
-        ev_push(d, a, PH_PV, order++, 5, d.c_seq[ci], n_new);
+        if (lane == 0) ev_push(d, a, PH_PV, order, 5, d.c_seq[ci], n_new);
+        order++;
         if (n_new == 0) continue;
         double dist = d.c_m[ci] * kExplosionProp;
         double mpc = dist / n_new;
@@ -2244,7 +2266,7 @@ __device__ void pv_serial_body(const Dev &d, int a, int64_t *scr_k, int *scr_v) 
           d.c_seq[ni] = seq;
           d.c_flags[ni] = F_ALIVE | F_INHASH | F_NEW;  // addPlayerCell hashes it
           d.c_active[ni] = 0;
-          cgrid_count_cell(d, a, ni, px, py);  // (step 1 of the player-cell grid)
+          if (lane == 0) cgrid_count_cell(d, a, ni, px, py);  // (step 1 of the player-cell grid)
           d.p_list[(ncur + k) * NP + gp] = (uint8_t)slot;
         }
         d.p_ncells[gp] = ncur + n_new;
